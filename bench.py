@@ -1,0 +1,219 @@
+"""Headline benchmark: C2 = one stream of 1e9 int64 keys per GPU, k = 1024, Algorithm R (philox_r).
+
+A step is one full pass of the hot path over the batch: a fresh Sampler (Sampler.apply) samples
+the device-resident keys (K1 last-writer kernel + resolve), then result() brings the k-slot
+reservoir to the host.  With N GPUs the stream is N x 1e9 elements split by index range (each
+rank seeks to its offset, weak scaling) and the per-rank reservoirs are combined with one RCCL
+all_gather + merge kernel inside the step.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+  roofline      -- K1's average launch time, measured with HIP events on the sampler's stream
+  cpu_baseline  -- the oracle's C restatement of the reference (Algorithm L) on one host core
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import mmap
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "elements sampled/sec (Gelem/s) + % HBM roofline, 1B Long keys k=1024, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BYTES_PER_ELEM = 8     # each 64-bit key charged once
+
+
+def splitmix_fill(out: torch.Tensor, base: int, chunk: int = 1 << 27) -> None:
+    """key[i] = splitmix64(0x5EED0000 + i), generated on the device."""
+    def s64(c):
+        return c - (1 << 64) if c >= 1 << 63 else c
+
+    g, m1, m2 = s64(0x9E3779B97F4A7C15), s64(0xBF58476D1CE4E5B9), s64(0x94D049BB133111EB)
+    n = out.numel()
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        z = torch.arange(base + a, base + b, dtype=torch.int64, device=out.device) + g
+        z = (z ^ ((z >> 30) & ((1 << 34) - 1))) * m1
+        z = (z ^ ((z >> 27) & ((1 << 37) - 1))) * m2
+        out[a:b] = z ^ ((z >> 31) & ((1 << 33) - 1))
+
+
+def cpu_baseline(k: int, n_stream: int, seed: int) -> dict:
+    """Time the oracle (C restatement of Sampler.scala) on one host core, bounded to ~10 s."""
+    from oracle import oracle as O
+
+    L = O.lib()
+    buf_n = 20_000_000
+    keys = O.splitmix_keys(0x5EED0000, buf_n)
+    out = np.zeros(k, dtype=np.int64)
+    t = L.or_time_algo_l_per_element(k, seed, keys, buf_n, 1, out.ctypes.data_as(C.c_void_p))
+    reps = max(1, min(int(n_stream // buf_n), int(8.0 / max(t, 1e-3))))
+    t = L.or_time_algo_l_per_element(k, seed, keys, buf_n, reps, out.ctypes.data_as(C.c_void_p))
+    per_elem = reps * buf_n / t / 1e9
+    # sampleAll(IndexedSeq) skip path over the full stream: an untouched zero-page mapping stands in
+    # for the 8 GB array (the path reads only ~k ln(n/k) elements)
+    zbuf = mmap.mmap(-1, n_stream * 8)
+    addr = C.addressof(C.c_char.from_buffer(zbuf))
+    ts = L.or_time_algo_l_indexed(k, seed, C.c_void_p(addr), n_stream, out.ctypes.data_as(C.c_void_p))
+    del addr
+    zbuf.close()
+    return {
+        "value": round(per_elem, 4),
+        "unit": "Gelem/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"per-element sample() (Algorithm L, Sampler.scala:248-259) over one stream of "
+                  f"{reps * buf_n:.3g} keys (a {buf_n:.0e}-key C2 prefix replayed {reps}x), k={k}",
+        "skip_path": {"value": round(n_stream / ts / 1e9, 2), "unit": "Gelem/s",
+                      "sample": f"sampleAll(IndexedSeq) skip path (Sampler.scala:261-273) over "
+                                f"{n_stream:.0e} elements; touches ~k ln(n/k) of them"},
+    }
+
+
+def load_traffic(n: int):
+    """HBM bytes per K1 launch from the committed PMC pass (profiles/), if one matches n."""
+    path = os.path.join(ROOT, "profiles", "pmc_k1.json")
+    try:
+        d = json.load(open(path))
+        if int(d.get("n", -1)) == n:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1_000_000_000, help="keys per GPU")
+    ap.add_argument("--k", type=int, default=1024)
+    ap.add_argument("--seed", type=int, default=0xC0FFEE)
+    ap.add_argument("--stream-id", type=int, default=0x5A5A)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from reservoir_amd import Sampler, _native
+    from reservoir_amd import distributed as D
+
+    n, k = args.n, args.k
+    offset = rank * n
+    keys = torch.empty(n, dtype=torch.int64, device=dev)
+    splitmix_fill(keys, 0x5EED0000 + offset)
+    stream = torch.cuda.current_stream(dev)
+
+    def make():
+        s = Sampler(k, seed=args.seed, stream_id=args.stream_id, device=local)()
+        s.set_stream(stream.cuda_stream)
+        return s
+
+    samplers = [make() for _ in range(args.warmup + args.steps)]
+    L = _native.load()
+    for s in samplers[args.warmup:]:
+        N_ok = L.rsv_profile_enable(s.handle, 1)
+        _native.check(N_ok)
+
+    def step(s):
+        s.seek(offset)
+        s.sample_all(keys)
+        if world > 1:
+            D.combine(s, device=dev)
+        return s.result()
+
+    for s in samplers[: args.warmup]:
+        step(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = None
+    for s in samplers[args.warmup:]:
+        res = step(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # K1 launch time (HIP events on the launch stream), averaged over the timed steps
+    tot_ms, launches = 0.0, 0
+    for s in samplers[args.warmup:]:
+        ms, cnt = C.c_double(), C.c_int64()
+        _native.check(L.rsv_profile_read(s.handle, C.byref(ms), C.byref(cnt)))
+        tot_ms += ms.value
+        launches += cnt.value
+    k1_s = tot_ms / max(launches, 1) / 1e3
+    assert res is not None and res.size == k
+
+    if rank == 0:
+        total = n * world * args.steps
+        achieved = BYTES_PER_ELEM * n / k1_s / 1e9
+        line = {
+            "metric": METRIC,
+            "value": round(total / elapsed / 1e9, 3),
+            "unit": "Gelem/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic",
+            "config": {
+                "workload": "C2: single stream, 1e9 int64 keys per GPU (splitmix64), k=1024, "
+                            "Algorithm R last-writer (engine philox_r); step = fresh Sampler, "
+                            "sampleAll over device-resident keys, result() to host",
+                "keys_per_gpu": n, "k": k, "stream_elements": n * world,
+                "parallelism": f"index-range split over {world} GPU(s), RCCL all_gather combine"
+                               if world > 1 else "single GPU",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": load_traffic(n),
+                "kernel": "k1_last_writer",
+                "launch_avg_us": round(k1_s * 1e6, 2),
+                "note": "achieved charges 8 B per element (SURVEY.md 8(d)); K1 reads no key "
+                        "(draws depend only on the index), so it is bound by Philox integer "
+                        "VALU work, not HBM -- see DESIGN.md Roofline",
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(k, n, args.seed)
+        print(json.dumps(line), flush=True)
+    for s in samplers:
+        s.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,169 @@
+/*
+ * reservoir_hip.h -- C ABI of libreservoir_hip.so, the MI355X (gfx950) reservoir-sampling engine.
+ *
+ * This is the drop-in boundary behind the lgbt.princess.reservoir API.  Every entry point names
+ * the reference interface it replaces (paths relative to NthPortal/reservoir):
+ *   S  = core/src/main/scala/lgbt/princess/reservoir/Sampler.scala
+ *   SI = akka-stream/src/main/scala/lgbt/princess/reservoir/akkasupport/SampleImpl.scala
+ * A Scala binding (Panama FFM downcalls or JNI) is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - plain C: no C++ or torch types; opaque handle; every call returns rsv_status.
+ *   - keys are primitive fixed-width values (Int -> key_width 4, Long -> key_width 8) that the
+ *     host extracted with the sampler's `map` (S:115-116: map may be called more than k times).
+ *   - "device" pointers are HIP device pointers on the handle's device; "host" pointers are
+ *     ordinary (pageable or pinned) memory.  The caller owns every buffer it passes in.
+ *   - one handle is single-threaded (S:18-19); distinct handles are independent.
+ *   - errors: rsv_last_error() returns a thread-local message for the last failing call.
+ */
+#ifndef RESERVOIR_HIP_H
+#define RESERVOIR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSV_ABI_VERSION 1
+
+/* Status codes; a JVM binding maps them 1:1 onto the reference's exceptions. */
+typedef enum rsv_status {
+    RSV_OK = 0,
+    RSV_E_ILLEGAL_ARGUMENT = 1, /* IllegalArgumentException: k <= 0 or k > Int.MaxValue-2 (S:80-81) */
+    RSV_E_ILLEGAL_STATE = 2,    /* IllegalStateException "use of sampler after calling `result()`" (S:186) */
+    RSV_E_NULL_POINTER = 3,     /* NullPointerException: a required pointer is NULL (S:82, S:94) */
+    RSV_E_DEVICE = 4,           /* HIP runtime / kernel failure -> RuntimeException (fails the akka Future, SI:43-46) */
+    RSV_E_OUT_OF_MEMORY = 5,    /* device or pinned allocation failed -> OutOfMemoryError */
+    RSV_E_UNSUPPORTED = 6       /* valid request this build does not implement (message says which) */
+} rsv_status;
+
+typedef enum rsv_kind {
+    RSV_KIND_ELEMENTS = 0, /* Sampler.apply   (S:128-136): equal-probability sample, duplicates kept */
+    RSV_KIND_DISTINCT = 1  /* Sampler.distinct (S:171-180): bottom-k over the scrambled hash     */
+} rsv_kind;
+
+typedef enum rsv_engine {
+    /* Algorithm R, data-parallel: element i >= k replaces slot j_i = floor(U_i (i+1) / 2^64) when
+     * j_i < k, U_i a counter-based Philox4x32-10 draw of (seed, stream_id, i) (draw
+     * format R1).  Bit-identical for any batching and any index-range split over GPUs. */
+    RSV_ENGINE_PHILOX_R = 0,
+    /* The reference's own Algorithm L (S:224-246) driven by java.util.Random(seed), exactly as
+     * SamplerTest.useConsistentRandom seeds it; the eviction events are replayed on the GPU.
+     * Bit-identical to the reference Sampler for the same seed. */
+    RSV_ENGINE_JAVA_L = 1
+} rsv_engine;
+
+typedef enum rsv_hash_kind {
+    RSV_HASH_DEFAULT = 0,     /* B#hashCode().toLong (S:75): JAVA_INT for key_width 4, JAVA_LONG for 8 */
+    RSV_HASH_IDENTITY = 1,    /* hash = key as a signed Long (a bijection: bit-exact distinct sets) */
+    RSV_HASH_JAVA_LONG = 2,   /* java.lang.Long.hashCode: (int)(v ^ v>>>32), sign-extended */
+    RSV_HASH_JAVA_INT = 3,    /* java.lang.Integer.hashCode: v, sign-extended */
+    RSV_HASH_PRECOMPUTED = 4  /* caller passes int64 hashes beside the keys (arbitrary JVM `hash`) */
+} rsv_hash_kind;
+
+typedef enum rsv_mem { RSV_MEM_HOST = 0, RSV_MEM_DEVICE = 1 } rsv_mem;
+
+typedef struct rsv_config {
+    uint32_t struct_size;     /* = sizeof(rsv_config) */
+    int32_t  kind;            /* rsv_kind */
+    int32_t  max_sample_size; /* k: S:130 maxSampleSize / S:173 */
+    int32_t  key_width;       /* 4 (Int) or 8 (Long) */
+    int32_t  reusable;        /* S:130/S:173 reusable: result() may be called repeatedly (S:353-381, S:430-433) */
+    int32_t  pre_allocate;    /* S:130 preAllocate: accepted; device slots are always preallocated */
+    int32_t  engine;          /* rsv_engine (ELEMENTS only) */
+    int32_t  hash_kind;       /* rsv_hash_kind (DISTINCT only) */
+    int32_t  device;          /* HIP device ordinal; -1 = the calling thread's current device */
+    int32_t  reserved0;
+    uint64_t seed;            /* PHILOX_R: Philox key; JAVA_L / DISTINCT: java.util.Random seed (S:199, S:385-388) */
+    uint64_t stream_id;       /* PHILOX_R: Philox stream (independent sampler id) */
+} rsv_config;
+
+typedef struct rsv_sampler rsv_sampler;
+
+/* Library / error plumbing */
+int32_t     rsv_abi_version(void);
+const char* rsv_last_error(void);
+const char* rsv_status_string(rsv_status s);
+rsv_status  rsv_config_init(rsv_config* cfg); /* defaults: ELEMENTS, k=1, key_width 8, PHILOX_R */
+
+/* Construction = Sampler.apply / Sampler.distinct (S:128-136, S:171-180) incl. validation
+ * validateSharedParams (S:77-83).  `map`/`hash` nullness is checked on the JVM side. */
+rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out);
+void       rsv_destroy(rsv_sampler* s);
+
+/* Sampler.sample(element) (S:37-38; RandomElements.sampleImpl S:248-259; RandomValues.sample
+ * S:394-409).  The key is staged in a pinned host batch and flushed to the GPU in bulk; `hash`
+ * is read only for RSV_HASH_PRECOMPUTED (may be NULL otherwise). */
+rsv_status rsv_sample(rsv_sampler* s, const void* key, const int64_t* hash);
+
+/* Sampler.sampleAll(elements) (S:49-50, S:289-316): appends n keys at global indices
+ * [count, count+n).  mem says where `keys` (and `hashes`) live.  Identical results to n calls of
+ * rsv_sample, for any split into batches (SamplerTest.scala:117-142). */
+rsv_status rsv_sample_batch(rsv_sampler* s, const void* keys, int64_t n, int32_t mem,
+                            const int64_t* hashes);
+
+/* Sampler.result() (S:59-60; resultImpl S:318-331; RandomValues.result S:411).  Writes
+ * min(count, k) keys (ELEMENTS: slot order, which is part of the reference result) or the distinct
+ * set (DISTINCT: ascending scrambled hash; the reference's order is HashSet order) into host
+ * memory `out` of `cap` keys, and the count into *out_n.  Single-use samplers close (S:345-350):
+ * any later call but rsv_is_open returns RSV_E_ILLEGAL_STATE. */
+rsv_status rsv_result(rsv_sampler* s, void* out, int64_t cap, int64_t* out_n);
+/* Same, into device memory (no host round trip of the keys). */
+rsv_status rsv_result_device(rsv_sampler* s, void* out_dev, int64_t cap, int64_t* out_n);
+
+int32_t    rsv_is_open(const rsv_sampler* s); /* Sampler.isOpen (S:67, S:193, S:380) */
+int64_t    rsv_count(const rsv_sampler* s);   /* elements sampled so far (S:203) */
+
+/* Streams: every handle owns a non-blocking HIP stream; a caller may substitute its own. */
+rsv_status rsv_set_stream(rsv_sampler* s, void* hip_stream);
+void*      rsv_get_stream(const rsv_sampler* s);
+rsv_status rsv_synchronize(rsv_sampler* s);
+
+/* Kernel timing: while enabled, HIP events bracket every launch of the handle's hot kernel (K1
+ * for PHILOX_R, the event replay K1' for JAVA_L, the K3 filter for DISTINCT) on its stream.
+ * rsv_profile_read synchronizes and returns the summed kernel time and the launch count. */
+rsv_status rsv_profile_enable(rsv_sampler* s, int32_t on);
+rsv_status rsv_profile_read(rsv_sampler* s, double* total_ms, int64_t* launches);
+
+/* ---- Multi-GPU (index-range split of one stream; RSV_ENGINE_PHILOX_R / DISTINCT) ---------- */
+/* Declare that the next sampled element has global index `index` (>= count): the elements in
+ * between belong to other ranks.  PHILOX_R only. */
+rsv_status rsv_seek(rsv_sampler* s, int64_t index);
+/* Export the partial state into caller device buffers.
+ *   ELEMENTS: idx_dev[k] = global index held by each slot (-1 = empty), keys_dev[k].
+ *   DISTINCT: up to k (key, hash) pairs in ascending hash order, *out_n = count; idx_dev unused. */
+rsv_status rsv_export_state(rsv_sampler* s, int64_t* idx_dev, void* keys_dev, int64_t* hash_dev,
+                            int64_t* out_n);
+/* Merge `parts` exported states (laid out back to back, `part_len` entries each, e.g. gathered
+ * from every rank) into this sampler.  ELEMENTS: per slot the largest global index wins (last
+ * writer).  DISTINCT: bottom-k of the union.  total_count sets the merged element count. */
+rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* keys_dev,
+                           const int64_t* hash_dev, const int64_t* part_n_host, int32_t parts,
+                           int64_t part_len, int64_t total_count);
+
+/* ---- Stateless batch entry points --------------------------------------------------------- */
+/* Segmented sampling: S independent Algorithm-R samplers (no reference counterpart; = S separate
+ * Sampler instances, S:196-332).  Stream s samples keys_dev[offsets[s] .. offsets[s+1]) with
+ * Philox stream id stream_base + s and writes out_dev[s*k .. s*k+k) (slot order; slots >=
+ * counts[s] are zero) and counts_dev[s] = min(len, k).  All pointers are device pointers. */
+rsv_status rsv_sample_segmented(const void* keys_dev, const int64_t* offsets_dev, int64_t num_streams,
+                                int32_t key_width, int32_t k, uint64_t seed, uint64_t stream_base,
+                                void* out_dev, int64_t* counts_dev, void* hip_stream);
+
+/* Event replay (K1'): apply eviction events (1-based position, slot) -- the
+ * `samples(rand.nextInt(k)) = map(element)` writes of S:243-246 -- for elements at global indices
+ * [base_index, base_index+n) held in keys_dev, onto reservoir_dev[k] (in/out, device).  Also
+ * performs the fill phase (S:253-255) for indices < k.  The last event per slot wins. */
+rsv_status rsv_replay_events(const void* keys_dev, int64_t n, int32_t key_width, int64_t base_index,
+                             const int64_t* ev_pos_dev, const int32_t* ev_slot_dev, int64_t n_events,
+                             int32_t k, void* reservoir_dev, void* hip_stream);
+
+/* Export the per-element draw sequence j_i (format R1) for indices [i0, i0+n) into j_dev. */
+rsv_status rsv_export_draws(uint64_t seed, uint64_t stream_id, uint64_t i0, int64_t n,
+                            uint64_t* j_dev, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RESERVOIR_HIP_H */

@@ -1,0 +1,132 @@
+// rsv_device.h -- device helpers shared by the gfx950 kernels: Philox4x32-10, draw format R1,
+// and the scrambled hash of Sampler.distinct.
+//
+// Draw format R1 (DESIGN.md "Draw format"): for element index i of Philox stream s under key
+// (seed), U_i is a 64-bit uniform assembled from two counter-based Philox4x32-10 calls:
+//   level 0: ctr = (g0, g0>>32, s, s>>32), g0 = i >> 4   -> 16 bytes shared by 16 indices;
+//            b_i = byte (i & 15) (little-endian words) is the top byte of U_i
+//   level 1: ctr = (g1, (g1>>32) | 1<<31, s, s>>32), g1 = i >> 1 -> two 64-bit words;
+//            L_i = word (i & 1) = (w[2(i&1)] << 32) | w[2(i&1)+1]
+//   U_i = (b_i << 56) | (L_i >> 8),  j_i = floor(U_i * (i+1) / 2^64)   (uniform on [0, i])
+// Element i >= k replaces slot j_i iff j_i < k (Algorithm R).  Since U_i >= b_i * 2^56, a
+// necessary condition for j_i < k is b_i * (i+1) < 256 k; the kernels test that on level-0
+// bytes only and evaluate level 1 for the ~1/256 candidates that pass.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsv {
+
+struct u32x4 {
+    uint32_t x, y, z, w;
+};
+
+constexpr uint32_t kPhiloxM0 = 0xD2511F53u;
+constexpr uint32_t kPhiloxM1 = 0xCD9E8D57u;
+constexpr uint32_t kPhiloxW0 = 0x9E3779B9u;
+constexpr uint32_t kPhiloxW1 = 0xBB67AE85u;
+constexpr uint32_t kDomainLevel1 = 0x80000000u;
+
+// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11).  k0/k1 are wave-uniform (kernel args), so
+// the key schedule stays in SGPRs; each round is two 32x32->64 multiplies and two xor3.
+__device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                               uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += kPhiloxW0;
+            k1 += kPhiloxW1;
+        }
+        const uint64_t p0 = (uint64_t)kPhiloxM0 * c0;
+        const uint64_t p1 = (uint64_t)kPhiloxM1 * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0;
+        c1 = (uint32_t)p1;
+        c2 = n2;
+        c3 = (uint32_t)p0;
+    }
+    return {c0, c1, c2, c3};
+}
+
+struct DrawKey {
+    uint32_t k0, k1;  // Philox key = seed
+    uint32_t s0, s1;  // Philox stream words (counter words 2, 3)
+};
+
+__device__ __forceinline__ u32x4 level0(const DrawKey& dk, uint64_t g0) {
+    return philox4x32_10((uint32_t)g0, (uint32_t)(g0 >> 32), dk.s0, dk.s1, dk.k0, dk.k1);
+}
+
+__device__ __forceinline__ uint32_t word_of(const u32x4& w, uint32_t q) {
+    return q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
+}
+
+// byte e (0..15) of a level-0 block
+__device__ __forceinline__ uint32_t level0_byte(const u32x4& w, uint32_t e) {
+    return (word_of(w, e >> 2) >> (8 * (e & 3))) & 0xFFu;
+}
+
+// exact j_i given b_i (level-1 evaluated here)
+__device__ __forceinline__ uint64_t exact_j(const DrawKey& dk, uint64_t i, uint32_t b) {
+    const uint64_t g1 = i >> 1;
+    const u32x4 w =
+        philox4x32_10((uint32_t)g1, (uint32_t)(g1 >> 32) | kDomainLevel1, dk.s0, dk.s1, dk.k0, dk.k1);
+    const uint64_t L = (i & 1) ? (((uint64_t)w.z << 32) | w.w) : (((uint64_t)w.x << 32) | w.y);
+    const uint64_t U = ((uint64_t)b << 56) | (L >> 8);
+    return __umul64hi(U, i + 1);
+}
+
+// 16-bit mask of zero bytes of a level-0 block (exact: no false positives)
+__device__ __forceinline__ uint32_t zero_byte_mask16(const u32x4& w) {
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t x = word_of(w, q);
+        const uint32_t y = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte
+        // gather bits 7, 15, 23, 31 -> 4 bits
+        const uint32_t nib = ((y >> 7) & 1u) | ((y >> 14) & 2u) | ((y >> 21) & 4u) | ((y >> 28) & 8u);
+        m |= nib << (4 * q);
+    }
+    return m;
+}
+
+// true iff some byte of the block is zero (cheap sparse-region pre-test)
+__device__ __forceinline__ bool any_zero_byte(const u32x4& w) {
+    const uint32_t y0 = ((w.x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w.x;
+    const uint32_t y1 = ((w.y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w.y;
+    const uint32_t y2 = ((w.z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w.z;
+    const uint32_t y3 = ((w.w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w.w;
+    return ((y0 & y1 & y2 & y3) | 0x7F7F7F7Fu) != 0xFFFFFFFFu;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sampler.distinct scrambled hash (Sampler.scala:396) with scala.util.hashing.byteswap64
+// (scala-library 2.13.6: v * 0x9e3779b97f4a7c15, reverse bytes, * 0x9e3779b97f4a7c15).
+__host__ __device__ __forceinline__ uint64_t bswap64(uint64_t v) { return __builtin_bswap64(v); }
+
+__host__ __device__ __forceinline__ int64_t byteswap64(int64_t v) {
+    uint64_t hc = (uint64_t)v * 0x9e3779b97f4a7c15ULL;
+    hc = bswap64(hc);
+    return (int64_t)(hc * 0x9e3779b97f4a7c15ULL);
+}
+
+__host__ __device__ __forceinline__ int64_t scramble(int64_t r0, int64_t r1, int64_t hashed) {
+    return byteswap64(r1 ^ byteswap64(r0 ^ hashed));
+}
+
+enum HashKind : int { kHashIdentity = 1, kHashJavaLong = 2, kHashJavaInt = 3, kHashPrecomputed = 4 };
+
+template <typename KeyT, int HASH>
+__host__ __device__ __forceinline__ int64_t hash_of(KeyT key) {
+    if constexpr (HASH == kHashJavaLong) {
+        const uint64_t v = (uint64_t)(int64_t)key;
+        return (int64_t)(int32_t)(uint32_t)(v ^ (v >> 32));
+    } else if constexpr (HASH == kHashJavaInt) {
+        return (int64_t)(int32_t)key;
+    } else {
+        return (int64_t)key;  // identity (Int keys widen with sign, like Int.toLong)
+    }
+}
+
+}  // namespace rsv

@@ -1,0 +1,476 @@
+// rsv_distinct.hip -- Sampler.distinct (RandomValues, Sampler.scala:383-412) on gfx950.
+//
+// The reference keeps, for a stream of elements, the k distinct elements with the smallest signed
+// h = byteswap64(r1 ^ byteswap64(r0 ^ hash(elem))) (its max-heap evicts the current maximum
+// whenever a smaller unseen element arrives, Sampler.scala:403-407).  With an injective `hash`
+// the result is the bottom-k of h over the distinct elements, independent of arrival order, so
+// it is computed here as
+//   K3  filter:  one streaming pass over the keys (HBM-bound, 8 B/elem for Long keys): compute h,
+//                keep (h, key) with h <= T in a candidate buffer (wave-aggregated append)
+//   merge:       candidates + current set -> radix sort by (h, key) -> drop exact duplicates ->
+//                first k = new set
+// T is the current maximum (minus one) once the set is full, otherwise a quantile estimated from
+// a strided sample of the batch; a threshold that proves too tight (fewer than k distinct
+// candidates) or too loose (candidate buffer overflow) is corrected and the pass re-run, so the
+// result is exact regardless of the estimate.
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/reservoir_hip.h"
+#include "rsv_device.h"
+#include "rsv_internal.h"
+
+namespace rsv {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int64_t kSample = 65536;
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+    const uint32_t lane = threadIdx.x & 63;
+    return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+template <typename KeyT>
+__device__ __forceinline__ void append_if(bool c, int64_t h, KeyT key, int64_t* __restrict__ cand_h,
+                                          KeyT* __restrict__ cand_k,
+                                          unsigned long long* __restrict__ counter, int64_t cap) {
+    const unsigned long long b = __ballot(c);
+    if (b == 0) return;
+    const int leader = __ffsll((long long)b) - 1;
+    unsigned long long base = 0;
+    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(counter, (unsigned long long)__popcll(b));
+    base = __shfl(base, leader);
+    if (c) {
+        const unsigned long long pos = base + __popcll(b & lanemask_lt());
+        if ((int64_t)pos < cap) {
+            cand_h[pos] = h;
+            cand_k[pos] = key;
+        }
+    }
+}
+
+template <typename KeyT, int HASH>
+__device__ __forceinline__ int64_t elem_hash(const KeyT* keys, const int64_t* hashes, int64_t idx,
+                                             KeyT key, int64_t r0, int64_t r1) {
+    if constexpr (HASH == kHashPrecomputed) return scramble(r0, r1, hashes[idx]);
+    else return scramble(r0, r1, hash_of<KeyT, HASH>(key));
+}
+
+template <typename KeyT>
+struct Vec;
+typedef long long v2i64 __attribute__((ext_vector_type(2)));
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+template <>
+struct Vec<int64_t> {
+    using T = v2i64;
+    static constexpr int N = 2;
+    __device__ static int64_t get(const T& v, int e) { return v[e]; }
+};
+template <>
+struct Vec<int32_t> {
+    using T = v4i32;
+    static constexpr int N = 4;
+    __device__ static int32_t get(const T& v, int e) { return v[e]; }
+};
+
+// K3 filter: streaming pass, 2 x 16-B loads in flight per lane per iteration.
+template <typename KeyT, int HASH>
+__global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ keys,
+                                                    const int64_t* __restrict__ hashes, int64_t n,
+                                                    int64_t r0, int64_t r1, int64_t tinc,
+                                                    int64_t* __restrict__ cand_h,
+                                                    KeyT* __restrict__ cand_k,
+                                                    unsigned long long* __restrict__ counter,
+                                                    int64_t cap) {
+    using V = Vec<KeyT>;
+    constexpr int U = 2;
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n_vec = n / V::N;
+    const typename V::T* kv = reinterpret_cast<const typename V::T*>(keys);
+    for (int64_t v0 = tid; v0 - tid < n_vec; v0 += T * U) {  // uniform trip count per wave
+        typename V::T x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t v = v0 + u * T;
+            if (v < n_vec) x[u] = __builtin_nontemporal_load(kv + v);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t v = v0 + u * T;
+            const bool ok = v < n_vec;
+#pragma unroll
+            for (int e = 0; e < V::N; ++e) {
+                const KeyT key = ok ? V::get(x[u], e) : (KeyT)0;
+                const int64_t idx = v * V::N + e;
+                const int64_t h = ok ? elem_hash<KeyT, HASH>(keys, hashes, idx, key, r0, r1) : 0;
+                append_if<KeyT>(ok && h <= tinc, h, key, cand_h, cand_k, counter, cap);
+            }
+        }
+    }
+    // tail (n % V::N elements)
+    for (int64_t idx = n_vec * V::N + tid; idx - tid < n; idx += T) {
+        const bool ok = idx < n;
+        const KeyT key = ok ? keys[idx] : (KeyT)0;
+        const int64_t h = ok ? elem_hash<KeyT, HASH>(keys, hashes, idx, key, r0, r1) : 0;
+        append_if<KeyT>(ok && h <= tinc, h, key, cand_h, cand_k, counter, cap);
+    }
+}
+
+template <typename KeyT, int HASH>
+__global__ __launch_bounds__(kBlock) void sample_hash_kernel(const KeyT* __restrict__ keys,
+                                                             const int64_t* __restrict__ hashes,
+                                                             int64_t n, int64_t ns, int64_t r0,
+                                                             int64_t r1, int64_t* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ns) return;
+    const int64_t idx = (int64_t)(((unsigned __int128)t * (uint64_t)n) / (uint64_t)ns);
+    out[t] = elem_hash<KeyT, HASH>(keys, hashes, idx, keys[idx], r0, r1);
+}
+
+// after sorting by (h, key): flag = first of each run of identical (h, key)
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void dedup_flags(const int64_t* __restrict__ h,
+                                                      const KeyT* __restrict__ key, int64_t n,
+                                                      uint32_t* __restrict__ flags) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    flags[p] = (p == 0 || h[p] != h[p - 1] || key[p] != key[p - 1]) ? 1u : 0u;
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void compact_first_k(const int64_t* __restrict__ h,
+                                                          const KeyT* __restrict__ key,
+                                                          const uint32_t* __restrict__ flags,
+                                                          const uint32_t* __restrict__ pos, int64_t n,
+                                                          int64_t k, int64_t* __restrict__ out_h,
+                                                          KeyT* __restrict__ out_k,
+                                                          int64_t* __restrict__ out_count) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    if (flags[p] && (int64_t)pos[p] < k) {
+        out_h[pos[p]] = h[p];
+        out_k[pos[p]] = key[p];
+    }
+    if (p == n - 1) *out_count = (int64_t)pos[p] + (int64_t)flags[p];
+}
+
+inline unsigned grid_1d(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+struct DistinctState {
+    int32_t k = 0;
+    int kw = 8;
+    int hash_kind = kHashIdentity;
+    int64_t r0 = 0, r1 = 0;
+    int64_t m = 0;                // current set size
+    int64_t max_h = INT64_MIN;    // valid when m == k
+    int64_t* set_h = nullptr;     // [k], ascending (h, key)
+    void* set_k = nullptr;        // [k]
+    int64_t cand_cap = 0;
+    int64_t* cand_h = nullptr;
+    void* cand_k = nullptr;
+    unsigned long long* counter = nullptr;
+    int64_t merge_cap = 0;        // k + cand_cap
+    int64_t *mh0 = nullptr, *mh1 = nullptr;
+    void *mk0 = nullptr, *mk1 = nullptr;
+    uint32_t *flags = nullptr, *pos = nullptr;
+    int64_t* d_count = nullptr;
+    void* temp = nullptr;
+    size_t temp_bytes = 0;
+    int64_t* samp = nullptr;      // [2 * kSample]
+    int64_t* h_pinned = nullptr;  // host scalars
+    std::vector<int64_t> samp_host;
+    KernelTimer* timer = nullptr;
+};
+
+void distinct_set_timer(DistinctState* d, KernelTimer* t) { d->timer = t; }
+
+template <typename KeyT>
+static hipError_t temp_bytes_for(int64_t cap, size_t* bytes) {
+    size_t a = 0, b = 0, c = 0, d = 0;
+    hipError_t e;
+    e = rocprim::radix_sort_pairs(nullptr, a, (KeyT*)nullptr, (KeyT*)nullptr, (int64_t*)nullptr,
+                                  (int64_t*)nullptr, (size_t)cap);
+    if (e != hipSuccess) return e;
+    e = rocprim::radix_sort_pairs(nullptr, b, (int64_t*)nullptr, (int64_t*)nullptr, (KeyT*)nullptr,
+                                  (KeyT*)nullptr, (size_t)cap);
+    if (e != hipSuccess) return e;
+    e = rocprim::exclusive_scan(nullptr, c, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)cap,
+                                rocprim::plus<uint32_t>());
+    if (e != hipSuccess) return e;
+    e = rocprim::radix_sort_keys(nullptr, d, (int64_t*)nullptr, (int64_t*)nullptr, (size_t)kSample);
+    if (e != hipSuccess) return e;
+    *bytes = std::max(std::max(a, b), std::max(c, d));
+    return hipSuccess;
+}
+
+DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t r0, int64_t r1,
+                               int* status) {
+    DistinctState* d = new DistinctState();
+    d->k = k;
+    d->kw = key_width;
+    d->hash_kind = hash_kind;
+    d->r0 = r0;
+    d->r1 = r1;
+    d->cand_cap = 4 * (int64_t)k + 4096;
+    d->merge_cap = (int64_t)k + d->cand_cap;
+    const size_t kw = (size_t)key_width;
+    hipError_t e = hipSuccess;
+    auto A = [&](void** p, size_t bytes) {
+        if (e == hipSuccess) e = hipMalloc(p, bytes ? bytes : 16);
+    };
+    A((void**)&d->set_h, (size_t)k * 8);
+    A(&d->set_k, (size_t)k * kw);
+    A((void**)&d->cand_h, (size_t)d->cand_cap * 8);
+    A(&d->cand_k, (size_t)d->cand_cap * kw);
+    A((void**)&d->counter, 16);
+    A((void**)&d->mh0, (size_t)d->merge_cap * 8);
+    A((void**)&d->mh1, (size_t)d->merge_cap * 8);
+    A(&d->mk0, (size_t)d->merge_cap * kw);
+    A(&d->mk1, (size_t)d->merge_cap * kw);
+    A((void**)&d->flags, (size_t)d->merge_cap * 4);
+    A((void**)&d->pos, (size_t)d->merge_cap * 4);
+    A((void**)&d->d_count, 16);
+    A((void**)&d->samp, 2 * kSample * 8);
+    if (e == hipSuccess)
+        e = key_width == 8 ? temp_bytes_for<int64_t>(d->merge_cap, &d->temp_bytes)
+                           : temp_bytes_for<int32_t>(d->merge_cap, &d->temp_bytes);
+    A(&d->temp, d->temp_bytes);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&d->h_pinned, 64, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        set_error(std::string("distinct_create: ") + hipGetErrorString(e));
+        *status = e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;
+        distinct_destroy(d);
+        return nullptr;
+    }
+    *status = RSV_OK;
+    return d;
+}
+
+void distinct_destroy(DistinctState* d) {
+    if (!d) return;
+    void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->counter, d->mh0, d->mh1, d->mk0,
+                  d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    if (d->h_pinned) (void)hipHostFree(d->h_pinned);
+    delete d;
+}
+
+int64_t distinct_size(const DistinctState* d) { return d->m; }
+
+template <typename KeyT>
+static hipError_t launch_filter(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
+                                int64_t tinc, hipStream_t st) {
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 8 + 1), 1), 256 * 8);
+    KeyT* ck = (KeyT*)d->cand_k;
+    switch (d->hash_kind) {
+    case kHashJavaLong:
+        hipLaunchKernelGGL((k3_filter<KeyT, kHashJavaLong>), dim3(grid), dim3(kBlock), 0, st, keys, hashes,
+                           n, d->r0, d->r1, tinc, d->cand_h, ck, d->counter, d->cand_cap);
+        break;
+    case kHashJavaInt:
+        hipLaunchKernelGGL((k3_filter<KeyT, kHashJavaInt>), dim3(grid), dim3(kBlock), 0, st, keys, hashes,
+                           n, d->r0, d->r1, tinc, d->cand_h, ck, d->counter, d->cand_cap);
+        break;
+    case kHashPrecomputed:
+        hipLaunchKernelGGL((k3_filter<KeyT, kHashPrecomputed>), dim3(grid), dim3(kBlock), 0, st, keys,
+                           hashes, n, d->r0, d->r1, tinc, d->cand_h, ck, d->counter, d->cand_cap);
+        break;
+    default:
+        hipLaunchKernelGGL((k3_filter<KeyT, kHashIdentity>), dim3(grid), dim3(kBlock), 0, st, keys, hashes,
+                           n, d->r0, d->r1, tinc, d->cand_h, ck, d->counter, d->cand_cap);
+    }
+    return hipGetLastError();
+}
+
+template <typename KeyT>
+static hipError_t launch_sample(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
+                                int64_t ns, hipStream_t st) {
+    const unsigned grid = grid_1d(ns);
+    switch (d->hash_kind) {
+    case kHashJavaLong:
+        hipLaunchKernelGGL((sample_hash_kernel<KeyT, kHashJavaLong>), dim3(grid), dim3(kBlock), 0, st,
+                           keys, hashes, n, ns, d->r0, d->r1, d->samp);
+        break;
+    case kHashJavaInt:
+        hipLaunchKernelGGL((sample_hash_kernel<KeyT, kHashJavaInt>), dim3(grid), dim3(kBlock), 0, st,
+                           keys, hashes, n, ns, d->r0, d->r1, d->samp);
+        break;
+    case kHashPrecomputed:
+        hipLaunchKernelGGL((sample_hash_kernel<KeyT, kHashPrecomputed>), dim3(grid), dim3(kBlock), 0, st,
+                           keys, hashes, n, ns, d->r0, d->r1, d->samp);
+        break;
+    default:
+        hipLaunchKernelGGL((sample_hash_kernel<KeyT, kHashIdentity>), dim3(grid), dim3(kBlock), 0, st,
+                           keys, hashes, n, ns, d->r0, d->r1, d->samp);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    size_t tb = d->temp_bytes;
+    return rocprim::radix_sort_keys(d->temp, tb, d->samp, d->samp + kSample, (size_t)ns, 0, 64, st);
+}
+
+// Merge `c` entries at (src_h, src_k) with the current set; new set = first k distinct by
+// (h, key).  Returns the distinct count of the union in *n_distinct.
+template <typename KeyT>
+static hipError_t merge_into_set(DistinctState* d, const int64_t* src_h, const KeyT* src_k, int64_t c,
+                                 int64_t* n_distinct, hipStream_t st) {
+    const int64_t total = d->m + c;
+    if (total == 0) {
+        *n_distinct = 0;
+        return hipSuccess;
+    }
+    if (total > d->merge_cap) return hipErrorInvalidValue;
+    KeyT* mk0 = (KeyT*)d->mk0;
+    KeyT* mk1 = (KeyT*)d->mk1;
+    hipError_t e;
+    if (d->m) {
+        if ((e = hipMemcpyAsync(d->mh0, d->set_h, d->m * 8, hipMemcpyDeviceToDevice, st))) return e;
+        if ((e = hipMemcpyAsync(mk0, d->set_k, d->m * sizeof(KeyT), hipMemcpyDeviceToDevice, st))) return e;
+    }
+    if (c) {
+        if ((e = hipMemcpyAsync(d->mh0 + d->m, src_h, c * 8, hipMemcpyDeviceToDevice, st))) return e;
+        if ((e = hipMemcpyAsync(mk0 + d->m, src_k, c * sizeof(KeyT), hipMemcpyDeviceToDevice, st))) return e;
+    }
+    size_t tb = d->temp_bytes;
+    // stable LSD order: by key, then by h  ->  sorted by (h, key)
+    if ((e = rocprim::radix_sort_pairs(d->temp, tb, mk0, mk1, d->mh0, d->mh1, (size_t)total, 0,
+                                       8 * (unsigned)sizeof(KeyT), st)))
+        return e;
+    tb = d->temp_bytes;
+    if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->mh1, d->mh0, mk1, mk0, (size_t)total, 0, 64, st)))
+        return e;
+    hipLaunchKernelGGL(dedup_flags<KeyT>, dim3(grid_1d(total)), dim3(kBlock), 0, st, d->mh0, mk0, total,
+                       d->flags);
+    if ((e = hipGetLastError())) return e;
+    tb = d->temp_bytes;
+    if ((e = rocprim::exclusive_scan(d->temp, tb, d->flags, d->pos, 0u, (size_t)total,
+                                     rocprim::plus<uint32_t>(), st)))
+        return e;
+    hipLaunchKernelGGL(compact_first_k<KeyT>, dim3(grid_1d(total)), dim3(kBlock), 0, st, d->mh0, mk0,
+                       d->flags, d->pos, total, (int64_t)d->k, d->set_h, (KeyT*)d->set_k, d->d_count);
+    if ((e = hipGetLastError())) return e;
+    if ((e = hipMemcpyAsync(d->h_pinned, d->d_count, 8, hipMemcpyDeviceToHost, st))) return e;
+    if ((e = hipStreamSynchronize(st))) return e;
+    *n_distinct = d->h_pinned[0];
+    d->m = std::min<int64_t>(*n_distinct, d->k);
+    if (d->m == d->k) {
+        if ((e = hipMemcpyAsync(d->h_pinned + 1, d->set_h + d->k - 1, 8, hipMemcpyDeviceToHost, st))) return e;
+        if ((e = hipStreamSynchronize(st))) return e;
+        d->max_h = d->h_pinned[1];
+    }
+    return hipSuccess;
+}
+
+template <typename KeyT>
+static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
+                       hipStream_t st) {
+#define DTRY(x)                                                                      \
+    do {                                                                             \
+        hipError_t _e = (x);                                                         \
+        if (_e != hipSuccess) {                                                      \
+            set_error(std::string("distinct: " #x ": ") + hipGetErrorString(_e));    \
+            return _e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;   \
+        }                                                                            \
+    } while (0)
+    if (n <= 0) return RSV_OK;
+    const bool full = d->m == d->k;
+    if (full && d->max_h == INT64_MIN) return RSV_OK;  // nothing can be smaller than the max
+    const int64_t t_allowed = full ? d->max_h - 1 : INT64_MAX;  // Sampler.scala:403 (strict <)
+    int64_t q = 0, ns = 0;
+    auto take_sample = [&]() -> int {
+        ns = std::min<int64_t>(n, kSample);
+        DTRY(launch_sample<KeyT>(d, keys, hashes, n, ns, st));
+        d->samp_host.resize((size_t)ns);
+        DTRY(hipMemcpyAsync(d->samp_host.data(), d->samp + kSample, ns * 8, hipMemcpyDeviceToHost, st));
+        DTRY(hipStreamSynchronize(st));
+        return RSV_OK;
+    };
+    auto quantile = [&](int64_t qq) -> int64_t {
+        return qq >= ns ? t_allowed : std::min(d->samp_host[(size_t)std::max<int64_t>(qq, 0)], t_allowed);
+    };
+    int64_t tinc = t_allowed;
+    if (!full && n > d->cand_cap / 2) {  // estimate a threshold that passes ~2k elements
+        if (int rc = take_sample()) return rc;
+        q = (int64_t)((__int128)(2 * (int64_t)d->k + 1024) * ns / n) + 8;
+        tinc = quantile(q);
+    }
+    for (int attempt = 0; attempt < 128; ++attempt) {
+        DTRY(hipMemsetAsync(d->counter, 0, 8, st));
+        if (d->timer) d->timer->mark(st);
+        DTRY(launch_filter<KeyT>(d, keys, hashes, n, tinc, st));
+        if (d->timer) d->timer->mark(st);
+        DTRY(hipMemcpyAsync(d->h_pinned + 2, d->counter, 8, hipMemcpyDeviceToHost, st));
+        DTRY(hipStreamSynchronize(st));
+        const int64_t c = d->h_pinned[2];
+        if (c > d->cand_cap) {  // threshold too loose for the candidate buffer: tighten
+            if (ns == 0) {
+                if (int rc = take_sample()) return rc;
+                q = (int64_t)((__int128)(d->cand_cap / 4) * ns / n);
+            } else {
+                q /= 2;
+            }
+            int64_t t = quantile(q);
+            if (t >= tinc) t = tinc - (int64_t)(((uint64_t)tinc - (uint64_t)INT64_MIN) / 2) - 1;
+            tinc = t;
+            continue;
+        }
+        int64_t nd = 0;
+        DTRY(merge_into_set<KeyT>(d, d->cand_h, (const KeyT*)d->cand_k, c, &nd, st));
+        // exact once every batch element below the new k-th hash was a candidate
+        if (tinc >= t_allowed || (d->m == d->k && d->max_h <= tinc)) return RSV_OK;
+        // too tight: widen (the partial merge is harmless: bottom-k(bottom-k(S u C1) u C2) equals
+        // bottom-k(S u C2) for C1 a subset of C2)
+        if (ns == 0) {
+            if (int rc = take_sample()) return rc;
+            q = 0;
+        }
+        q = q < 16 ? 64 : q * 4;
+        tinc = quantile(q);
+    }
+    set_error("distinct: threshold search did not converge");
+    return RSV_E_DEVICE;
+#undef DTRY
+}
+
+int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* hashes, int64_t n,
+                           hipStream_t st) {
+    return d->kw == 8 ? sample_impl<int64_t>(d, (const int64_t*)keys, hashes, n, st)
+                      : sample_impl<int32_t>(d, (const int32_t*)keys, hashes, n, st);
+}
+
+int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStream_t st) {
+    if (d->m == 0) return RSV_OK;
+    if (keys_dev) RSV_HIP_TRY(hipMemcpyAsync(keys_dev, d->set_k, d->m * d->kw, hipMemcpyDeviceToDevice, st));
+    if (hash_dev) RSV_HIP_TRY(hipMemcpyAsync(hash_dev, d->set_h, d->m * 8, hipMemcpyDeviceToDevice, st));
+    return RSV_OK;
+}
+
+int distinct_merge(DistinctState* d, const void* keys_dev, const int64_t* hash_dev, int64_t n,
+                   hipStream_t st) {
+    int64_t off = 0;
+    while (off < n) {  // chunks that fit the merge buffer
+        const int64_t c = std::min<int64_t>(n - off, d->cand_cap);
+        int64_t nd = 0;
+        hipError_t e = d->kw == 8
+                           ? merge_into_set<int64_t>(d, hash_dev + off, (const int64_t*)keys_dev + off, c, &nd, st)
+                           : merge_into_set<int32_t>(d, hash_dev + off, (const int32_t*)keys_dev + off, c, &nd, st);
+        if (e != hipSuccess) {
+            set_error(std::string("distinct_merge: ") + hipGetErrorString(e));
+            return RSV_E_DEVICE;
+        }
+        off += c;
+    }
+    return RSV_OK;
+}
+
+}  // namespace rsv

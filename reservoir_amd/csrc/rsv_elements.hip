@@ -1,0 +1,271 @@
+// rsv_elements.hip -- gfx950 kernels for the element sampler (Sampler.apply, Sampler.scala:196-332)
+// reformulated as data-parallel Algorithm R with counter-based draws (format R1, rsv_device.h).
+//
+//   K1  k1_last_writer   single stream: per-slot last writer (max index) of an index range
+//   --  resolve          fill phase + gather of the winning keys into the reservoir
+//   K1' replay_events    the reference's Algorithm-L eviction events -> per-slot last writer
+//   K2  k2_segmented     one wave per independent stream, slot table in LDS
+//   --  merge_slots      multi-GPU combine of exported partial reservoirs (last writer wins)
+//
+// None of these kernels streams the key array: a draw depends only on (seed, stream, index), so
+// only the k winning keys are ever read (DESIGN.md "Roofline").
+#include "rsv_device.h"
+#include "rsv_internal.h"
+
+namespace rsv {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint32_t clip_mask16(uint64_t i0, uint64_t lo, uint64_t hi) {
+    uint32_t m = 0xFFFFu;
+    if (i0 < lo) m = (lo - i0 >= 16) ? 0u : ((0xFFFFu << (uint32_t)(lo - i0)) & 0xFFFFu);
+    if (i0 + 16 > hi) m &= (hi <= i0) ? 0u : (0xFFFFu >> (uint32_t)(16 - (hi - i0)));
+    return m;
+}
+
+// Candidate mask of one level-0 block: bit e set iff b_{i0+e} * (i0+e+1) < 256k (necessary
+// condition for j < k).  Beyond index 256k-1 this is simply "byte == 0" (1 in 256).
+__device__ __forceinline__ uint32_t candidate_mask16(const u32x4& w, uint64_t i0, uint64_t dense_lim) {
+    if (i0 + 1 >= dense_lim) {
+        if (!any_zero_byte(w)) return 0u;
+        return zero_byte_mask16(w);
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < 16; ++e) {
+        const uint64_t b = level0_byte(w, e);
+        if (b * (i0 + e + 1) < dense_lim) m |= 1u << e;
+    }
+    return m;
+}
+
+__global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k, uint64_t lo,
+                                                         uint64_t hi, uint64_t g_begin,
+                                                         uint64_t n_groups,
+                                                         unsigned long long* __restrict__ win) {
+    const uint64_t dense_lim = 256ull * k;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; gi < n_groups; gi += stride) {
+        const uint64_t g = g_begin + gi;
+        const uint64_t i0 = g << 4;
+        const u32x4 w = level0(dk, g);
+        uint32_t mask = candidate_mask16(w, i0, dense_lim);
+        if (!mask) continue;
+        mask &= clip_mask16(i0, lo, hi);
+        while (mask) {
+            const uint32_t e = __builtin_ctz(mask);
+            mask &= mask - 1;
+            const uint64_t i = i0 + e;
+            const uint64_t j = exact_j(dk, i, level0_byte(w, e));
+            if (j < k) atomicMax(&win[j], (unsigned long long)i);
+        }
+    }
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void resolve_kernel(const KeyT* __restrict__ keys, int64_t base,
+                                                         int64_t n, uint32_t k,
+                                                         unsigned long long* __restrict__ win,
+                                                         KeyT* __restrict__ slot_key,
+                                                         int64_t* __restrict__ slot_idx) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    if ((int64_t)j >= base && (int64_t)j < base + n) {  // fill phase (Sampler.scala:253-255)
+        slot_key[j] = keys[j - base];
+        if (slot_idx) slot_idx[j] = j;
+    }
+    const unsigned long long wi = win[j];
+    if (wi) {  // last eviction into slot j in this batch (Sampler.scala:243-246)
+        slot_key[j] = keys[(int64_t)wi - base];
+        if (slot_idx) slot_idx[j] = (int64_t)wi;
+        win[j] = 0;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void replay_kernel(const int64_t* __restrict__ ev_pos,
+                                                        const int32_t* __restrict__ ev_slot,
+                                                        int64_t n_events, uint32_t k,
+                                                        unsigned long long* __restrict__ win) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_events) return;
+    const int32_t s = ev_slot[e];
+    const int64_t p = ev_pos[e];
+    if (s >= 0 && (uint32_t)s < k && p >= 2) atomicMax(&win[s], (unsigned long long)(p - 1));
+}
+
+__global__ __launch_bounds__(kBlock) void export_draws_kernel(DrawKey dk, uint64_t i0, int64_t n,
+                                                              uint64_t* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint64_t i = i0 + (uint64_t)t;
+    const u32x4 w = level0(dk, i >> 4);
+    out[t] = exact_j(dk, i, level0_byte(w, (uint32_t)(i & 15)));
+}
+
+// K2: one wave per stream; the wave's k-entry last-writer table lives in LDS.
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void k2_segmented(const KeyT* __restrict__ keys,
+                                                       const int64_t* __restrict__ offsets, int64_t S,
+                                                       uint32_t k, uint32_t k0, uint32_t k1,
+                                                       uint64_t stream_base, KeyT* __restrict__ out,
+                                                       int64_t* __restrict__ counts) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_tab[];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t wpb = blockDim.x >> 6;
+    unsigned long long* tab = lds_tab + (size_t)wave * k;
+    const uint64_t dense_lim = 256ull * k;
+    for (int64_t sb = (int64_t)blockIdx.x * wpb; sb < S; sb += (int64_t)gridDim.x * wpb) {
+        const int64_t s = sb + wave;
+        const bool active = s < S;
+        for (uint32_t j = lane; j < k; j += 64) tab[j] = 0;
+        __syncthreads();
+        int64_t off = 0, len = 0;
+        if (active) {
+            off = offsets[s];
+            len = offsets[s + 1] - off;
+            const uint64_t stream = stream_base + (uint64_t)s;
+            const DrawKey dk{k0, k1, (uint32_t)stream, (uint32_t)(stream >> 32)};
+            const uint64_t n_groups = ((uint64_t)len + 15) >> 4;
+            for (uint64_t g = (k >> 4) + lane; g < n_groups; g += 64) {
+                const uint64_t i0 = g << 4;
+                const u32x4 w = level0(dk, g);
+                uint32_t mask = candidate_mask16(w, i0, dense_lim);
+                if (!mask) continue;
+                mask &= clip_mask16(i0, k, (uint64_t)len);
+                while (mask) {
+                    const uint32_t e = __builtin_ctz(mask);
+                    mask &= mask - 1;
+                    const uint64_t i = i0 + e;
+                    const uint64_t j = exact_j(dk, i, level0_byte(w, e));
+                    if (j < k) atomicMax(&tab[j], (unsigned long long)i);
+                }
+            }
+        }
+        __syncthreads();
+        if (active) {
+            KeyT* o = out + s * (int64_t)k;
+            for (uint32_t j = lane; j < k; j += 64) {
+                const unsigned long long wi = tab[j];
+                o[j] = wi ? keys[off + (int64_t)wi] : ((int64_t)j < len ? keys[off + j] : (KeyT)0);
+            }
+            if (lane == 0) counts[s] = len < (int64_t)k ? len : (int64_t)k;
+        }
+        __syncthreads();
+    }
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void merge_slots_kernel(const int64_t* __restrict__ idx_parts,
+                                                             const KeyT* __restrict__ key_parts,
+                                                             int32_t parts, int64_t part_len,
+                                                             uint32_t k, int64_t* __restrict__ slot_idx,
+                                                             KeyT* __restrict__ slot_key) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    int64_t best = slot_idx[j];
+    KeyT key = slot_key[j];
+    for (int32_t p = 0; p < parts; ++p) {
+        const int64_t idx = idx_parts[(int64_t)p * part_len + j];
+        if (idx > best) {
+            best = idx;
+            key = key_parts[(int64_t)p * part_len + j];
+        }
+    }
+    slot_idx[j] = best;
+    slot_key[j] = key;
+}
+
+inline DrawKey make_key(const DrawParams& dp) {
+    return DrawKey{(uint32_t)dp.seed, (uint32_t)(dp.seed >> 32), (uint32_t)dp.stream,
+                   (uint32_t)(dp.stream >> 32)};
+}
+
+inline unsigned grid_for(uint64_t items, unsigned cap) {
+    uint64_t b = (items + kBlock - 1) / kBlock;
+    if (b < 1) b = 1;
+    return (unsigned)(b < cap ? b : cap);
+}
+
+}  // namespace
+
+hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
+                                 unsigned long long* batch_win, hipStream_t st) {
+    if (hi <= lo) return hipSuccess;
+    const uint64_t g_begin = lo >> 4, g_end = (hi + 15) >> 4;
+    const uint64_t n_groups = g_end - g_begin;
+    const unsigned grid = grid_for(n_groups, 256 * 8);
+    hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
+                       g_begin, n_groups, batch_win);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,
+                          unsigned long long* batch_win, void* slot_key, int64_t* slot_idx,
+                          hipStream_t st) {
+    const unsigned grid = (unsigned)((k + kBlock - 1) / kBlock);
+    if (key_width == 8)
+        hipLaunchKernelGGL(resolve_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, st,
+                           (const int64_t*)keys, base, n, k, batch_win, (int64_t*)slot_key, slot_idx);
+    else
+        hipLaunchKernelGGL(resolve_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, st,
+                           (const int32_t*)keys, base, n, k, batch_win, (int32_t*)slot_key, slot_idx);
+    return hipGetLastError();
+}
+
+hipError_t launch_replay_events(const int64_t* ev_pos, const int32_t* ev_slot, int64_t n_events,
+                                uint32_t k, unsigned long long* batch_win, hipStream_t st) {
+    if (n_events <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((n_events + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(replay_kernel, dim3(grid), dim3(kBlock), 0, st, ev_pos, ev_slot, n_events, k,
+                       batch_win);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_draws(const DrawParams& dp, uint64_t i0, int64_t n, uint64_t* j,
+                               hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(export_draws_kernel, dim3(grid), dim3(kBlock), 0, st, make_key(dp), i0, n, j);
+    return hipGetLastError();
+}
+
+int segmented_waves_per_block(uint32_t k) {
+    const uint32_t w = 8192u / (k ? k : 1);
+    return (int)(w < 1 ? 1 : (w > 4 ? 4 : w));
+}
+
+hipError_t launch_segmented(const void* keys, int key_width, const int64_t* offsets, int64_t S,
+                            uint32_t k, const DrawParams& dp, void* out, int64_t* counts,
+                            hipStream_t st) {
+    if (S <= 0) return hipSuccess;
+    const int wpb = segmented_waves_per_block(k);
+    const size_t lds = (size_t)wpb * k * sizeof(unsigned long long);
+    uint64_t blocks = ((uint64_t)S + wpb - 1) / wpb;
+    const uint64_t cap = 256ull * 16;
+    const unsigned grid = (unsigned)(blocks < cap ? blocks : cap);
+    const uint32_t k0 = (uint32_t)dp.seed, k1 = (uint32_t)(dp.seed >> 32);
+    if (key_width == 8)
+        hipLaunchKernelGGL(k2_segmented<int64_t>, dim3(grid), dim3(64 * wpb), lds, st,
+                           (const int64_t*)keys, offsets, S, k, k0, k1, dp.stream, (int64_t*)out, counts);
+    else
+        hipLaunchKernelGGL(k2_segmented<int32_t>, dim3(grid), dim3(64 * wpb), lds, st,
+                           (const int32_t*)keys, offsets, S, k, k0, k1, dp.stream, (int32_t*)out, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_slots(const int64_t* idx_parts, const void* key_parts, int key_width,
+                              int32_t parts, int64_t part_len, uint32_t k, int64_t* slot_idx,
+                              void* slot_key, hipStream_t st) {
+    const unsigned grid = (unsigned)((k + kBlock - 1) / kBlock);
+    if (key_width == 8)
+        hipLaunchKernelGGL(merge_slots_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, st, idx_parts,
+                           (const int64_t*)key_parts, parts, part_len, k, slot_idx, (int64_t*)slot_key);
+    else
+        hipLaunchKernelGGL(merge_slots_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, st, idx_parts,
+                           (const int32_t*)key_parts, parts, part_len, k, slot_idx, (int32_t*)slot_key);
+    return hipGetLastError();
+}
+
+}  // namespace rsv

@@ -1,0 +1,103 @@
+// rsv_internal.h -- host-side declarations shared between the runtime and the kernel translation
+// units of libreservoir_hip.so.  Not part of the public ABI (that is include/reservoir_hip.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace rsv {
+
+// thread-local last error (rsv_last_error)
+void set_error(const std::string& msg);
+
+#define RSV_HIP_TRY(expr)                                                                     \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess) {                                                               \
+            ::rsv::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));              \
+            return _e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;            \
+        }                                                                                     \
+    } while (0)
+
+// HIP-event timing of a handle's hot kernel (rsv_profile_enable / rsv_profile_read)
+struct KernelTimer {
+    bool on = false;
+    std::vector<hipEvent_t> ev;  // start/stop pairs, recycled after each drain
+    size_t used = 0;
+    double total_ms = 0;
+    int64_t launches = 0;
+    void mark(hipStream_t st) {
+        if (!on) return;
+        if (used == ev.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return;
+            ev.push_back(e);
+        }
+        (void)hipEventRecord(ev[used++], st);
+    }
+    hipError_t drain() {
+        for (size_t i = 0; i + 1 < used; i += 2) {
+            hipError_t e = hipEventSynchronize(ev[i + 1]);
+            if (e != hipSuccess) return e;
+            float ms = 0;
+            e = hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+            if (e != hipSuccess) return e;
+            total_ms += ms;
+            launches++;
+        }
+        used = 0;
+        return hipSuccess;
+    }
+    ~KernelTimer() {
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+struct DrawParams {
+    uint64_t seed;
+    uint64_t stream;
+};
+
+// ---- elements (Algorithm R, draw format R1) -------------------------------------------------
+// K1: per-slot last writer of the index range [lo, hi) (only indices >= k can evict) into
+// batch_win[k] (0 = no writer in this batch; atomicMax keeps the largest index).
+hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
+                                 unsigned long long* batch_win, hipStream_t st);
+// Resolve: fill phase for slots in [base, base+n) and winners of batch_win; resets batch_win.
+// slot_idx may be null.
+hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,
+                          unsigned long long* batch_win, void* slot_key, int64_t* slot_idx,
+                          hipStream_t st);
+// K1': events (1-based pos, slot) -> batch_win
+hipError_t launch_replay_events(const int64_t* ev_pos, const int32_t* ev_slot, int64_t n_events,
+                                uint32_t k, unsigned long long* batch_win, hipStream_t st);
+hipError_t launch_export_draws(const DrawParams& dp, uint64_t i0, int64_t n, uint64_t* j,
+                               hipStream_t st);
+// K2: segmented
+hipError_t launch_segmented(const void* keys, int key_width, const int64_t* offsets, int64_t S,
+                            uint32_t k, const DrawParams& dp, void* out, int64_t* counts,
+                            hipStream_t st);
+// merge of exported element states: per slot max index among parts (and current state)
+hipError_t launch_merge_slots(const int64_t* idx_parts, const void* key_parts, int key_width,
+                              int32_t parts, int64_t part_len, uint32_t k, int64_t* slot_idx,
+                              void* slot_key, hipStream_t st);
+
+// ---- distinct (bottom-k over the scrambled hash) --------------------------------------------
+struct DistinctState;  // defined in rsv_distinct.hip
+DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t r0, int64_t r1,
+                               int* status);
+void distinct_set_timer(DistinctState* d, KernelTimer* t);
+void distinct_destroy(DistinctState* d);
+// keys/hashes are device pointers
+int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* hashes, int64_t n,
+                           hipStream_t st);
+int64_t distinct_size(const DistinctState* d);
+// copies the set (ascending hash) to device buffers; either may be null
+int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStream_t st);
+// merge external (key, hash) entries (device) into the set
+int distinct_merge(DistinctState* d, const void* keys_dev, const int64_t* hash_dev, int64_t n,
+                   hipStream_t st);
+
+}  // namespace rsv

@@ -1,0 +1,591 @@
+// rsv_runtime.hip -- implementation of the C ABI (include/reservoir_hip.h): sampler handles,
+// lifecycle (SingleUse / MultiResult, Sampler.scala:182-194, :334-381, :414-433), staging of
+// per-element calls into pinned batches, host->device batching, engine dispatch, multi-GPU
+// state export/merge.  All data-parallel work runs in the kernels of rsv_elements.hip and
+// rsv_distinct.hip; there is no CPU compute path.
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/reservoir_hip.h"
+#include "rsv_device.h"
+#include "rsv_internal.h"
+
+namespace rsv {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int segmented_waves_per_block(uint32_t k);
+
+// ---------------------------------------------------------------------------------------------
+// java.util.Random + Algorithm L event generator for RSV_ENGINE_JAVA_L (product implementation;
+// the oracle under oracle/ is an independent restatement used only by the tests).
+struct JavaRandom {
+    uint64_t seed = 0;
+    void init(int64_t s) { seed = ((uint64_t)s ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1); }
+    int32_t next(int bits) {
+        seed = (seed * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+        return (int32_t)(uint32_t)(seed >> (48 - bits));
+    }
+    double next_double() {  // java.util.Random.nextDouble
+        const int64_t a = next(26), b = next(27);
+        return (double)((a << 27) + b) * 0x1.0p-53;
+    }
+    int32_t next_int(int32_t bound) {  // java.util.Random.nextInt(int)
+        int32_t r = next(31);
+        const int32_t m = bound - 1;
+        if ((bound & m) == 0) return (int32_t)(((int64_t)bound * (int64_t)r) >> 31);
+        for (int32_t u = r;; u = next(31)) {
+            r = u % bound;
+            if ((int32_t)((uint32_t)u - (uint32_t)r + (uint32_t)m) >= 0) break;
+        }
+        return r;
+    }
+    int64_t next_long() {
+        const int64_t hi = next(32), lo = next(32);
+        return (int64_t)(((uint64_t)hi << 32) + (uint64_t)lo);
+    }
+};
+
+struct AlgoLState {  // RandomElements' private state (Sampler.scala:199-205)
+    JavaRandom rand;
+    int32_t k = 0;
+    double W = 1.0;
+    int64_t next_sample_count = 0;
+
+    static int64_t d2l(double d) {  // JVM double -> long (saturating, NaN -> 0)
+        if (d != d) return 0;
+        if (d >= 9223372036854775807.0) return INT64_MAX;
+        if (d <= -9223372036854775808.0) return INT64_MIN;
+        return (int64_t)d;
+    }
+    void update() {  // updateNextSampleCount, Sampler.scala:228-236
+        W = W * std::exp(std::log(rand.next_double()) / (double)k);
+        const double skip = std::floor(std::log(rand.next_double()) / std::log(1.0 - W));
+        next_sample_count = (int64_t)((uint64_t)next_sample_count + (uint64_t)d2l(skip) + 1ULL);
+    }
+    void init(int32_t kk, int64_t seed) {  // as SamplerTest.useConsistentRandom re-seeds it
+        k = kk;
+        rand.init(seed);
+        W = 1.0;
+        next_sample_count = kk;
+        update();
+    }
+    // eviction events for 1-based positions (base, base+n] -- the per-element rule of
+    // sampleImpl (Sampler.scala:248-259): position c > k evicts iff c >= nextSampleCount.
+    void events(int64_t base, int64_t n, std::vector<int64_t>& pos, std::vector<int32_t>& slot) {
+        int64_t cur = base + 1;
+        const int64_t end = base + n;
+        if (cur <= k) cur = (int64_t)k + 1;
+        while (cur <= end) {
+            const int64_t p = std::max(next_sample_count, cur);
+            if (p > end) break;
+            pos.push_back(p);
+            slot.push_back(rand.next_int(k));  // sampleWithEviction, Sampler.scala:243-246
+            update();
+            cur = p + 1;
+        }
+    }
+};
+
+}  // namespace rsv
+
+using namespace rsv;
+
+struct rsv_sampler {
+    rsv_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    bool open = true;
+    int64_t count = 0;
+    int kw = 8;
+    uint32_t k = 0;
+    // ELEMENTS
+    void* slot_key = nullptr;
+    int64_t* slot_idx = nullptr;
+    unsigned long long* batch_win = nullptr;
+    AlgoLState algo_l;
+    std::vector<int64_t> ev_pos_h;
+    std::vector<int32_t> ev_slot_h;
+    int64_t* ev_pos_d = nullptr;
+    int32_t* ev_slot_d = nullptr;
+    int64_t ev_cap = 0;
+    // DISTINCT
+    DistinctState* distinct = nullptr;
+    int hash_kind = kHashIdentity;
+    // host staging: per-element calls and host batches
+    uint8_t* stage_h = nullptr;  // pinned, stage_cap keys
+    int64_t* stage_hash_h = nullptr;
+    int64_t stage_n = 0;
+    int64_t stage_cap = 0;
+    void* chunk_d = nullptr;     // device chunk for host batches
+    int64_t* chunk_hash_d = nullptr;
+    int64_t chunk_cap = 0;
+    KernelTimer timer;
+};
+
+namespace {
+
+constexpr int32_t kMaxSize = 2147483647 - 2;  // Sampler.scala:71 (hotspot VM array limit)
+constexpr int64_t kStageKeys = 1 << 20;
+constexpr int64_t kChunkKeys = 1 << 22;
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+rsv_status fail(rsv_status st, const std::string& msg) {
+    set_error(msg);
+    return st;
+}
+
+rsv_status check_open(const rsv_sampler* s) {  // SingleUse.checkOpen, Sampler.scala:185-186
+    if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
+    if (!s->open) return fail(RSV_E_ILLEGAL_STATE, "use of sampler after calling `result()`");
+    return RSV_OK;
+}
+
+rsv_status ensure_events(rsv_sampler* s, int64_t n) {
+    if (n <= s->ev_cap) return RSV_OK;
+    int64_t cap = std::max<int64_t>(n, 2 * s->ev_cap);
+    if (s->ev_pos_d) (void)hipFree(s->ev_pos_d);
+    if (s->ev_slot_d) (void)hipFree(s->ev_slot_d);
+    s->ev_pos_d = nullptr;
+    s->ev_slot_d = nullptr;
+    s->ev_cap = 0;
+    RSV_HIP_TRY(hipMalloc((void**)&s->ev_pos_d, cap * 8));
+    RSV_HIP_TRY(hipMalloc((void**)&s->ev_slot_d, cap * 4));
+    s->ev_cap = cap;
+    return RSV_OK;
+}
+
+// one batch of n keys already in device memory, at global indices [count, count+n)
+rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t* hashes, int64_t n) {
+    if (n <= 0) return RSV_OK;
+    const int64_t base = s->count;
+    if (s->cfg.kind == RSV_KIND_DISTINCT) {
+        int rc = distinct_sample_device(s->distinct, keys, hashes, n, s->stream);
+        if (rc != RSV_OK) return (rsv_status)rc;
+    } else if (s->cfg.engine == RSV_ENGINE_JAVA_L) {
+        s->ev_pos_h.clear();
+        s->ev_slot_h.clear();
+        s->algo_l.events(base, n, s->ev_pos_h, s->ev_slot_h);
+        const int64_t ne = (int64_t)s->ev_pos_h.size();
+        if (ne) {
+            if (rsv_status st = ensure_events(s, ne)) return st;
+            RSV_HIP_TRY(hipMemcpyAsync(s->ev_pos_d, s->ev_pos_h.data(), ne * 8, hipMemcpyHostToDevice, s->stream));
+            RSV_HIP_TRY(hipMemcpyAsync(s->ev_slot_d, s->ev_slot_h.data(), ne * 4, hipMemcpyHostToDevice, s->stream));
+            s->timer.mark(s->stream);
+            RSV_HIP_TRY(launch_replay_events(s->ev_pos_d, s->ev_slot_d, ne, s->k, s->batch_win, s->stream));
+            s->timer.mark(s->stream);
+        }
+        RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, s->stream));
+        if (ne) RSV_HIP_TRY(hipStreamSynchronize(s->stream));  // host event vectors are reused
+    } else {
+        const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
+        const uint64_t lo = std::max<uint64_t>((uint64_t)base, s->k), hi = (uint64_t)(base + n);
+        s->timer.mark(s->stream);
+        RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
+        s->timer.mark(s->stream);
+        RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, s->stream));
+    }
+    s->count = base + n;
+    return RSV_OK;
+}
+
+rsv_status ensure_chunk(rsv_sampler* s) {
+    if (s->chunk_d) return RSV_OK;
+    RSV_HIP_TRY(hipMalloc(&s->chunk_d, kChunkKeys * s->kw));
+    if (s->cfg.kind == RSV_KIND_DISTINCT && s->hash_kind == kHashPrecomputed)
+        RSV_HIP_TRY(hipMalloc((void**)&s->chunk_hash_d, kChunkKeys * 8));
+    s->chunk_cap = kChunkKeys;
+    return RSV_OK;
+}
+
+rsv_status process_host_batch(rsv_sampler* s, const void* keys, const int64_t* hashes, int64_t n) {
+    if (n <= 0) return RSV_OK;
+    if (rsv_status st = ensure_chunk(s)) return st;
+    for (int64_t off = 0; off < n; off += s->chunk_cap) {
+        const int64_t c = std::min(s->chunk_cap, n - off);
+        RSV_HIP_TRY(hipMemcpyAsync(s->chunk_d, (const uint8_t*)keys + off * s->kw, c * s->kw,
+                                   hipMemcpyHostToDevice, s->stream));
+        if (s->chunk_hash_d && hashes)
+            RSV_HIP_TRY(hipMemcpyAsync(s->chunk_hash_d, hashes + off, c * 8, hipMemcpyHostToDevice, s->stream));
+        if (rsv_status st = process_device_batch(s, s->chunk_d, s->chunk_hash_d, c)) return st;
+    }
+    // the caller may reuse its buffer after return (ownership stays with the caller)
+    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    return RSV_OK;
+}
+
+rsv_status flush_stage(rsv_sampler* s) {
+    if (s->stage_n == 0) return RSV_OK;
+    const int64_t n = s->stage_n;
+    s->stage_n = 0;
+    return process_host_batch(s, s->stage_h, s->stage_hash_h, n);
+}
+
+void free_all(rsv_sampler* s) {
+    void* ds[] = {s->slot_key, s->slot_idx, s->batch_win, s->ev_pos_d, s->ev_slot_d, s->chunk_d,
+                  s->chunk_hash_d};
+    for (void* p : ds)
+        if (p) (void)hipFree(p);
+    if (s->stage_h) (void)hipHostFree(s->stage_h);
+    if (s->stage_hash_h) (void)hipHostFree(s->stage_hash_h);
+    if (s->distinct) distinct_destroy(s->distinct);
+    if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
+}
+
+int resolve_hash_kind(int32_t hk, int kw) {
+    switch (hk) {
+    case RSV_HASH_IDENTITY: return kHashIdentity;
+    case RSV_HASH_JAVA_LONG: return kHashJavaLong;
+    case RSV_HASH_JAVA_INT: return kHashJavaInt;
+    case RSV_HASH_PRECOMPUTED: return kHashPrecomputed;
+    default: return kw == 4 ? kHashJavaInt : kHashJavaLong;  // B#hashCode (Sampler.scala:75)
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t rsv_abi_version(void) { return RSV_ABI_VERSION; }
+
+const char* rsv_last_error(void) { return g_last_error.c_str(); }
+
+const char* rsv_status_string(rsv_status s) {
+    switch (s) {
+    case RSV_OK: return "ok";
+    case RSV_E_ILLEGAL_ARGUMENT: return "illegal argument";
+    case RSV_E_ILLEGAL_STATE: return "illegal state";
+    case RSV_E_NULL_POINTER: return "null pointer";
+    case RSV_E_DEVICE: return "device error";
+    case RSV_E_OUT_OF_MEMORY: return "out of memory";
+    case RSV_E_UNSUPPORTED: return "unsupported";
+    }
+    return "unknown status";
+}
+
+rsv_status rsv_config_init(rsv_config* cfg) {
+    if (!cfg) return fail(RSV_E_NULL_POINTER, "config is NULL");
+    memset(cfg, 0, sizeof(*cfg));
+    cfg->struct_size = sizeof(rsv_config);
+    cfg->kind = RSV_KIND_ELEMENTS;
+    cfg->max_sample_size = 1;
+    cfg->key_width = 8;
+    cfg->engine = RSV_ENGINE_PHILOX_R;
+    cfg->hash_kind = RSV_HASH_DEFAULT;
+    cfg->device = -1;
+    return RSV_OK;
+}
+
+rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out) {
+    if (!cfg || !out) return fail(RSV_E_NULL_POINTER, "config/out is NULL");
+    *out = nullptr;
+    if (cfg->struct_size != sizeof(rsv_config))
+        return fail(RSV_E_ILLEGAL_ARGUMENT, "rsv_config.struct_size mismatch (ABI version)");
+    // validateSharedParams, Sampler.scala:79-83
+    if (cfg->max_sample_size > kMaxSize) return fail(RSV_E_ILLEGAL_ARGUMENT, "maxSampleSize exceeds VM limit");
+    if (cfg->max_sample_size <= 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "maxSampleSize must be positive");
+    if (cfg->key_width != 4 && cfg->key_width != 8)
+        return fail(RSV_E_ILLEGAL_ARGUMENT, "key_width must be 4 or 8");
+    if (cfg->kind != RSV_KIND_ELEMENTS && cfg->kind != RSV_KIND_DISTINCT)
+        return fail(RSV_E_ILLEGAL_ARGUMENT, "unknown sampler kind");
+    if (cfg->kind == RSV_KIND_ELEMENTS && cfg->engine != RSV_ENGINE_PHILOX_R && cfg->engine != RSV_ENGINE_JAVA_L)
+        return fail(RSV_E_ILLEGAL_ARGUMENT, "unknown engine");
+    if (cfg->hash_kind < RSV_HASH_DEFAULT || cfg->hash_kind > RSV_HASH_PRECOMPUTED)
+        return fail(RSV_E_ILLEGAL_ARGUMENT, "unknown hash kind");
+
+    rsv_sampler* s = new rsv_sampler();
+    s->cfg = *cfg;
+    s->kw = cfg->key_width;
+    s->k = (uint32_t)cfg->max_sample_size;
+    int dev = cfg->device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+    s->device = dev;
+    DeviceGuard g(dev);
+    auto bail = [&](rsv_status st, const std::string& msg) {
+        free_all(s);
+        delete s;
+        return fail(st, msg);
+    };
+    hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return bail(RSV_E_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    s->own_stream = true;
+    if (cfg->kind == RSV_KIND_ELEMENTS) {
+        const size_t k = s->k;
+        e = hipMalloc(&s->slot_key, k * s->kw);
+        if (e == hipSuccess) e = hipMalloc((void**)&s->slot_idx, k * 8);
+        if (e == hipSuccess) e = hipMalloc((void**)&s->batch_win, k * 8);
+        if (e == hipSuccess) e = hipMemsetAsync(s->slot_key, 0, k * s->kw, s->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(s->slot_idx, 0xFF, k * 8, s->stream);  // -1 = empty
+        if (e == hipSuccess) e = hipMemsetAsync(s->batch_win, 0, k * 8, s->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+        if (e != hipSuccess)
+            return bail(e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE,
+                        std::string("allocating reservoir: ") + hipGetErrorString(e));
+        if (cfg->engine == RSV_ENGINE_JAVA_L) s->algo_l.init((int32_t)s->k, (int64_t)cfg->seed);
+    } else {
+        // RandomValues r0, r1 (Sampler.scala:385-388) from java.util.Random(seed)
+        JavaRandom r;
+        r.init((int64_t)cfg->seed);
+        const int64_t r0 = r.next_long(), r1 = r.next_long();
+        s->hash_kind = resolve_hash_kind(cfg->hash_kind, s->kw);
+        int st = RSV_OK;
+        s->distinct = distinct_create((int32_t)s->k, s->kw, s->hash_kind, r0, r1, &st);
+        if (!s->distinct) {
+            std::string msg = g_last_error;
+            return bail((rsv_status)st, msg);
+        }
+        distinct_set_timer(s->distinct, &s->timer);
+    }
+    *out = s;
+    return RSV_OK;
+}
+
+void rsv_destroy(rsv_sampler* s) {
+    if (!s) return;
+    DeviceGuard g(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    free_all(s);
+    delete s;
+}
+
+rsv_status rsv_sample(rsv_sampler* s, const void* key, const int64_t* hash) {
+    if (rsv_status st = check_open(s)) return st;
+    if (!key) return fail(RSV_E_NULL_POINTER, "key is NULL");
+    const bool pre = s->cfg.kind == RSV_KIND_DISTINCT && s->hash_kind == kHashPrecomputed;
+    if (pre && !hash) return fail(RSV_E_NULL_POINTER, "hash is NULL for RSV_HASH_PRECOMPUTED");
+    DeviceGuard g(s->device);
+    if (!s->stage_h) {
+        RSV_HIP_TRY(hipHostMalloc((void**)&s->stage_h, kStageKeys * s->kw, hipHostMallocDefault));
+        if (pre) RSV_HIP_TRY(hipHostMalloc((void**)&s->stage_hash_h, kStageKeys * 8, hipHostMallocDefault));
+        s->stage_cap = kStageKeys;
+    }
+    memcpy(s->stage_h + s->stage_n * s->kw, key, s->kw);
+    if (pre) s->stage_hash_h[s->stage_n] = *hash;
+    if (++s->stage_n == s->stage_cap) return flush_stage(s);
+    return RSV_OK;
+}
+
+rsv_status rsv_sample_batch(rsv_sampler* s, const void* keys, int64_t n, int32_t mem, const int64_t* hashes) {
+    if (rsv_status st = check_open(s)) return st;
+    if (n < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative batch size");
+    if (n == 0) return RSV_OK;
+    if (!keys) return fail(RSV_E_NULL_POINTER, "keys is NULL");
+    const bool pre = s->cfg.kind == RSV_KIND_DISTINCT && s->hash_kind == kHashPrecomputed;
+    if (pre && !hashes) return fail(RSV_E_NULL_POINTER, "hashes is NULL for RSV_HASH_PRECOMPUTED");
+    DeviceGuard g(s->device);
+    if (rsv_status st = flush_stage(s)) return st;  // keep global index order
+    if (mem == RSV_MEM_DEVICE) return process_device_batch(s, keys, pre ? hashes : nullptr, n);
+    if (mem == RSV_MEM_HOST) return process_host_batch(s, keys, pre ? hashes : nullptr, n);
+    return fail(RSV_E_ILLEGAL_ARGUMENT, "mem must be RSV_MEM_HOST or RSV_MEM_DEVICE");
+}
+
+static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* out_n, bool device_out) {
+    if (rsv_status st = check_open(s)) return st;
+    if (!out_n) return fail(RSV_E_NULL_POINTER, "out_n is NULL");
+    DeviceGuard g(s->device);
+    if (rsv_status st = flush_stage(s)) return st;
+    int64_t m;
+    const void* src;
+    if (s->cfg.kind == RSV_KIND_DISTINCT) {
+        m = distinct_size(s->distinct);
+        if (m > cap) return fail(RSV_E_ILLEGAL_ARGUMENT, "result buffer too small");
+        if (m && !out) return fail(RSV_E_NULL_POINTER, "out is NULL");
+        if (m) {
+            if (device_out) {
+                if (int rc = distinct_export(s->distinct, out, nullptr, s->stream)) return (rsv_status)rc;
+            } else {
+                // stage through the chunk buffer-free path: export to device scratch then copy
+                void* tmp = nullptr;
+                RSV_HIP_TRY(hipMalloc(&tmp, m * s->kw));
+                int rc = distinct_export(s->distinct, tmp, nullptr, s->stream);
+                hipError_t e = hipMemcpyAsync(out, tmp, m * s->kw, hipMemcpyDeviceToHost, s->stream);
+                hipError_t e2 = hipStreamSynchronize(s->stream);
+                (void)hipFree(tmp);
+                if (rc) return (rsv_status)rc;
+                RSV_HIP_TRY(e);
+                RSV_HIP_TRY(e2);
+            }
+        }
+        src = nullptr;
+    } else {
+        m = std::min<int64_t>(s->count, (int64_t)s->k);  // resultImpl, Sampler.scala:318-331
+        if (m > cap) return fail(RSV_E_ILLEGAL_ARGUMENT, "result buffer too small");
+        if (m && !out) return fail(RSV_E_NULL_POINTER, "out is NULL");
+        src = s->slot_key;
+        if (m) {
+            RSV_HIP_TRY(hipMemcpyAsync(out, src, m * s->kw,
+                                       device_out ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s->stream));
+        }
+    }
+    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    *out_n = m;
+    if (!s->cfg.reusable) s->open = false;  // SingleUse.close, Sampler.scala:188-191, :345-350
+    return RSV_OK;
+}
+
+rsv_status rsv_result(rsv_sampler* s, void* out, int64_t cap, int64_t* out_n) {
+    return result_impl(s, out, cap, out_n, false);
+}
+
+rsv_status rsv_result_device(rsv_sampler* s, void* out_dev, int64_t cap, int64_t* out_n) {
+    return result_impl(s, out_dev, cap, out_n, true);
+}
+
+int32_t rsv_is_open(const rsv_sampler* s) { return s && s->open ? 1 : 0; }
+
+int64_t rsv_count(const rsv_sampler* s) { return s ? s->count + s->stage_n : 0; }
+
+rsv_status rsv_set_stream(rsv_sampler* s, void* hip_stream) {
+    if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
+    DeviceGuard g(s->device);
+    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    if (s->own_stream) (void)hipStreamDestroy(s->stream);
+    s->stream = (hipStream_t)hip_stream;
+    s->own_stream = false;
+    return RSV_OK;
+}
+
+void* rsv_get_stream(const rsv_sampler* s) { return s ? (void*)s->stream : nullptr; }
+
+rsv_status rsv_synchronize(rsv_sampler* s) {
+    if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
+    DeviceGuard g(s->device);
+    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    return RSV_OK;
+}
+
+rsv_status rsv_profile_enable(rsv_sampler* s, int32_t on) {
+    if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
+    s->timer.on = on != 0;
+    return RSV_OK;
+}
+
+rsv_status rsv_profile_read(rsv_sampler* s, double* total_ms, int64_t* launches) {
+    if (!s || !total_ms || !launches) return fail(RSV_E_NULL_POINTER, "NULL argument");
+    DeviceGuard g(s->device);
+    RSV_HIP_TRY(s->timer.drain());
+    *total_ms = s->timer.total_ms;
+    *launches = s->timer.launches;
+    return RSV_OK;
+}
+
+rsv_status rsv_seek(rsv_sampler* s, int64_t index) {
+    if (rsv_status st = check_open(s)) return st;
+    if (s->cfg.kind != RSV_KIND_ELEMENTS || s->cfg.engine != RSV_ENGINE_PHILOX_R)
+        return fail(RSV_E_UNSUPPORTED, "rsv_seek needs an ELEMENTS sampler on RSV_ENGINE_PHILOX_R");
+    DeviceGuard g(s->device);
+    if (rsv_status st = flush_stage(s)) return st;
+    if (index < s->count) return fail(RSV_E_ILLEGAL_ARGUMENT, "rsv_seek cannot move backwards");
+    s->count = index;
+    return RSV_OK;
+}
+
+rsv_status rsv_export_state(rsv_sampler* s, int64_t* idx_dev, void* keys_dev, int64_t* hash_dev,
+                            int64_t* out_n) {
+    if (rsv_status st = check_open(s)) return st;
+    if (!out_n) return fail(RSV_E_NULL_POINTER, "out_n is NULL");
+    DeviceGuard g(s->device);
+    if (rsv_status st = flush_stage(s)) return st;
+    if (s->cfg.kind == RSV_KIND_DISTINCT) {
+        if (int rc = distinct_export(s->distinct, keys_dev, hash_dev, s->stream)) return (rsv_status)rc;
+        *out_n = distinct_size(s->distinct);
+    } else {
+        if (idx_dev) RSV_HIP_TRY(hipMemcpyAsync(idx_dev, s->slot_idx, s->k * 8ull, hipMemcpyDeviceToDevice, s->stream));
+        if (keys_dev)
+            RSV_HIP_TRY(hipMemcpyAsync(keys_dev, s->slot_key, (size_t)s->k * s->kw, hipMemcpyDeviceToDevice, s->stream));
+        *out_n = s->k;
+    }
+    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    return RSV_OK;
+}
+
+rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* keys_dev, const int64_t* hash_dev,
+                           const int64_t* part_n_host, int32_t parts, int64_t part_len, int64_t total_count) {
+    if (rsv_status st = check_open(s)) return st;
+    if (parts < 0 || part_len < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative parts/part_len");
+    if (parts > 0 && !keys_dev) return fail(RSV_E_NULL_POINTER, "keys_dev is NULL");
+    DeviceGuard g(s->device);
+    if (rsv_status st = flush_stage(s)) return st;
+    if (s->cfg.kind == RSV_KIND_DISTINCT) {
+        if (parts > 0 && (!hash_dev || !part_n_host)) return fail(RSV_E_NULL_POINTER, "hash_dev/part_n is NULL");
+        for (int32_t p = 0; p < parts; ++p) {
+            const int64_t n = std::min(part_n_host[p], part_len);
+            int rc = distinct_merge(s->distinct, (const uint8_t*)keys_dev + (size_t)p * part_len * s->kw,
+                                    hash_dev + (size_t)p * part_len, n, s->stream);
+            if (rc) return (rsv_status)rc;
+        }
+    } else {
+        if (part_len < (int64_t)s->k) return fail(RSV_E_ILLEGAL_ARGUMENT, "part_len < k");
+        if (parts > 0 && !idx_dev) return fail(RSV_E_NULL_POINTER, "idx_dev is NULL");
+        RSV_HIP_TRY(launch_merge_slots(idx_dev, keys_dev, s->kw, parts, part_len, s->k, s->slot_idx, s->slot_key,
+                                       s->stream));
+    }
+    if (total_count > s->count) s->count = total_count;
+    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    return RSV_OK;
+}
+
+rsv_status rsv_sample_segmented(const void* keys_dev, const int64_t* offsets_dev, int64_t num_streams,
+                                int32_t key_width, int32_t k, uint64_t seed, uint64_t stream_base, void* out_dev,
+                                int64_t* counts_dev, void* hip_stream) {
+    if (k <= 0 || k > kMaxSize) return fail(RSV_E_ILLEGAL_ARGUMENT, "k out of range");
+    if (key_width != 4 && key_width != 8) return fail(RSV_E_ILLEGAL_ARGUMENT, "key_width must be 4 or 8");
+    if (num_streams < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative stream count");
+    if (num_streams == 0) return RSV_OK;
+    if (!offsets_dev || !out_dev || !counts_dev) return fail(RSV_E_NULL_POINTER, "NULL buffer");
+    const size_t lds = (size_t)segmented_waves_per_block((uint32_t)k) * (size_t)k * 8;
+    if (lds > 160 * 1024)
+        return fail(RSV_E_UNSUPPORTED, "segmented sampling keeps each stream's k slots in LDS: k <= 20480");
+    const DrawParams dp{seed, stream_base};
+    RSV_HIP_TRY(launch_segmented(keys_dev, key_width, offsets_dev, num_streams, (uint32_t)k, dp, out_dev, counts_dev,
+                                 (hipStream_t)hip_stream));
+    return RSV_OK;
+}
+
+rsv_status rsv_replay_events(const void* keys_dev, int64_t n, int32_t key_width, int64_t base_index,
+                             const int64_t* ev_pos_dev, const int32_t* ev_slot_dev, int64_t n_events, int32_t k,
+                             void* reservoir_dev, void* hip_stream) {
+    if (k <= 0 || k > kMaxSize) return fail(RSV_E_ILLEGAL_ARGUMENT, "k out of range");
+    if (key_width != 4 && key_width != 8) return fail(RSV_E_ILLEGAL_ARGUMENT, "key_width must be 4 or 8");
+    if (n < 0 || n_events < 0 || base_index < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative size");
+    if (!reservoir_dev || (n && !keys_dev) || (n_events && (!ev_pos_dev || !ev_slot_dev)))
+        return fail(RSV_E_NULL_POINTER, "NULL buffer");
+    hipStream_t st = (hipStream_t)hip_stream;
+    unsigned long long* win = nullptr;
+    RSV_HIP_TRY(hipMallocAsync((void**)&win, (size_t)k * 8, st));
+    hipError_t e = hipMemsetAsync(win, 0, (size_t)k * 8, st);
+    if (e == hipSuccess) e = launch_replay_events(ev_pos_dev, ev_slot_dev, n_events, (uint32_t)k, win, st);
+    if (e == hipSuccess) e = launch_resolve(keys_dev, key_width, base_index, n, (uint32_t)k, win, reservoir_dev, nullptr, st);
+    hipError_t e2 = hipFreeAsync(win, st);
+    RSV_HIP_TRY(e);
+    RSV_HIP_TRY(e2);
+    return RSV_OK;
+}
+
+rsv_status rsv_export_draws(uint64_t seed, uint64_t stream_id, uint64_t i0, int64_t n, uint64_t* j_dev,
+                            void* hip_stream) {
+    if (n < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative n");
+    if (n && !j_dev) return fail(RSV_E_NULL_POINTER, "j_dev is NULL");
+    const DrawParams dp{seed, stream_id};
+    RSV_HIP_TRY(launch_export_draws(dp, i0, n, j_dev, (hipStream_t)hip_stream));
+    return RSV_OK;
+}
+
+}  // extern "C"

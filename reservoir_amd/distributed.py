@@ -1,0 +1,58 @@
+"""Multi-GPU sampling: one process per GPU, torch.distributed (RCCL over xGMI) for the one exchange.
+
+The reference has no multi-device story.  Two shardings are exact here:
+
+* one giant stream of an element sampler ("philox_r"): rank r samples its contiguous index
+  range [offset_r, offset_r + n_r) after ``seek(offset_r)``; because a draw depends only on
+  (seed, stream, global index), the union of the per-rank last writers, taken per slot by the
+  largest global index, is bit-identical to one sampler fed the whole stream.
+* a distinct sampler: bottom-k is mergeable, any split of the elements works.
+
+``combine`` is the only collective: every rank exports its k-slot partial state, one
+``all_gather_into_tensor`` moves it (k x 16 B per rank: latency-bound, not link-bound), and each
+rank merges all parts with the engine's merge kernel.  Independent streams (segmented sampling)
+need no collective at all.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n_total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous index range [lo, hi) of rank ``rank`` for a stream of ``n_total`` elements."""
+    base, rem = divmod(n_total, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def sample_shard(sampler, keys_local, global_offset: int) -> None:
+    """Sample this rank's shard of one stream (keys at [global_offset, +len))."""
+    if not sampler.is_distinct:
+        sampler.seek(global_offset)
+    sampler.sample_all(keys_local)
+
+
+def combine(sampler, group=None, device=None) -> None:
+    """All-gather the partial states of every rank and merge them into ``sampler`` (on all ranks)."""
+    world = dist.get_world_size(group)
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+    idx, keys, hashes, n = sampler.export_state(device)
+    k = keys.numel()
+    g_idx = torch.empty((world, k), dtype=idx.dtype, device=idx.device)
+    g_keys = torch.empty((world, k), dtype=keys.dtype, device=keys.device)
+    g_hash = torch.empty((world, k), dtype=hashes.dtype, device=hashes.device)
+    meta = torch.tensor([n, sampler.count], dtype=torch.int64, device=idx.device)
+    g_meta = torch.empty((world, 2), dtype=torch.int64, device=idx.device)
+    if sampler.is_distinct:
+        dist.all_gather_into_tensor(g_hash, hashes, group=group)
+    else:
+        dist.all_gather_into_tensor(g_idx, idx, group=group)
+    dist.all_gather_into_tensor(g_keys, keys, group=group)
+    dist.all_gather_into_tensor(g_meta, meta, group=group)
+    m = g_meta.cpu()
+    part_n = m[:, 0].tolist()
+    # elements: the stream ends at the largest rank end; distinct: counts add up
+    total = int(m[:, 1].sum()) if sampler.is_distinct else int(m[:, 1].max())
+    sampler.merge_state(g_idx, g_keys, g_hash, part_n, total)

@@ -1,0 +1,291 @@
+"""Host-side mirror of ``lgbt.princess.reservoir.Sampler`` over the HIP engine.
+
+Reference: core/src/main/scala/lgbt/princess/reservoir/Sampler.scala (NthPortal/reservoir).
+
+    Sampler(max_sample_size, pre_allocate=False, reusable=False)(map)      # Sampler.apply  :128-136
+    Sampler.distinct(max_sample_size, reusable=False)(map, hash=default)   # Sampler.distinct :171-180
+
+    s.sample(x)        # Sampler.sample    :37-38
+    s.sample_all(xs)   # Sampler.sampleAll :49-50
+    s.result()         # Sampler.result    :59-60
+    s.is_open          # Sampler.isOpen    :67
+
+Names, argument meaning and exceptions follow the reference (IllegalArgumentException for a
+bad size, NullPointerException for a missing ``map``/``hash``, IllegalStateException after
+``result()`` on a single-use sampler).  ``map`` runs on the host (the reference allows it to be
+called more than ``maxSampleSize`` times, Sampler.scala:115-116); the extracted primitive keys go
+to the GPU in batches.  Keys already resident in HBM (a torch CUDA tensor) are sampled in place.
+
+Extensions (keyword-only, defaulted so reference-style calls are unchanged):
+    key_type  "long" (B = Long, 8-byte keys, default) or "int" (B = Int, 4-byte keys)
+    engine    "philox_r" (default: data-parallel Algorithm R) or "java_l" (the reference's own
+              Algorithm L over java.util.Random(seed): bit-identical results to the reference)
+    seed      RNG seed (default: fresh entropy, like ``new Random()`` at Sampler.scala:199)
+    stream_id Philox stream of a "philox_r" sampler
+    device    HIP device ordinal (default: current device)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Any, Callable, Iterable
+
+import numpy as np
+
+from . import _native as N
+from ._native import IllegalArgumentException, IllegalStateException, NullPointerException
+
+MAX_SIZE = 2**31 - 1 - 2  # Sampler.scala:71
+
+
+def identity(x):
+    return x
+
+
+_KEY = {"long": (8, np.int64), "int": (4, np.int32)}
+_ENGINE = {"philox_r": N.ENGINE_PHILOX_R, "java_l": N.ENGINE_JAVA_L}
+
+
+def _fresh_seed() -> int:
+    return int.from_bytes(os.urandom(8), "little")
+
+
+def _validate_shared(max_sample_size: int, map_fn) -> None:
+    # validateSharedParams, Sampler.scala:79-83
+    if max_sample_size > MAX_SIZE:
+        raise IllegalArgumentException("requirement failed: maxSampleSize exceeds VM limit")
+    if max_sample_size <= 0:
+        raise IllegalArgumentException("requirement failed: maxSampleSize must be positive")
+    if map_fn is None:
+        raise NullPointerException("`map` cannot be `null`")
+
+
+def _is_torch_cuda(x) -> bool:
+    t = type(x)
+    return t.__module__.startswith("torch") and t.__name__ == "Tensor" and getattr(x, "is_cuda", False)
+
+
+class GpuSampler:
+    """A ``Sampler[A, B]`` whose state lives on an MI355X (one opaque C-ABI handle)."""
+
+    def __init__(self, kind: int, max_sample_size: int, map_fn: Callable, *, reusable: bool,
+                 pre_allocate: bool = False, hash_fn=None, hash_kind: int = N.HASH_DEFAULT,
+                 key_type: str = "long", engine: str = "philox_r", seed: int | None = None,
+                 stream_id: int = 0, device: int | None = None):
+        if key_type not in _KEY:
+            raise IllegalArgumentException(f"key_type must be one of {sorted(_KEY)}")
+        if engine not in _ENGINE:
+            raise IllegalArgumentException(f"engine must be one of {sorted(_ENGINE)}")
+        self._L = N.load()
+        self._map = map_fn
+        self._hash_fn = hash_fn
+        self._width, self._dtype = _KEY[key_type]
+        self._kind = kind
+        self._k = max_sample_size
+        cfg = N.RsvConfig()
+        N.check(self._L.rsv_config_init(C.byref(cfg)))
+        cfg.kind = kind
+        cfg.max_sample_size = max_sample_size
+        cfg.key_width = self._width
+        cfg.reusable = 1 if reusable else 0
+        cfg.pre_allocate = 1 if pre_allocate else 0
+        cfg.engine = _ENGINE[engine]
+        cfg.hash_kind = hash_kind
+        cfg.device = -1 if device is None else int(device)
+        cfg.seed = (_fresh_seed() if seed is None else int(seed)) & (2**64 - 1)
+        cfg.stream_id = int(stream_id) & (2**64 - 1)
+        self.seed = cfg.seed
+        h = C.c_void_p()
+        N.check(self._L.rsv_create(C.byref(cfg), C.byref(h)))
+        self._h = h
+        self._precomputed = hash_kind == N.HASH_PRECOMPUTED
+
+    # -- lifecycle ----------------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.rsv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    @property
+    def is_open(self) -> bool:
+        return bool(self._L.rsv_is_open(self._h))
+
+    isOpen = is_open
+
+    @property
+    def count(self) -> int:
+        return int(self._L.rsv_count(self._h))
+
+    @property
+    def stream(self) -> int:
+        return int(self._L.rsv_get_stream(self._h) or 0)
+
+    def set_stream(self, hip_stream: int) -> None:
+        N.check(self._L.rsv_set_stream(self._h, C.c_void_p(hip_stream)))
+
+    def synchronize(self) -> None:
+        N.check(self._L.rsv_synchronize(self._h))
+
+    # -- Sampler trait --------------------------------------------------------------------------
+    def _key_hash(self, element):
+        key = self._map(element)
+        hv = None
+        if self._precomputed:
+            hv = C.c_int64(int(self._hash_fn(key)))
+        return key, hv
+
+    def sample(self, element: Any) -> None:
+        """Sampler.sample (Sampler.scala:37-38)."""
+        if not self._L.rsv_is_open(self._h):
+            raise IllegalStateException("use of sampler after calling `result()`")
+        key, hv = self._key_hash(element)
+        kbuf = self._dtype(key).tobytes() if not isinstance(key, (bytes, bytearray)) else key
+        N.check(self._L.rsv_sample(self._h, C.c_char_p(kbuf),
+                                   C.byref(hv) if hv is not None else None))
+
+    def sample_all(self, elements: Iterable) -> None:
+        """Sampler.sampleAll (Sampler.scala:49-50): same result as sample() on each element."""
+        if not self._L.rsv_is_open(self._h):
+            raise IllegalStateException("use of sampler after calling `result()`")
+        if _is_torch_cuda(elements) and self._map is identity and not self._precomputed:
+            import torch
+
+            t = elements.contiguous()
+            cur = torch.cuda.current_stream(t.device)
+            if cur.cuda_stream != self.stream:
+                cur.synchronize()  # the tensor was produced on torch's stream
+            if t.element_size() != self._width:
+                raise IllegalArgumentException("device tensor dtype does not match key_type")
+            N.check(self._L.rsv_sample_batch(self._h, C.c_void_p(t.data_ptr()), t.numel(),
+                                             N.MEM_DEVICE, None))
+            return
+        if isinstance(elements, np.ndarray) and self._map is identity:
+            keys = np.ascontiguousarray(elements, dtype=self._dtype)
+        else:
+            keys = np.fromiter((self._map(x) for x in elements), dtype=self._dtype)
+        hashes = None
+        if self._precomputed:
+            hashes = np.ascontiguousarray(
+                np.fromiter((int(self._hash_fn(k)) for k in keys.tolist()), dtype=np.int64,
+                            count=keys.size))
+        N.check(self._L.rsv_sample_batch(
+            self._h, keys.ctypes.data_as(C.c_void_p), keys.size, N.MEM_HOST,
+            hashes.ctypes.data_as(C.c_void_p) if hashes is not None else None))
+
+    sampleAll = sample_all
+
+    def result(self) -> np.ndarray:
+        """Sampler.result (Sampler.scala:59-60). Slot order for element samplers."""
+        if not self._L.rsv_is_open(self._h):
+            raise IllegalStateException("use of sampler after calling `result()`")
+        out = np.empty(self._k, dtype=self._dtype)
+        n = C.c_int64(0)
+        N.check(self._L.rsv_result(self._h, out.ctypes.data_as(C.c_void_p), self._k, C.byref(n)))
+        return out[: n.value].copy()
+
+    def result_device(self, out_tensor) -> int:
+        """Write the result into a device tensor (no host round trip); returns its length."""
+        n = C.c_int64(0)
+        N.check(self._L.rsv_result_device(self._h, C.c_void_p(out_tensor.data_ptr()),
+                                          out_tensor.numel(), C.byref(n)))
+        return n.value
+
+    # -- multi-GPU helpers (reservoir_amd.distributed) ------------------------------------------
+    @property
+    def is_distinct(self) -> bool:
+        return self._kind == N.KIND_DISTINCT
+
+    @property
+    def max_sample_size(self) -> int:
+        return self._k
+
+    @property
+    def key_dtype(self):
+        return self._dtype
+
+    def seek(self, index: int) -> None:
+        """Next element has global index ``index`` (index-range split across ranks)."""
+        N.check(self._L.rsv_seek(self._h, int(index)))
+
+    def export_state(self, device):
+        """Partial state as device tensors (idx[k], keys[k], hashes[k], n)."""
+        import torch
+
+        tdt = torch.int64 if self._width == 8 else torch.int32
+        idx = torch.full((self._k,), -1, dtype=torch.int64, device=device)
+        keys = torch.zeros(self._k, dtype=tdt, device=device)
+        hashes = torch.zeros(self._k, dtype=torch.int64, device=device)
+        n = C.c_int64(0)
+        N.check(self._L.rsv_export_state(self._h, C.c_void_p(idx.data_ptr()),
+                                         C.c_void_p(keys.data_ptr()), C.c_void_p(hashes.data_ptr()),
+                                         C.byref(n)))
+        return idx, keys, hashes, n.value
+
+    def merge_state(self, idx, keys, hashes, part_n, total_count: int) -> None:
+        """Merge gathered partial states ([parts, k] device tensors) into this sampler."""
+        parts = int(keys.shape[0])
+        pn = np.ascontiguousarray(np.asarray(part_n, dtype=np.int64))
+        N.check(self._L.rsv_merge_state(
+            self._h, C.c_void_p(idx.data_ptr()), C.c_void_p(keys.data_ptr()),
+            C.c_void_p(hashes.data_ptr()), pn.ctypes.data_as(C.c_void_p), parts,
+            int(keys.shape[1]), int(total_count)))
+
+
+def Sampler(max_sample_size: int, pre_allocate: bool = False, reusable: bool = False, **ext):
+    """``Sampler.apply`` (Sampler.scala:128-136): ``Sampler(k)(map)``."""
+
+    def make(map_fn: Callable = identity) -> GpuSampler:
+        _validate_shared(max_sample_size, map_fn)  # validateNonDistinctParams :85-88
+        return GpuSampler(N.KIND_ELEMENTS, max_sample_size, map_fn, reusable=reusable,
+                          pre_allocate=pre_allocate, **ext)
+
+    return make
+
+
+_DEFAULT_HASH = object()
+
+
+def _resolve_hash(hash):
+    """validateDistinctParams (Sampler.scala:90-95) + mapping onto rsv_hash_kind."""
+    if hash is None:
+        raise NullPointerException("`hash` cannot be `null`")
+    if hash is _DEFAULT_HASH:
+        return N.HASH_DEFAULT, None
+    if isinstance(hash, str):
+        kinds = {"identity": N.HASH_IDENTITY, "java_long": N.HASH_JAVA_LONG, "java_int": N.HASH_JAVA_INT}
+        if hash not in kinds:
+            raise IllegalArgumentException(f"unknown hash kind {hash!r}")
+        return kinds[hash], None
+    if callable(hash):
+        return N.HASH_PRECOMPUTED, hash
+    raise IllegalArgumentException("hash must be callable or a known hash kind")
+
+
+def distinct(max_sample_size: int, reusable: bool = False, **ext):
+    """``Sampler.distinct`` (Sampler.scala:171-180): ``Sampler.distinct(k)(map, hash)``.
+
+    ``hash`` defaults to ``B#hashCode().toLong`` (Sampler.scala:75); pass ``"identity"`` for the
+    bijective Long identity hash, or any callable (evaluated on the host, shipped as int64).
+    """
+
+    def make(map_fn: Callable = identity, hash=_DEFAULT_HASH) -> GpuSampler:
+        _validate_shared(max_sample_size, map_fn)
+        hk, hf = _resolve_hash(hash)
+        return GpuSampler(N.KIND_DISTINCT, max_sample_size, map_fn, reusable=reusable,
+                          hash_fn=hf, hash_kind=hk, **ext)
+
+    return make
+
+
+Sampler.distinct = distinct  # type: ignore[attr-defined]
+Sampler.apply = Sampler  # type: ignore[attr-defined]

@@ -1,0 +1,221 @@
+"""Element sampler (Sampler.apply) on the GPU: parity with the oracle, boundaries, lifecycle.
+
+Parity contract P2: the "philox_r" engine equals the sequential Algorithm R
+restatement fed the same draw sequence (format R1), bit-exactly, for every batching and split.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+
+
+def _dev_keys(torch, cuda, keys):
+    return torch.from_numpy(np.ascontiguousarray(keys)).to(cuda)
+
+
+@pytest.mark.parametrize("case", GOLDEN["algo_r"], ids=lambda c: f"k{c['k']}_n{c['n']}")
+def test_golden_algo_r(cuda, oracle, case):
+    from reservoir_amd import Sampler
+
+    keys = oracle.splitmix_keys(case["key_base"], case["n"])
+    s = Sampler(case["k"], seed=case["seed"], stream_id=case["stream"])()
+    s.sample_all(keys)
+    assert s.result().tolist() == case["result"]
+
+
+@pytest.mark.parametrize("k", [1, 2, 5, 63, 64, 100, 1000, 1024, 4099])
+@pytest.mark.parametrize("n", [0, 1, 7, 1000, 65_537, 300_000])
+def test_parity_vs_oracle(cuda, oracle, k, n):
+    import torch
+
+    from reservoir_amd import Sampler
+
+    keys = oracle.splitmix_keys(k * 1000 + n, n)
+    want, _ = oracle.algo_r(0xABCDEF + k, n, k, keys)
+    s = Sampler(k, seed=0xABCDEF + k, stream_id=n)()
+    s.sample_all(_dev_keys(torch, cuda, keys))
+    got = s.result()
+    assert got.size == min(n, k)
+    assert np.array_equal(got, want[: got.size])
+
+
+def test_batching_and_memory_invariance(cuda, oracle):
+    """sample == sampleAll == any chunking, host or device memory (SamplerTest.scala:117-142)."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    n, k = 500_000, 1024
+    keys = oracle.splitmix_keys(5, n)
+    want, _ = oracle.algo_r(99, 1, k, keys)
+    rng = np.random.default_rng(0)
+    cuts = np.r_[0, np.sort(rng.choice(np.arange(1, n), 20, replace=False)), n]
+    s_dev = Sampler(k, seed=99, stream_id=1)()
+    s_host = Sampler(k, seed=99, stream_id=1)()
+    kd = _dev_keys(torch, cuda, keys)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        s_dev.sample_all(kd[a:b])
+        s_host.sample_all(keys[a:b])
+    assert np.array_equal(s_dev.result(), want)
+    assert np.array_equal(s_host.result(), want)
+    s_el = Sampler(k, seed=99, stream_id=1)()
+    for x in keys[:3000]:
+        s_el.sample(int(x))
+    s_el.sample_all(keys[3000:])
+    assert np.array_equal(s_el.result(), want)
+
+
+def test_int_keys_and_map(cuda, oracle):
+    from reservoir_amd import Sampler
+
+    xs = list(range(1, 20001))
+    s = Sampler(10, key_type="int", seed=3)(lambda x: x * 2)
+    s.sample_all(xs)
+    want, _ = oracle.algo_r(3, 0, 10, np.array(xs, dtype=np.int64) * 2)
+    assert s.result().tolist() == want.tolist()
+
+
+def test_draw_export_matches_oracle(cuda, oracle):
+    from reservoir_amd import batch
+
+    for case in GOLDEN["draws_r1"]:
+        j = batch.export_draws(case["seed"], case["stream"], case["i0"], case["n"]).cpu().numpy()
+        assert [int(x) for x in j.astype(np.uint64)] == case["j"]
+    j = batch.export_draws(17, 3, 10_000, 100_000).cpu().numpy().astype(np.uint64)
+    assert np.array_equal(j, oracle.export_draws(17, 3, 10_000, 100_000))
+
+
+def test_draw_replay_contract(cuda, oracle):
+    """north star: equal to a sequential sampler fed the exported per-element draw sequence."""
+    import torch
+
+    from reservoir_amd import Sampler, batch
+
+    n, k = 200_000, 256
+    keys = oracle.splitmix_keys(8, n)
+    j = batch.export_draws(42, 9, 0, n).cpu().numpy().astype(np.uint64)
+    want = oracle.algo_r_replay(k, j, keys)
+    s = Sampler(k, seed=42, stream_id=9)()
+    s.sample_all(torch.from_numpy(keys).to(cuda))
+    assert np.array_equal(s.result(), want)
+
+
+def test_boundaries_and_duplicates(cuda):
+    from reservoir_amd import Sampler
+
+    def run(k, xs):
+        s = Sampler(k, key_type="int")()
+        for x in xs:
+            s.sample(x)
+        return s.result().tolist()
+
+    assert sorted(run(5, range(1, 6))) == [1, 2, 3, 4, 5]  # SamplerTest.scala:81-83
+    assert sorted(run(6, range(1, 6))) == [1, 2, 3, 4, 5]  # :85-87
+    assert run(1, []) == []  # :89-91
+    assert run(10, [1] * 10) == [1] * 10  # :320-327
+
+
+def test_single_use_lifecycle(cuda):
+    from reservoir_amd import IllegalStateException, Sampler
+
+    s = Sampler(10)()
+    assert s.is_open
+    s.result()
+    assert not s.is_open  # SamplerTest.scala:263-267
+    with pytest.raises(IllegalStateException):
+        s.sample(1)  # :246-250
+    with pytest.raises(IllegalStateException):
+        s.result()  # :252-256
+
+
+def test_reusable_does_not_clobber(cuda):
+    """SamplerTest.scala:292-316."""
+    from reservoir_amd import Sampler
+
+    s = Sampler(64, reusable=True, key_type="int")()
+
+    def results():
+        res = s.result()
+        lst = res.tolist()
+        return res, s.result(), lst
+
+    outs = [results()]
+    for a, b in [(1, 32), (33, 64), (65, 128)]:
+        for x in range(a, b + 1):
+            s.sample(x)
+        outs.append(results())
+    for ra, rb, lst in outs:
+        assert np.array_equal(ra, rb) and ra.tolist() == lst
+    assert s.is_open
+    assert sorted(outs[2][0].tolist()) == list(range(1, 65))
+
+
+def test_statistics_sometimes_and_not_always(cuda):
+    """SamplerTest.scala:93-115 via independent samplers (fresh seeds)."""
+    from reservoir_amd import Sampler
+
+    res = [Sampler(5, key_type="int")() for _ in range(100)]
+    for s in res:
+        s.sample_all(range(1, 7))
+    got = [s.result().tolist() for s in res]
+    assert any(6 in g for g in got) and any(6 not in g for g in got)
+
+
+def test_index_range_split_merge(cuda, oracle):
+    """Multi-GPU contract on one device: shards sampled after seek(offset), merged per slot."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    n, k, parts = 1_000_003, 1024, 5
+    keys = oracle.splitmix_keys(31, n)
+    want, _ = oracle.algo_r(7, 2, k, keys)
+    kd = torch.from_numpy(keys).to(cuda)
+    bounds = np.linspace(0, n, parts + 1).astype(np.int64)
+    idx_parts, key_parts = [], []
+    for p in range(parts):
+        s = Sampler(k, seed=7, stream_id=2)()
+        s.seek(int(bounds[p]))
+        s.sample_all(kd[bounds[p]:bounds[p + 1]])
+        idx, kk, _, _ = s.export_state(cuda)
+        idx_parts.append(idx)
+        key_parts.append(kk)
+    merged = Sampler(k, seed=7, stream_id=2)()
+    merged.merge_state(torch.stack(idx_parts), torch.stack(key_parts),
+                       torch.zeros((parts, k), dtype=torch.int64, device=cuda), [k] * parts, n)
+    assert merged.count == n
+    assert np.array_equal(merged.result(), want)
+
+
+@pytest.mark.slow
+def test_full_size_split_invariance(cuda):
+    """C2 size (1e9 keys, k = 1024): one pass == 7 ragged batches == 4-way index split."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    n, k = 1_000_000_000, 1024
+    keys = torch.arange(n, dtype=torch.int64, device=cuda)  # key == index: result exposes indices
+    s = Sampler(k, seed=0xC0FFEE, stream_id=0x5A5A)()
+    s.set_stream(torch.cuda.current_stream().cuda_stream)
+    s.sample_all(keys)
+    one = s.result()
+    assert one.size == k and len(set(one.tolist())) == k  # distinct indices
+    assert one.min() >= 0 and one.max() < n
+    cuts = [0, 1, 1023, 1024, 7_777_777, 400_000_000, 999_999_999, n]
+    s2 = Sampler(k, seed=0xC0FFEE, stream_id=0x5A5A)()
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        s2.sample_all(keys[a:b])
+    assert np.array_equal(s2.result(), one)
+    # slot j holds its last writer: every winner index i >= k must draw j
+    from reservoir_amd import batch
+
+    for j in range(0, k, 97):
+        i = int(one[j])
+        if i >= k:
+            assert int(batch.export_draws(0xC0FFEE, 0x5A5A, i, 1)[0]) == j

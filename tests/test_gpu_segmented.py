@@ -1,0 +1,118 @@
+"""Segmented sampling (K2): S independent samplers per launch.  Parity with the oracle on ragged
+inputs, and the reference's 5-sigma fairness/independence tests (SamplerTest.scala:156-240) run
+with 1e6 independent samplers in one launch."""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("k", [1, 5, 64, 100, 1024])
+def test_ragged_parity(cuda, oracle, k):
+    import torch
+
+    from reservoir_amd import batch
+
+    rng = np.random.default_rng(k)
+    lens = rng.integers(0, 5000, size=300)
+    lens[:6] = [0, 1, k - 1 if k > 1 else 0, k, k + 1, 4096]
+    offs = np.r_[0, np.cumsum(lens)].astype(np.int64)
+    keys = oracle.splitmix_keys(k, int(offs[-1]))
+    want, wcnt = oracle.algo_r_segmented(77, 1000, k, keys, offs)
+    out, cnt = batch.sample_segmented(torch.from_numpy(keys).to(cuda), torch.from_numpy(offs).to(cuda), k,
+                                      seed=77, stream_base=1000)
+    assert np.array_equal(cnt.cpu().numpy(), wcnt)
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_int32_keys(cuda, oracle):
+    import torch
+
+    from reservoir_amd import batch
+
+    offs = np.arange(0, 4096 * 50 + 1, 4096, dtype=np.int64)
+    keys = (oracle.splitmix_keys(1, int(offs[-1])) >> 33).astype(np.int32)
+    want, _ = oracle.algo_r_segmented(3, 0, 64, keys.astype(np.int64), offs)
+    out, _ = batch.sample_segmented(torch.from_numpy(keys).to(cuda), torch.from_numpy(offs).to(cuda), 64, seed=3)
+    assert np.array_equal(out.cpu().numpy().astype(np.int64), want)
+
+
+def test_segment_equals_single_sampler(cuda, oracle):
+    """stream s of a segmented launch == a single sampler with stream_id = stream_base + s."""
+    import torch
+
+    from reservoir_amd import Sampler, batch
+
+    offs = np.array([0, 10_000, 10_500, 30_000], dtype=np.int64)
+    keys = oracle.splitmix_keys(2, 30_000)
+    kd = torch.from_numpy(keys).to(cuda)
+    out, _ = batch.sample_segmented(kd, torch.from_numpy(offs).to(cuda), 128, seed=11, stream_base=40)
+    for s in range(3):
+        sm = Sampler(128, seed=11, stream_id=40 + s)()
+        sm.sample_all(kd[offs[s]:offs[s + 1]])
+        r = sm.result()
+        assert np.array_equal(out[s, : r.size].cpu().numpy(), r)
+
+
+def _million_trials(cuda, torch, batch, seed):
+    trials, c = 1_000_000, 10
+    elements = torch.arange(1, c + 1, dtype=torch.int64, device=cuda).repeat(trials)
+    offs = torch.arange(0, trials * c + 1, c, dtype=torch.int64, device=cuda)
+    out, cnt = batch.sample_segmented(elements, offs, c // 2, seed=seed)
+    assert int(cnt.min()) == c // 2
+    return out  # [trials, 5] sampled elements
+
+
+def test_fairness_five_sigma_1e6(cuda):
+    """SamplerTest.scala:156-176 with the reference's n = 1e6."""
+    import torch
+
+    from reservoir_amd import batch
+
+    out = _million_trials(cuda, torch, batch, seed=2024)
+    counts = torch.bincount(out.flatten(), minlength=11)[1:].cpu().numpy()
+    sd = math.sqrt(1_000_000 / 4.0)
+    assert np.all(np.abs(counts - 500_000) < math.ceil(5 * sd)), counts
+    # no element twice in one sample (sampling without replacement)
+    srt = torch.sort(out, dim=1).values
+    assert bool((srt[:, 1:] != srt[:, :-1]).all())
+
+
+def test_pairwise_independence_five_sigma_1e6(cuda):
+    """SamplerTest.scala:198-232: pairs with the same inclusion status, within 5 sigma."""
+    import torch
+
+    from reservoir_amd import batch
+
+    n, c = 1_000_000, 10
+    out = _million_trials(cuda, torch, batch, seed=77)
+    member = torch.zeros((n, c + 1), dtype=torch.bool, device=cuda)
+    member.scatter_(1, out, True)
+    member = member[:, 1:].to(torch.float32)
+    same = member.T @ member + (1 - member).T @ (1 - member)  # [c, c] counts of equal status
+    p = ((c / 2.0) - 1) / (c - 1)
+    mean = round(n * p)
+    sd = math.sqrt(n * p * (1 - p))
+    s = same.cpu().numpy()
+    off = s[~np.eye(c, dtype=bool)]
+    assert np.all(np.abs(off - mean) < math.ceil(5 * sd)), off
+
+
+def test_slot_chi_square(cuda):
+    """Chi-square slot-inclusion uniformity (north star) at k = 64 over 4096-element streams."""
+    import torch
+
+    from reservoir_amd import batch
+
+    S, L, k = 20_000, 4096, 64
+    keys = torch.arange(L, dtype=torch.int64, device=cuda).repeat(S)  # key = index in stream
+    offs = torch.arange(0, S * L + 1, L, dtype=torch.int64, device=cuda)
+    out, _ = batch.sample_segmented(keys, offs, k, seed=99)
+    # inclusion count of each index in 64 bins of 64 consecutive indices: uniform k/L each
+    bins = torch.bincount(out.flatten() // 64, minlength=64).to(torch.float64).cpu().numpy()
+    exp = S * k / 64
+    chi2 = ((bins - exp) ** 2 / exp).sum()
+    # sampling without replacement lowers the variance; dof 63: p(chi2 > 120) < 1e-5
+    assert chi2 < 120, chi2
