@@ -27,20 +27,23 @@ constexpr uint32_t kPhiloxW0 = 0x9E3779B9u;
 constexpr uint32_t kPhiloxW1 = 0xBB67AE85u;
 constexpr uint32_t kDomainLevel1 = 0x80000000u;
 
+// three-input xor in one VALU op (gfx950 has no v_xor3_b32; v_bitop3_b32 with truth table 0x96)
+__device__ __forceinline__ uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t key) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(key));
+    return r;
+}
+
 // Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11).  k0/k1 are wave-uniform (kernel args), so
-// the key schedule stays in SGPRs; each round is two 32x32->64 multiplies and two xor3.
+// the key schedule stays in SGPRs; each round is two v_mad_u64_u32 and two v_bitop3 (xor3).
 __device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        if (r) {
-            k0 += kPhiloxW0;
-            k1 += kPhiloxW1;
-        }
         const uint64_t p0 = (uint64_t)kPhiloxM0 * c0;
         const uint64_t p1 = (uint64_t)kPhiloxM1 * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        const uint32_t n0 = xor3_key((uint32_t)(p1 >> 32), c1, k0 + (uint32_t)r * kPhiloxW0);
+        const uint32_t n2 = xor3_key((uint32_t)(p0 >> 32), c3, k1 + (uint32_t)r * kPhiloxW1);
         c0 = n0;
         c1 = (uint32_t)p1;
         c2 = n2;

@@ -11,6 +11,7 @@
 // only the k winning keys are ever read (DESIGN.md "Roofline").
 #include "rsv_device.h"
 #include "rsv_internal.h"
+#include "rsv_scan.h"
 
 namespace rsv {
 
@@ -18,50 +19,34 @@ namespace {
 
 constexpr int kBlock = 256;
 
-__device__ __forceinline__ uint32_t clip_mask16(uint64_t i0, uint64_t lo, uint64_t hi) {
-    uint32_t m = 0xFFFFu;
-    if (i0 < lo) m = (lo - i0 >= 16) ? 0u : ((0xFFFFu << (uint32_t)(lo - i0)) & 0xFFFFu);
-    if (i0 + 16 > hi) m &= (hi <= i0) ? 0u : (0xFFFFu >> (uint32_t)(16 - (hi - i0)));
-    return m;
-}
-
-// Candidate mask of one level-0 block: bit e set iff b_{i0+e} * (i0+e+1) < 256k (necessary
-// condition for j < k).  Beyond index 256k-1 this is simply "byte == 0" (1 in 256).
-__device__ __forceinline__ uint32_t candidate_mask16(const u32x4& w, uint64_t i0, uint64_t dense_lim) {
-    if (i0 + 1 >= dense_lim) {
-        if (!any_zero_byte(w)) return 0u;
-        return zero_byte_mask16(w);
-    }
-    uint32_t m = 0;
-#pragma unroll
-    for (uint32_t e = 0; e < 16; ++e) {
-        const uint64_t b = level0_byte(w, e);
-        if (b * (i0 + e + 1) < dense_lim) m |= 1u << e;
-    }
-    return m;
-}
-
+// K1: grid-stride over level-0 blocks (16 indices each); wave-uniform loop so the candidate
+// queue can run full-wave level-1 evaluations.  Hits (k ln(n/k) of them) go straight to global
+// atomicMax on the k-slot winner table: 14k atomics per 1e9 indices at k = 1024.
 __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k, uint64_t lo,
                                                          uint64_t hi, uint64_t g_begin,
                                                          uint64_t n_groups,
                                                          unsigned long long* __restrict__ win) {
+    __shared__ uint64_t qs[kBlock / 64][kQueue];
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t* q = qs[threadIdx.x >> 6];
+    uint32_t qn = 0;
+    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
     const uint64_t dense_lim = 256ull * k;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; gi < n_groups; gi += stride) {
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n_groups;
+         base += stride) {
+        const uint64_t gi = base + lane;
         const uint64_t g = g_begin + gi;
         const uint64_t i0 = g << 4;
         const u32x4 w = level0(dk, g);
-        uint32_t mask = candidate_mask16(w, i0, dense_lim);
-        if (!mask) continue;
-        mask &= clip_mask16(i0, lo, hi);
-        while (mask) {
-            const uint32_t e = __builtin_ctz(mask);
-            mask &= mask - 1;
-            const uint64_t i = i0 + e;
-            const uint64_t j = exact_j(dk, i, level0_byte(w, e));
-            if (j < k) atomicMax(&win[j], (unsigned long long)i);
+        uint32_t mask = 0;
+        if (gi < n_groups) {
+            mask = candidate_mask16(w, i0, dense_lim);
+            if (mask) mask &= clip_mask16(i0, lo, hi);
         }
+        enqueue_block(dk, w, i0, mask, q, qn, lane, k, hit);
     }
+    drain_queue(dk, q, qn, lane, k, hit);
 }
 
 template <typename KeyT>
@@ -114,7 +99,9 @@ __global__ __launch_bounds__(kBlock) void k2_segmented(const KeyT* __restrict__ 
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_tab[];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t wpb = blockDim.x >> 6;
-    unsigned long long* tab = lds_tab + (size_t)wave * k;
+    // per wave: k-entry last-writer table, then the candidate queue
+    unsigned long long* tab = lds_tab + (size_t)wave * (k + kQueue);
+    uint64_t* q = (uint64_t*)(tab + k);
     const uint64_t dense_lim = 256ull * k;
     for (int64_t sb = (int64_t)blockIdx.x * wpb; sb < S; sb += (int64_t)gridDim.x * wpb) {
         const int64_t s = sb + wave;
@@ -126,22 +113,23 @@ __global__ __launch_bounds__(kBlock) void k2_segmented(const KeyT* __restrict__ 
             off = offsets[s];
             len = offsets[s + 1] - off;
             const uint64_t stream = stream_base + (uint64_t)s;
-            const DrawKey dk{k0, k1, (uint32_t)stream, (uint32_t)(stream >> 32)};
+            const DrawKey dk{k0, k1, (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)stream),
+                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(stream >> 32))};
             const uint64_t n_groups = ((uint64_t)len + 15) >> 4;
-            for (uint64_t g = (k >> 4) + lane; g < n_groups; g += 64) {
+            auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&tab[j], (unsigned long long)i); };
+            uint32_t qn = 0;
+            for (uint64_t gb = k >> 4; gb < n_groups; gb += 64) {
+                const uint64_t g = gb + lane;
                 const uint64_t i0 = g << 4;
                 const u32x4 w = level0(dk, g);
-                uint32_t mask = candidate_mask16(w, i0, dense_lim);
-                if (!mask) continue;
-                mask &= clip_mask16(i0, k, (uint64_t)len);
-                while (mask) {
-                    const uint32_t e = __builtin_ctz(mask);
-                    mask &= mask - 1;
-                    const uint64_t i = i0 + e;
-                    const uint64_t j = exact_j(dk, i, level0_byte(w, e));
-                    if (j < k) atomicMax(&tab[j], (unsigned long long)i);
+                uint32_t mask = 0;
+                if (g < n_groups) {
+                    mask = candidate_mask16(w, i0, dense_lim);
+                    if (mask) mask &= clip_mask16(i0, k, (uint64_t)len);
                 }
+                enqueue_block(dk, w, i0, mask, q, qn, lane, k, hit);
             }
+            drain_queue(dk, q, qn, lane, k, hit);
         }
         __syncthreads();
         if (active) {
@@ -241,7 +229,7 @@ hipError_t launch_segmented(const void* keys, int key_width, const int64_t* offs
                             hipStream_t st) {
     if (S <= 0) return hipSuccess;
     const int wpb = segmented_waves_per_block(k);
-    const size_t lds = (size_t)wpb * k * sizeof(unsigned long long);
+    const size_t lds = (size_t)wpb * (k + kQueue) * sizeof(unsigned long long);
     uint64_t blocks = ((uint64_t)S + wpb - 1) / wpb;
     const uint64_t cap = 256ull * 16;
     const unsigned grid = (unsigned)(blocks < cap ? blocks : cap);

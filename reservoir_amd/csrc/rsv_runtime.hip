@@ -550,9 +550,9 @@ rsv_status rsv_sample_segmented(const void* keys_dev, const int64_t* offsets_dev
     if (num_streams < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative stream count");
     if (num_streams == 0) return RSV_OK;
     if (!offsets_dev || !out_dev || !counts_dev) return fail(RSV_E_NULL_POINTER, "NULL buffer");
-    const size_t lds = (size_t)segmented_waves_per_block((uint32_t)k) * (size_t)k * 8;
+    const size_t lds = (size_t)segmented_waves_per_block((uint32_t)k) * ((size_t)k + 128) * 8;
     if (lds > 160 * 1024)
-        return fail(RSV_E_UNSUPPORTED, "segmented sampling keeps each stream's k slots in LDS: k <= 20480");
+        return fail(RSV_E_UNSUPPORTED, "segmented sampling keeps each stream's k slots in LDS: k <= 20352");
     const DrawParams dp{seed, stream_base};
     RSV_HIP_TRY(launch_segmented(keys_dev, key_width, offsets_dev, num_streams, (uint32_t)k, dp, out_dev, counts_dev,
                                  (hipStream_t)hip_stream));

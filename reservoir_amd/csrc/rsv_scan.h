@@ -1,0 +1,85 @@
+// rsv_scan.h -- the level-0 scan shared by K1 (one stream) and K2 (segmented): evaluate the 16-
+// index level-0 Philox blocks, and push the ~1/256 candidate indices through a per-wave LDS queue
+// so the level-1 Philox (exact j) always runs with all 64 lanes busy.
+//
+// Without the queue the candidates are evaluated where they are found: almost every wave
+// iteration holds one (64 lanes x 16 indices / 256), so the whole wave pays a second Philox for a
+// single active lane -- measured 383 us vs ~120 us for the level-0 work alone at 1e9 indices.
+#pragma once
+#include "rsv_device.h"
+
+namespace rsv {
+
+constexpr uint32_t kQueue = 128;  // per-wave LDS entries: < 64 waiting + one round of <= 64 pushes
+constexpr uint64_t kIndexMask = (1ull << 56) - 1;  // queue entry = (b_i << 56) | i
+
+__device__ __forceinline__ unsigned long long lanemask_lt64() {
+    const uint32_t lane = threadIdx.x & 63;
+    return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+__device__ __forceinline__ uint32_t clip_mask16(uint64_t i0, uint64_t lo, uint64_t hi) {
+    uint32_t m = 0xFFFFu;
+    if (i0 < lo) m = (lo - i0 >= 16) ? 0u : ((0xFFFFu << (uint32_t)(lo - i0)) & 0xFFFFu);
+    if (i0 + 16 > hi) m &= (hi <= i0) ? 0u : (0xFFFFu >> (uint32_t)(16 - (hi - i0)));
+    return m;
+}
+
+// Candidate mask of one level-0 block: bit e set iff b_{i0+e} * (i0+e+1) < 256k (a necessary
+// condition for j < k).  Beyond index 256k-1 this is simply "byte == 0" (1 in 256).
+__device__ __forceinline__ uint32_t candidate_mask16(const u32x4& w, uint64_t i0, uint64_t dense_lim) {
+    if (i0 + 1 >= dense_lim) {
+        if (!any_zero_byte(w)) return 0u;
+        return zero_byte_mask16(w);
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < 16; ++e) {
+        const uint64_t b = level0_byte(w, e);
+        if (b * (i0 + e + 1) < dense_lim) m |= 1u << e;
+    }
+    return m;
+}
+
+// Evaluate queue entry q[pos] (level 1) and report a hit (j < k) to `hit(j, i)`.
+template <class Hit>
+__device__ __forceinline__ void resolve_entry(const DrawKey& dk, uint64_t e, uint32_t k, Hit& hit) {
+    const uint64_t i = e & kIndexMask;
+    const uint64_t j = exact_j(dk, i, (uint32_t)(e >> 56));
+    if (j < k) hit((uint32_t)j, i);
+}
+
+// Push this lane's candidates (mask over the block starting at i0) into the wave queue; whenever
+// 64 entries wait, all lanes resolve one each.  Must be called by the whole wave (uniform flow).
+template <class Hit>
+__device__ __forceinline__ void enqueue_block(const DrawKey& dk, const u32x4& w, uint64_t i0,
+                                              uint32_t mask, uint64_t* q, uint32_t& qn,
+                                              uint32_t lane, uint32_t k, Hit& hit) {
+    while (__any(mask != 0)) {
+        const bool has = mask != 0;
+        const unsigned long long bal = __ballot(has);
+        if (has) {
+            const uint32_t e = __builtin_ctz(mask);
+            mask &= mask - 1;
+            q[qn + __popcll(bal & lanemask_lt64())] = ((uint64_t)level0_byte(w, e) << 56) | (i0 + e);
+        }
+        qn += (uint32_t)__popcll(bal);
+        if (qn >= 64) {
+            qn -= 64;
+            __builtin_amdgcn_wave_barrier();
+            resolve_entry(dk, q[qn + lane], k, hit);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+template <class Hit>
+__device__ __forceinline__ void drain_queue(const DrawKey& dk, const uint64_t* q, uint32_t& qn,
+                                            uint32_t lane, uint32_t k, Hit& hit) {
+    __builtin_amdgcn_wave_barrier();
+    if (lane < qn) resolve_entry(dk, q[lane], k, hit);
+    qn = 0;
+    __builtin_amdgcn_wave_barrier();
+}
+
+}  // namespace rsv

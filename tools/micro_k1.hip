@@ -1,0 +1,121 @@
+// micro_k1.hip -- instruction-rate and K1-variant microbenchmarks (development tool, not product).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../include tools/micro_k1.hip -o tools/micro_k1
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../reservoir_amd/csrc/rsv_device.h"
+
+using namespace rsv;
+
+#define CK(x)                                                                          \
+    do {                                                                               \
+        hipError_t e = (x);                                                            \
+        if (e != hipSuccess) {                                                         \
+            printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+            return 1;                                                                  \
+        }                                                                              \
+    } while (0)
+
+// ---- op-rate kernels: 8 independent chains, ITER iterations ---------------------------------
+template <int OP>
+__global__ __launch_bounds__(256) void op_rate(uint32_t* out, uint32_t seed, int iters) {
+    uint32_t a[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) a[c] = threadIdx.x * 7 + c + seed;
+    const uint32_t m = 0xD2511F53u ^ seed;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            if constexpr (OP == 0) {  // v_mad_u64_u32 (64-bit product, both halves used)
+                uint64_t p = (uint64_t)a[c] * m;
+                a[c] = (uint32_t)p ^ (uint32_t)(p >> 32);
+            } else if constexpr (OP == 1) {  // v_mul_hi_u32 only
+                a[c] = __umulhi(a[c], m) + c;
+            } else if constexpr (OP == 2) {  // v_mul_lo_u32 only
+                a[c] = a[c] * m + c;
+            } else if constexpr (OP == 3) {  // xor / add (full-rate reference)
+                a[c] = (a[c] ^ m) + c;
+            } else if constexpr (OP == 4) {  // 24-bit mul
+                a[c] = __umul24(a[c], m) + c;
+            }
+        }
+    }
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) r ^= a[c];
+    if (r == 0x12345678u) out[0] = r;
+}
+
+// ---- K1 variants over an index range ---------------------------------------------------------
+// V0: level 0 only (Philox + zero-byte pre-test), count blocks with a candidate
+__global__ __launch_bounds__(256) void k1_level0_only(DrawKey dk, uint64_t n_groups, unsigned long long* cnt) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t c = 0;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_groups; g += stride) {
+        const u32x4 w = level0(dk, g + (1ull << 20));
+        c += any_zero_byte(w);
+    }
+    if (c == 0xFFFFFFFFu) atomicAdd(cnt, c);
+}
+
+// V1: philox only, no test at all
+__global__ __launch_bounds__(256) void philox_only(DrawKey dk, uint64_t n_groups, unsigned long long* cnt) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t c = 0;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_groups; g += stride) {
+        const u32x4 w = level0(dk, g);
+        c ^= w.x ^ w.y ^ w.z ^ w.w;
+    }
+    if (c == 0x12345u) atomicAdd(cnt, c);
+}
+
+int main(int argc, char** argv) {
+    uint32_t* d;
+    CK(hipMalloc(&d, 64));
+    unsigned long long* cnt;
+    CK(hipMalloc(&cnt, 64));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int blocks = 256 * 8, iters = 4096;
+    const double ops = (double)blocks * 256 * iters * 8;
+    auto time_op = [&](auto kern, const char* name) -> int {
+        for (int rep = 0; rep < 3; ++rep) {
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d, 1u, iters);
+        }
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d, 1u, iters);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        // lane-ops per second and per CU per clock at 2.4 GHz
+        printf("%-28s %8.3f ms  %8.2f Tlane-op/s  %6.1f lane-op/clk/CU@2.4GHz\n", name, ms, ops / ms / 1e9,
+               ops / (ms * 1e-3) / 256 / 2.4e9);
+        return 0;
+    };
+    time_op(op_rate<0>, "mad_u64_u32 (+xor)");
+    time_op(op_rate<1>, "mul_hi_u32 (+add)");
+    time_op(op_rate<2>, "mul_lo_u32 (+add)");
+    time_op(op_rate<3>, "xor+add");
+    time_op(op_rate<4>, "mul_u32_u24 (+add)");
+
+    const uint64_t n_groups = 1000000000ull / 16;
+    DrawKey dk{0xC0FFEE, 0, 0x5A5A, 0};
+    auto time_k = [&](auto kern, const char* name, int grid) -> int {
+        for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, dk, n_groups, cnt);
+        CK(hipEventRecord(e0));
+        for (int rep = 0; rep < 5; ++rep) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, dk, n_groups, cnt);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("%-28s grid %6d  %8.1f us per 1e9 indices  (%.1f G philox/s)\n", name, grid, ms / 5 * 1e3,
+               n_groups / (ms / 5 * 1e-3) / 1e9);
+        return 0;
+    };
+    for (int grid : {1024, 2048, 4096, 8192}) time_k(philox_only, "philox_only", grid);
+    for (int grid : {2048, 8192}) time_k(k1_level0_only, "level0+zero-test", grid);
+    return 0;
+}
