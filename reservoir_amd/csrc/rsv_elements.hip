@@ -22,31 +22,37 @@ constexpr int kBlock = 256;
 // K1: grid-stride over level-0 blocks (16 indices each); wave-uniform loop so the candidate
 // queue can run full-wave level-1 evaluations.  Hits (k ln(n/k) of them) go straight to global
 // atomicMax on the k-slot winner table: 14k atomics per 1e9 indices at k = 1024.
+constexpr int kK1Unroll = 2;  // level-0 blocks per lane per iteration (two Philox chains in flight)
+
 __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k, uint64_t lo,
                                                          uint64_t hi, uint64_t g_begin,
                                                          uint64_t n_groups,
                                                          unsigned long long* __restrict__ win) {
-    __shared__ uint64_t qs[kBlock / 64][kQueue];
+    __shared__ uint64_t qs[kBlock / 64][3 * kBlockQueue];
     const uint32_t lane = threadIdx.x & 63;
     uint64_t* q = qs[threadIdx.x >> 6];
     uint32_t qn = 0;
     auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
     const uint64_t dense_lim = 256ull * k;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n_groups;
-         base += stride) {
-        const uint64_t gi = base + lane;
-        const uint64_t g = g_begin + gi;
-        const uint64_t i0 = g << 4;
-        const u32x4 w = level0(dk, g);
-        uint32_t mask = 0;
-        if (gi < n_groups) {
-            mask = candidate_mask16(w, i0, dense_lim);
-            if (mask) mask &= clip_mask16(i0, lo, hi);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * kK1Unroll;
+    for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * kK1Unroll;
+         base < n_groups; base += stride) {
+        u32x4 w[kK1Unroll];
+        uint64_t g[kK1Unroll];
+#pragma unroll
+        for (int u = 0; u < kK1Unroll; ++u) {
+            g[u] = g_begin + base + u * 64 + lane;
+            w[u] = level0(dk, g[u]);
         }
-        enqueue_block(dk, w, i0, mask, q, qn, lane, k, hit);
+#pragma unroll
+        for (int u = 0; u < kK1Unroll; ++u) {
+            // dense region (index < 256k): any block may hold candidates; else only zero bytes
+            const bool has = base + u * 64 + lane < n_groups &&
+                             (((g[u] << 4) + 1 < dense_lim) || any_zero_byte(w[u]));
+            push_block(has, g[u], w[u], q, qn, lane, dk, lo, hi, dense_lim, k, hit);
+        }
     }
-    drain_queue(dk, q, qn, lane, k, hit);
+    drain_blocks(q, qn, lane, dk, lo, hi, dense_lim, k, hit);
 }
 
 template <typename KeyT>
@@ -183,7 +189,7 @@ hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, 
     if (hi <= lo) return hipSuccess;
     const uint64_t g_begin = lo >> 4, g_end = (hi + 15) >> 4;
     const uint64_t n_groups = g_end - g_begin;
-    const unsigned grid = grid_for(n_groups, 256 * 8);
+    const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 16);
     hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
                        g_begin, n_groups, batch_win);
     return hipGetLastError();

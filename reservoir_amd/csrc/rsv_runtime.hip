@@ -126,6 +126,7 @@ struct rsv_sampler {
     void* chunk_d = nullptr;     // device chunk for host batches
     int64_t* chunk_hash_d = nullptr;
     int64_t chunk_cap = 0;
+    void* result_h = nullptr;  // pinned staging for result() (k keys)
     KernelTimer timer;
 };
 
@@ -244,6 +245,7 @@ void free_all(rsv_sampler* s) {
     for (void* p : ds)
         if (p) (void)hipFree(p);
     if (s->stage_h) (void)hipHostFree(s->stage_h);
+    if (s->result_h) (void)hipHostFree(s->result_h);
     if (s->stage_hash_h) (void)hipHostFree(s->stage_hash_h);
     if (s->distinct) distinct_destroy(s->distinct);
     if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
@@ -429,9 +431,13 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
         if (m > cap) return fail(RSV_E_ILLEGAL_ARGUMENT, "result buffer too small");
         if (m && !out) return fail(RSV_E_NULL_POINTER, "out is NULL");
         src = s->slot_key;
-        if (m) {
-            RSV_HIP_TRY(hipMemcpyAsync(out, src, m * s->kw,
-                                       device_out ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s->stream));
+        if (m && device_out) {
+            RSV_HIP_TRY(hipMemcpyAsync(out, src, m * s->kw, hipMemcpyDeviceToDevice, s->stream));
+        } else if (m) {  // through a pinned buffer: a pageable D2H costs a staged copy
+            if (!s->result_h) RSV_HIP_TRY(hipHostMalloc(&s->result_h, (size_t)s->k * s->kw, hipHostMallocDefault));
+            RSV_HIP_TRY(hipMemcpyAsync(s->result_h, src, m * s->kw, hipMemcpyDeviceToHost, s->stream));
+            RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+            memcpy(out, s->result_h, (size_t)m * s->kw);
         }
     }
     RSV_HIP_TRY(hipStreamSynchronize(s->stream));

@@ -82,4 +82,70 @@ __device__ __forceinline__ void drain_queue(const DrawKey& dk, const uint64_t* q
     __builtin_amdgcn_wave_barrier();
 }
 
+// ---- block queue (K1): a wave iteration pushes whole level-0 blocks that hold a candidate ----
+// In K1's sparse region (index >= 256k) a block holds a candidate only if one of its 16 bytes is
+// zero (6% of blocks, but ~98% of wave iterations see at least one).  Decoding the candidate
+// bytes where they are found would cost the whole wave every iteration, so the iteration only
+// tests "any zero byte" and pushes the raw block (g, 4 words = 24 B); decoding and the level-1
+// draws run at drain time, 64 blocks at once.
+constexpr uint32_t kBlockQueue = 128;  // entries of 3 x u64 per wave
+
+template <class Hit>
+__device__ __forceinline__ void resolve_block(const DrawKey& dk, uint64_t g, const u32x4& w,
+                                              uint64_t lo, uint64_t hi, uint64_t dense_lim,
+                                              uint32_t k, Hit& hit) {
+    const uint64_t i0 = g << 4;
+    uint32_t mask = candidate_mask16(w, i0, dense_lim) & clip_mask16(i0, lo, hi);
+    while (mask) {
+        const uint32_t e = __builtin_ctz(mask);
+        mask &= mask - 1;
+        const uint64_t j = exact_j(dk, i0 + e, level0_byte(w, e));
+        if (j < k) hit((uint32_t)j, i0 + e);
+    }
+}
+
+__device__ __forceinline__ void load_block(const uint64_t* q, uint32_t pos, uint64_t& g, u32x4& w) {
+    g = q[3 * pos];
+    const uint64_t a = q[3 * pos + 1], b = q[3 * pos + 2];
+    w = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+}
+
+template <class Hit>
+__device__ __forceinline__ void push_block(bool has, uint64_t g, const u32x4& w, uint64_t* q,
+                                           uint32_t& qn, uint32_t lane, const DrawKey& dk,
+                                           uint64_t lo, uint64_t hi, uint64_t dense_lim, uint32_t k,
+                                           Hit& hit) {
+    const unsigned long long bal = __ballot(has);
+    if (bal == 0) return;
+    if (has) {
+        const uint32_t pos = qn + __popcll(bal & lanemask_lt64());
+        q[3 * pos] = g;
+        q[3 * pos + 1] = ((uint64_t)w.y << 32) | w.x;
+        q[3 * pos + 2] = ((uint64_t)w.w << 32) | w.z;
+    }
+    qn += (uint32_t)__popcll(bal);
+    if (qn >= 64) {
+        qn -= 64;
+        __builtin_amdgcn_wave_barrier();
+        uint64_t gg;
+        u32x4 ww;
+        load_block(q, qn + lane, gg, ww);
+        resolve_block(dk, gg, ww, lo, hi, dense_lim, k, hit);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+template <class Hit>
+__device__ __forceinline__ void drain_blocks(const uint64_t* q, uint32_t qn, uint32_t lane,
+                                             const DrawKey& dk, uint64_t lo, uint64_t hi,
+                                             uint64_t dense_lim, uint32_t k, Hit& hit) {
+    __builtin_amdgcn_wave_barrier();
+    if (lane < qn) {
+        uint64_t gg;
+        u32x4 ww;
+        load_block(q, lane, gg, ww);
+        resolve_block(dk, gg, ww, lo, hi, dense_lim, k, hit);
+    }
+}
+
 }  // namespace rsv

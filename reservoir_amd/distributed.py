@@ -34,25 +34,28 @@ def sample_shard(sampler, keys_local, global_offset: int) -> None:
 
 
 def combine(sampler, group=None, device=None) -> None:
-    """All-gather the partial states of every rank and merge them into ``sampler`` (on all ranks)."""
+    """All-gather the partial states of every rank and merge them into ``sampler`` (on all ranks).
+
+    One collective: each rank packs [idx(k) | keys(k) | hashes(k) | n | count] into one int64
+    row (3k + 2 words, 24.6 KB at k = 1024) so the exchange pays one RCCL latency, not four.
+    """
     world = dist.get_world_size(group)
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
     idx, keys, hashes, n = sampler.export_state(device)
     k = keys.numel()
-    g_idx = torch.empty((world, k), dtype=idx.dtype, device=idx.device)
-    g_keys = torch.empty((world, k), dtype=keys.dtype, device=keys.device)
-    g_hash = torch.empty((world, k), dtype=hashes.dtype, device=hashes.device)
-    meta = torch.tensor([n, sampler.count], dtype=torch.int64, device=idx.device)
-    g_meta = torch.empty((world, 2), dtype=torch.int64, device=idx.device)
-    if sampler.is_distinct:
-        dist.all_gather_into_tensor(g_hash, hashes, group=group)
-    else:
-        dist.all_gather_into_tensor(g_idx, idx, group=group)
-    dist.all_gather_into_tensor(g_keys, keys, group=group)
-    dist.all_gather_into_tensor(g_meta, meta, group=group)
-    m = g_meta.cpu()
-    part_n = m[:, 0].tolist()
+    row = torch.empty(3 * k + 2, dtype=torch.int64, device=idx.device)
+    row[:k] = idx
+    row[k:2 * k] = keys.to(torch.int64)
+    row[2 * k:3 * k] = hashes
+    row[3 * k] = n
+    row[3 * k + 1] = sampler.count
+    flat = torch.empty(world * (3 * k + 2), dtype=torch.int64, device=idx.device)
+    dist.all_gather_into_tensor(flat, row, group=group)  # flat output: gloo and RCCL both accept
+    rows = flat.view(world, 3 * k + 2)
+    meta = rows[:, 3 * k:].cpu()
+    part_n = meta[:, 0].tolist()
     # elements: the stream ends at the largest rank end; distinct: counts add up
-    total = int(m[:, 1].sum()) if sampler.is_distinct else int(m[:, 1].max())
-    sampler.merge_state(g_idx, g_keys, g_hash, part_n, total)
+    total = int(meta[:, 1].sum()) if sampler.is_distinct else int(meta[:, 1].max())
+    g_keys = rows[:, k:2 * k].to(keys.dtype).contiguous()
+    sampler.merge_state(rows[:, :k].contiguous(), g_keys, rows[:, 2 * k:3 * k].contiguous(), part_n, total)

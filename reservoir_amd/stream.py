@@ -58,7 +58,14 @@ class SampleFlow:
                         p.set_exception(ex)
                     raise
                 sampler.sample(elem)  # SampleImpl.scala:27-31
-                yield elem  # push(out, elem)
+                try:
+                    yield elem  # push(out, elem)
+                except GeneratorExit:
+                    raise
+                except BaseException as cause:  # downstream failed: onDownstreamFinish(cause)
+                    if not p.done():
+                        p.set_exception(cause)
+                    raise
         except GeneratorExit:  # downstream cancelled without failure, SampleImpl.scala:48-54
             try_complete()
             raise

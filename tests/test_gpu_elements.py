@@ -219,3 +219,27 @@ def test_full_size_split_invariance(cuda):
         i = int(one[j])
         if i >= k:
             assert int(batch.export_draws(0xC0FFEE, 0x5A5A, i, 1)[0]) == j
+
+
+@pytest.mark.parametrize("i0", [2**32 - 100, 5 * 10**9, 2**40 + 3])
+def test_high_index_offsets(cuda, oracle, i0):
+    """Ranks beyond the first 2^32 indices (8-GPU C2 reaches 8e9): 64-bit draw arithmetic."""
+    import ctypes as C
+
+    import torch
+
+    from reservoir_amd import Sampler
+
+    n, k = 1_000_000, 1024
+    keys = oracle.splitmix_keys(i0 & 0xFFFF, n)
+    res = np.zeros(k, dtype=np.int64)
+    idx = np.full(k, -1, dtype=np.int64)
+    oracle.lib().or_algo_r(3, 4, k, i0, keys, n, res, idx.ctypes.data_as(C.c_void_p))
+    s = Sampler(k, seed=3, stream_id=4)()
+    s.seek(i0)
+    s.sample_all(torch.from_numpy(keys).to(cuda))
+    gidx, gkeys, _, _ = s.export_state(cuda)
+    assert np.array_equal(gidx.cpu().numpy(), idx)
+    hit = idx >= 0
+    assert hit.sum() > 0
+    assert np.array_equal(gkeys.cpu().numpy()[hit], res[hit])

@@ -5,6 +5,7 @@
 #include <stdio.h>
 
 #include "../reservoir_amd/csrc/rsv_device.h"
+#include "../reservoir_amd/csrc/rsv_scan.h"
 
 using namespace rsv;
 
@@ -70,6 +71,36 @@ __global__ __launch_bounds__(256) void philox_only(DrawKey dk, uint64_t n_groups
     if (c == 0x12345u) atomicAdd(cnt, c);
 }
 
+// V2: full K1 (block queue), UNROLL level-0 blocks per lane per iteration
+template <int UNROLL>
+__global__ __launch_bounds__(256) void k1_var(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                              uint64_t n_groups, unsigned long long* win) {
+    __shared__ uint64_t qs[4][3 * kBlockQueue];
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t* q = qs[threadIdx.x >> 6];
+    uint32_t qn = 0;
+    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
+    const uint64_t dense_lim = 256ull * k;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * UNROLL;
+    for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * UNROLL; base < n_groups;
+         base += stride) {
+        u32x4 w[UNROLL];
+        uint64_t g[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            g[u] = g_begin + base + u * 64 + lane;
+            w[u] = level0(dk, g[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t gi = base + u * 64 + lane;
+            const bool has = gi < n_groups && (((g[u] << 4) + 1 < dense_lim) || any_zero_byte(w[u]));
+            push_block(has, g[u], w[u], q, qn, lane, dk, lo, hi, dense_lim, k, hit);
+        }
+    }
+    drain_blocks(q, qn, lane, dk, lo, hi, dense_lim, k, hit);
+}
+
 int main(int argc, char** argv) {
     uint32_t* d;
     CK(hipMalloc(&d, 64));
@@ -117,5 +148,27 @@ int main(int argc, char** argv) {
     };
     for (int grid : {1024, 2048, 4096, 8192}) time_k(philox_only, "philox_only", grid);
     for (int grid : {2048, 8192}) time_k(k1_level0_only, "level0+zero-test", grid);
+    unsigned long long* win;
+    CK(hipMalloc(&win, 1024 * 8));
+    CK(hipMemset(win, 0, 1024 * 8));
+    auto time_v = [&](auto kern, const char* name, int grid, int unroll) -> int {
+        const uint64_t lo = 1024, hi = 1000000000ull;
+        for (int rep = 0; rep < 2; ++rep)
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, dk, 1024u, lo, hi, 0ull, n_groups, win);
+        CK(hipEventRecord(e0));
+        for (int rep = 0; rep < 5; ++rep)
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, dk, 1024u, lo, hi, 0ull, n_groups, win);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("%-28s grid %6d unroll %d  %8.1f us per 1e9 indices\n", name, grid, unroll, ms / 5 * 1e3);
+        return 0;
+    };
+    for (int grid : {1024, 2048, 4096}) {
+        time_v(k1_var<1>, "k1 block-queue", grid, 1);
+        time_v(k1_var<2>, "k1 block-queue", grid, 2);
+        time_v(k1_var<4>, "k1 block-queue", grid, 4);
+    }
     return 0;
 }
