@@ -79,7 +79,33 @@ struct Vec<int32_t> {
     __device__ static int32_t get(const T& v, int e) { return v[e]; }
 };
 
-// K3 filter: streaming pass, 2 x 16-B loads in flight per lane per iteration.
+// K3 filter: streaming pass.  The main loop covers whole grid tiles with unguarded loads (U x 16 B
+// per lane issued back to back, so each wave keeps U loads in flight); per-element work is the
+// scrambled hash and one compare, and the rare candidates take one wave-uniform slow path.
+template <typename KeyT, int HASH, int U>
+__device__ __forceinline__ void k3_tile(const typename Vec<KeyT>::T* x, int64_t v0, int64_t T,
+                                        const KeyT* keys, const int64_t* hashes, int64_t r0, int64_t r1,
+                                        int64_t tinc, int64_t* cand_h, KeyT* cand_k,
+                                        unsigned long long* counter, int64_t cap) {
+    using V = Vec<KeyT>;
+    int64_t h[U][V::N];
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int e = 0; e < V::N; ++e) {
+            h[u][e] = elem_hash<KeyT, HASH>(keys, hashes, (v0 + u * T) * V::N + e, V::get(x[u], e), r0, r1);
+            any |= h[u][e] <= tinc;
+        }
+    if (__any(any)) {  // ~1e-4 of the waves at the steady-state threshold
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int e = 0; e < V::N; ++e)
+                append_if<KeyT>(h[u][e] <= tinc, h[u][e], V::get(x[u], e), cand_h, cand_k, counter, cap);
+    }
+}
+
 template <typename KeyT, int HASH>
 __global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ keys,
                                                     const int64_t* __restrict__ hashes, int64_t n,
@@ -89,32 +115,31 @@ __global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ key
                                                     unsigned long long* __restrict__ counter,
                                                     int64_t cap) {
     using V = Vec<KeyT>;
-    constexpr int U = 2;
+    constexpr int U = 4;
     const int64_t T = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t n_vec = n / V::N;
     const typename V::T* kv = reinterpret_cast<const typename V::T*>(keys);
-    for (int64_t v0 = tid; v0 - tid < n_vec; v0 += T * U) {  // uniform trip count per wave
+    const int64_t full = n_vec / (T * U);  // whole tiles: every lane has U vectors
+    for (int64_t it = 0; it < full; ++it) {
+        const int64_t v0 = it * T * U + tid;
         typename V::T x[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t v = v0 + u * T;
-            if (v < n_vec) x[u] = __builtin_nontemporal_load(kv + v);
-        }
+        for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(kv + v0 + u * T);
+        k3_tile<KeyT, HASH, U>(x, v0, T, keys, hashes, r0, r1, tinc, cand_h, cand_k, counter, cap);
+    }
+    // remaining vectors, one per lane per step, then the n % V::N tail elements
+    for (int64_t v = full * T * U + tid; v - tid < n_vec; v += T) {
+        const bool ok = v < n_vec;
+        typename V::T x[1];
+        x[0] = ok ? kv[v] : typename V::T{};
+        int64_t h[V::N];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t v = v0 + u * T;
-            const bool ok = v < n_vec;
-#pragma unroll
-            for (int e = 0; e < V::N; ++e) {
-                const KeyT key = ok ? V::get(x[u], e) : (KeyT)0;
-                const int64_t idx = v * V::N + e;
-                const int64_t h = ok ? elem_hash<KeyT, HASH>(keys, hashes, idx, key, r0, r1) : 0;
-                append_if<KeyT>(ok && h <= tinc, h, key, cand_h, cand_k, counter, cap);
-            }
+        for (int e = 0; e < V::N; ++e) {
+            h[e] = ok ? elem_hash<KeyT, HASH>(keys, hashes, v * V::N + e, V::get(x[0], e), r0, r1) : 0;
+            append_if<KeyT>(ok && h[e] <= tinc, h[e], V::get(x[0], e), cand_h, cand_k, counter, cap);
         }
     }
-    // tail (n % V::N elements)
     for (int64_t idx = n_vec * V::N + tid; idx - tid < n; idx += T) {
         const bool ok = idx < n;
         const KeyT key = ok ? keys[idx] : (KeyT)0;
@@ -270,7 +295,7 @@ int64_t distinct_size(const DistinctState* d) { return d->m; }
 template <typename KeyT>
 static hipError_t launch_filter(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
                                 int64_t tinc, hipStream_t st) {
-    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 8 + 1), 1), 256 * 8);
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 16 + 1), 1), 256 * 8);
     KeyT* ck = (KeyT*)d->cand_k;
     switch (d->hash_kind) {
     case kHashJavaLong:

@@ -221,8 +221,9 @@ def test_full_size_split_invariance(cuda):
             assert int(batch.export_draws(0xC0FFEE, 0x5A5A, i, 1)[0]) == j
 
 
-@pytest.mark.parametrize("i0", [2**32 - 100, 5 * 10**9, 2**40 + 3])
-def test_high_index_offsets(cuda, oracle, i0):
+@pytest.mark.parametrize("i0,k,n", [(2**32 - 100, 1024, 1_000_000), (5 * 10**9, 65_536, 2_000_000),
+                                    (2**40 + 3, 1 << 20, 8_000_000)])
+def test_high_index_offsets(cuda, oracle, i0, k, n):
     """Ranks beyond the first 2^32 indices (8-GPU C2 reaches 8e9): 64-bit draw arithmetic."""
     import ctypes as C
 
@@ -230,7 +231,6 @@ def test_high_index_offsets(cuda, oracle, i0):
 
     from reservoir_amd import Sampler
 
-    n, k = 1_000_000, 1024
     keys = oracle.splitmix_keys(i0 & 0xFFFF, n)
     res = np.zeros(k, dtype=np.int64)
     idx = np.full(k, -1, dtype=np.int64)
