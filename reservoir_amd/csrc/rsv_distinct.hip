@@ -36,24 +36,54 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
     return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
+// Candidate output: staged per wave in LDS and written 64 at a time, so the global reservation
+// counter sees one atomic per 64 candidates (a single contended word sustains ~88 atomics/us:
+// one atomic per candidate cost 1.5 ms at 132k candidates).
 template <typename KeyT>
-__device__ __forceinline__ void append_if(bool c, int64_t h, KeyT key, int64_t* __restrict__ cand_h,
-                                          KeyT* __restrict__ cand_k,
-                                          unsigned long long* __restrict__ counter, int64_t cap) {
-    const unsigned long long b = __ballot(c);
-    if (b == 0) return;
-    const int leader = __ffsll((long long)b) - 1;
-    unsigned long long base = 0;
-    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(counter, (unsigned long long)__popcll(b));
-    base = __shfl(base, leader);
-    if (c) {
-        const unsigned long long pos = base + __popcll(b & lanemask_lt());
-        if ((int64_t)pos < cap) {
-            cand_h[pos] = h;
-            cand_k[pos] = key;
+struct CandOut {
+    int64_t* qh;  // LDS: 128 hashes of this wave
+    KeyT* qk;     // LDS: 128 keys
+    uint32_t qn;  // wave-uniform fill
+    int64_t* cand_h;
+    KeyT* cand_k;
+    unsigned long long* counter;
+    int64_t cap;
+
+    __device__ __forceinline__ void write64(uint32_t from, uint32_t cnt) {
+        const uint32_t lane = threadIdx.x & 63;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(counter, (unsigned long long)cnt);
+        base = __shfl(base, 0);
+        if (lane < cnt) {
+            const unsigned long long pos = base + lane;
+            if ((int64_t)pos < cap) {
+                cand_h[pos] = qh[from + lane];
+                cand_k[pos] = qk[from + lane];
+            }
         }
     }
-}
+    __device__ __forceinline__ void push(bool c, int64_t h, KeyT key) {
+        const unsigned long long bal = __ballot(c);
+        if (bal == 0) return;
+        if (c) {
+            const uint32_t pos = qn + __popcll(bal & lanemask_lt());
+            qh[pos] = h;
+            qk[pos] = key;
+        }
+        qn += (uint32_t)__popcll(bal);
+        if (qn >= 64) {
+            qn -= 64;
+            __builtin_amdgcn_wave_barrier();
+            write64(qn, 64);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __device__ __forceinline__ void flush() {
+        __builtin_amdgcn_wave_barrier();
+        if (qn) write64(0, qn);
+        qn = 0;
+    }
+};
 
 template <typename KeyT, int HASH>
 __device__ __forceinline__ int64_t elem_hash(const KeyT* keys, const int64_t* hashes, int64_t idx,
@@ -85,8 +115,7 @@ struct Vec<int32_t> {
 template <typename KeyT, int HASH, int U>
 __device__ __forceinline__ void k3_tile(const typename Vec<KeyT>::T* x, int64_t v0, int64_t T,
                                         const KeyT* keys, const int64_t* hashes, int64_t r0, int64_t r1,
-                                        int64_t tinc, int64_t* cand_h, KeyT* cand_k,
-                                        unsigned long long* counter, int64_t cap) {
+                                        int64_t tinc, CandOut<KeyT>& out) {
     using V = Vec<KeyT>;
     int64_t h[U][V::N];
     bool any = false;
@@ -102,7 +131,7 @@ __device__ __forceinline__ void k3_tile(const typename Vec<KeyT>::T* x, int64_t 
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int e = 0; e < V::N; ++e)
-                append_if<KeyT>(h[u][e] <= tinc, h[u][e], V::get(x[u], e), cand_h, cand_k, counter, cap);
+                out.push(h[u][e] <= tinc, h[u][e], V::get(x[u], e));
     }
 }
 
@@ -116,6 +145,9 @@ __global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ key
                                                     int64_t cap) {
     using V = Vec<KeyT>;
     constexpr int U = 4;
+    __shared__ int64_t sh_h[kBlock / 64][128];
+    __shared__ KeyT sh_k[kBlock / 64][128];
+    CandOut<KeyT> out{sh_h[threadIdx.x >> 6], sh_k[threadIdx.x >> 6], 0u, cand_h, cand_k, counter, cap};
     const int64_t T = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t n_vec = n / V::N;
@@ -126,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ key
         typename V::T x[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(kv + v0 + u * T);
-        k3_tile<KeyT, HASH, U>(x, v0, T, keys, hashes, r0, r1, tinc, cand_h, cand_k, counter, cap);
+        k3_tile<KeyT, HASH, U>(x, v0, T, keys, hashes, r0, r1, tinc, out);
     }
     // remaining vectors, one per lane per step, then the n % V::N tail elements
     for (int64_t v = full * T * U + tid; v - tid < n_vec; v += T) {
@@ -137,15 +169,16 @@ __global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ key
 #pragma unroll
         for (int e = 0; e < V::N; ++e) {
             h[e] = ok ? elem_hash<KeyT, HASH>(keys, hashes, v * V::N + e, V::get(x[0], e), r0, r1) : 0;
-            append_if<KeyT>(ok && h[e] <= tinc, h[e], V::get(x[0], e), cand_h, cand_k, counter, cap);
+            out.push(ok && h[e] <= tinc, h[e], V::get(x[0], e));
         }
     }
     for (int64_t idx = n_vec * V::N + tid; idx - tid < n; idx += T) {
         const bool ok = idx < n;
         const KeyT key = ok ? keys[idx] : (KeyT)0;
         const int64_t h = ok ? elem_hash<KeyT, HASH>(keys, hashes, idx, key, r0, r1) : 0;
-        append_if<KeyT>(ok && h <= tinc, h, key, cand_h, cand_k, counter, cap);
+        out.push(ok && h <= tinc, h, key);
     }
+    out.flush();
 }
 
 template <typename KeyT, int HASH>
