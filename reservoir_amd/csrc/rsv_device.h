@@ -94,13 +94,14 @@ __device__ __forceinline__ uint32_t zero_byte_mask16(const u32x4& w) {
     return m;
 }
 
-// true iff some byte of the block is zero (cheap sparse-region pre-test)
+// true iff some byte of the block is zero (sparse-region pre-test).  haszero(x) =
+// (x - 0x01010101) & ~x & 0x80808080 is non-zero exactly when x has a zero byte (its false
+// positives only occur above a true zero byte); hipcc folds the and-not-and into one v_bitop3.
+__device__ __forceinline__ uint32_t haszero_bits(uint32_t x) {
+    return (x - 0x01010101u) & ~x & 0x80808080u;
+}
 __device__ __forceinline__ bool any_zero_byte(const u32x4& w) {
-    const uint32_t y0 = ((w.x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w.x;
-    const uint32_t y1 = ((w.y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w.y;
-    const uint32_t y2 = ((w.z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w.z;
-    const uint32_t y3 = ((w.w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w.w;
-    return ((y0 & y1 & y2 & y3) | 0x7F7F7F7Fu) != 0xFFFFFFFFu;
+    return (haszero_bits(w.x) | haszero_bits(w.y) | haszero_bits(w.z) | haszero_bits(w.w)) != 0u;
 }
 
 // ---------------------------------------------------------------------------------------------

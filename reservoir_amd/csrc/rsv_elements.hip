@@ -44,13 +44,11 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
             g[u] = g_begin + base + u * 64 + lane;
             w[u] = level0(dk, g[u]);
         }
+        bool has[kK1Unroll];
 #pragma unroll
-        for (int u = 0; u < kK1Unroll; ++u) {
-            // dense region (index < 256k): any block may hold candidates; else only zero bytes
-            const bool has = base + u * 64 + lane < n_groups &&
-                             (((g[u] << 4) + 1 < dense_lim) || any_zero_byte(w[u]));
-            push_block(has, g[u], w[u], q, qn, lane, dk, lo, hi, dense_lim, k, hit);
-        }
+        for (int u = 0; u < kK1Unroll; ++u)  // dense region (index < 256k): any block may hit
+            has[u] = base + u * 64 + lane < n_groups && (((g[u] << 4) + 1 < dense_lim) || any_zero_byte(w[u]));
+        push_blocks<kK1Unroll>(has, g, w, q, qn, lane, dk, lo, hi, dense_lim, k, hit);
     }
     drain_blocks(q, qn, lane, dk, lo, hi, dense_lim, k, hit);
 }

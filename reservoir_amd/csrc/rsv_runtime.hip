@@ -436,11 +436,10 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
         } else if (m) {  // through a pinned buffer: a pageable D2H costs a staged copy
             if (!s->result_h) RSV_HIP_TRY(hipHostMalloc(&s->result_h, (size_t)s->k * s->kw, hipHostMallocDefault));
             RSV_HIP_TRY(hipMemcpyAsync(s->result_h, src, m * s->kw, hipMemcpyDeviceToHost, s->stream));
-            RSV_HIP_TRY(hipStreamSynchronize(s->stream));
-            memcpy(out, s->result_h, (size_t)m * s->kw);
         }
     }
     RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    if (m && !device_out && s->cfg.kind != RSV_KIND_DISTINCT) memcpy(out, s->result_h, (size_t)m * s->kw);
     *out_n = m;
     if (!s->cfg.reusable) s->open = false;  // SingleUse.close, Sampler.scala:188-191, :345-350
     return RSV_OK;

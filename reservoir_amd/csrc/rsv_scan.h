@@ -88,7 +88,7 @@ __device__ __forceinline__ void drain_queue(const DrawKey& dk, const uint64_t* q
 // bytes where they are found would cost the whole wave every iteration, so the iteration only
 // tests "any zero byte" and pushes the raw block (g, 4 words = 24 B); decoding and the level-1
 // draws run at drain time, 64 blocks at once.
-constexpr uint32_t kBlockQueue = 128;  // entries of 3 x u64 per wave
+constexpr uint32_t kBlockQueue = 192;  // entries of 3 x u64 per wave (>= 63 + 64 U, U <= 2)
 
 template <class Hit>
 __device__ __forceinline__ void resolve_block(const DrawKey& dk, uint64_t g, const u32x4& w,
@@ -110,21 +110,33 @@ __device__ __forceinline__ void load_block(const uint64_t* q, uint32_t pos, uint
     w = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
 }
 
-template <class Hit>
-__device__ __forceinline__ void push_block(bool has, uint64_t g, const u32x4& w, uint64_t* q,
-                                           uint32_t& qn, uint32_t lane, const DrawKey& dk,
-                                           uint64_t lo, uint64_t hi, uint64_t dense_lim, uint32_t k,
-                                           Hit& hit) {
-    const unsigned long long bal = __ballot(has);
-    if (bal == 0) return;
-    if (has) {
-        const uint32_t pos = qn + __popcll(bal & lanemask_lt64());
-        q[3 * pos] = g;
-        q[3 * pos + 1] = ((uint64_t)w.y << 32) | w.x;
-        q[3 * pos + 2] = ((uint64_t)w.w << 32) | w.z;
+// Push the U blocks of one iteration (has[u]: block u of this lane holds a candidate) with one
+// wave-uniform branch; whenever 64 blocks wait, all lanes resolve one each.  Queue capacity must be
+// >= 63 + 64 U entries.
+template <int U, class Hit>
+__device__ __forceinline__ void push_blocks(const bool (&has)[U], const uint64_t (&g)[U],
+                                            const u32x4 (&w)[U], uint64_t* q, uint32_t& qn,
+                                            uint32_t lane, const DrawKey& dk, uint64_t lo, uint64_t hi,
+                                            uint64_t dense_lim, uint32_t k, Hit& hit) {
+    unsigned long long bal[U], any = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        bal[u] = __ballot(has[u]);
+        any |= bal[u];
     }
-    qn += (uint32_t)__popcll(bal);
-    if (qn >= 64) {
+    if (any == 0) return;
+    const unsigned long long lt = lanemask_lt64();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (has[u]) {
+            const uint32_t pos = qn + __popcll(bal[u] & lt);
+            q[3 * pos] = g[u];
+            q[3 * pos + 1] = ((uint64_t)w[u].y << 32) | w[u].x;
+            q[3 * pos + 2] = ((uint64_t)w[u].w << 32) | w[u].z;
+        }
+        qn += (uint32_t)__popcll(bal[u]);
+    }
+    while (qn >= 64) {
         qn -= 64;
         __builtin_amdgcn_wave_barrier();
         uint64_t gg;

@@ -98,6 +98,7 @@ class GpuSampler:
         h = C.c_void_p()
         N.check(self._L.rsv_create(C.byref(cfg), C.byref(h)))
         self._h = h
+        self._stream = int(self._L.rsv_get_stream(h) or 0)
         self._precomputed = hash_kind == N.HASH_PRECOMPUTED
 
     # -- lifecycle ----------------------------------------------------------------------------
@@ -128,10 +129,12 @@ class GpuSampler:
 
     @property
     def stream(self) -> int:
-        return int(self._L.rsv_get_stream(self._h) or 0)
+        return self._stream
 
     def set_stream(self, hip_stream: int) -> None:
+        """Run this sampler's work on ``hip_stream`` (e.g. torch.cuda.current_stream().cuda_stream)."""
         N.check(self._L.rsv_set_stream(self._h, C.c_void_p(hip_stream)))
+        self._stream = int(hip_stream)
 
     def synchronize(self) -> None:
         N.check(self._L.rsv_synchronize(self._h))

@@ -91,12 +91,11 @@ __global__ __launch_bounds__(256) void k1_var(DrawKey dk, uint32_t k, uint64_t l
             g[u] = g_begin + base + u * 64 + lane;
             w[u] = level0(dk, g[u]);
         }
+        bool has[UNROLL];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const uint64_t gi = base + u * 64 + lane;
-            const bool has = gi < n_groups && (((g[u] << 4) + 1 < dense_lim) || any_zero_byte(w[u]));
-            push_block(has, g[u], w[u], q, qn, lane, dk, lo, hi, dense_lim, k, hit);
-        }
+        for (int u = 0; u < UNROLL; ++u)
+            has[u] = base + u * 64 + lane < n_groups && (((g[u] << 4) + 1 < dense_lim) || any_zero_byte(w[u]));
+        push_blocks<UNROLL>(has, g, w, q, qn, lane, dk, lo, hi, dense_lim, k, hit);
     }
     drain_blocks(q, qn, lane, dk, lo, hi, dense_lim, k, hit);
 }
@@ -165,10 +164,9 @@ int main(int argc, char** argv) {
         printf("%-28s grid %6d unroll %d  %8.1f us per 1e9 indices\n", name, grid, unroll, ms / 5 * 1e3);
         return 0;
     };
-    for (int grid : {1024, 2048, 4096}) {
+    for (int grid : {2048, 4096, 8192}) {
         time_v(k1_var<1>, "k1 block-queue", grid, 1);
         time_v(k1_var<2>, "k1 block-queue", grid, 2);
-        time_v(k1_var<4>, "k1 block-queue", grid, 4);
     }
     return 0;
 }
