@@ -88,8 +88,7 @@ __device__ __forceinline__ uint32_t zero_byte_mask16(const u32x4& w) {
         const uint32_t x = word_of(w, q);
         const uint32_t y = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte
         // gather bits 7, 15, 23, 31 -> 4 bits
-        const uint32_t nib = ((y >> 7) & 1u) | ((y >> 14) & 2u) | ((y >> 21) & 4u) | ((y >> 28) & 8u);
-        m |= nib << (4 * q);
+        m |= (((y >> 7) & 1u) | ((y >> 14) & 2u) | ((y >> 21) & 4u) | ((y >> 28) & 8u)) << (4 * q);
     }
     return m;
 }

@@ -26,17 +26,39 @@ __device__ __forceinline__ uint32_t clip_mask16(uint64_t i0, uint64_t lo, uint64
 }
 
 // Candidate mask of one level-0 block: bit e set iff b_{i0+e} * (i0+e+1) < 256k (a necessary
-// condition for j < k).  Beyond index 256k-1 this is simply "byte == 0" (1 in 256).
+// condition for j < k).  Beyond index 256k-1 this is simply "byte == 0" (1 in 256).  In the dense
+// region (K2's whole 4096-element streams at k = 64) a SWAR test "byte < T" with the block's
+// threshold T = ceil(256k / (i0+1)) (computed in fp32, rounded up) gives a superset with three
+// VALU ops per word; the few set bits are then checked exactly.
+__device__ __forceinline__ uint32_t gather_bit7(uint32_t y) {  // bits 7, 15, 23, 31 -> 0..3
+    return ((y >> 7) & 1u) | ((y >> 14) & 2u) | ((y >> 21) & 4u) | ((y >> 28) & 8u);
+}
+
 __device__ __forceinline__ uint32_t candidate_mask16(const u32x4& w, uint64_t i0, uint64_t dense_lim) {
     if (i0 + 1 >= dense_lim) {
         if (!any_zero_byte(w)) return 0u;
         return zero_byte_mask16(w);
     }
-    uint32_t m = 0;
+    const float tf = __fdividef((float)dense_lim, (float)(i0 + 1));
+    uint32_t sup;
+    if (tf <= 125.0f) {
+        const uint32_t T = (uint32_t)tf + 2u;  // >= the exact ceiling, <= 127
+        const uint32_t C = (128u - T) * 0x01010101u;
+        sup = 0;
 #pragma unroll
-    for (uint32_t e = 0; e < 16; ++e) {
-        const uint64_t b = level0_byte(w, e);
-        if (b * (i0 + e + 1) < dense_lim) m |= 1u << e;
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t x = word_of(w, q);
+            const uint32_t lt = ~(((x & 0x7F7F7F7Fu) + C) | x) & 0x80808080u;  // byte < T
+            sup |= gather_bit7(lt) << (4 * q);
+        }
+    } else {
+        sup = 0xFFFFu;
+    }
+    uint32_t m = 0;
+    while (sup) {
+        const uint32_t e = __builtin_ctz(sup);
+        sup &= sup - 1;
+        if ((uint64_t)level0_byte(w, e) * (i0 + e + 1) < dense_lim) m |= 1u << e;
     }
     return m;
 }

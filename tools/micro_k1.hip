@@ -71,8 +71,9 @@ __global__ __launch_bounds__(256) void philox_only(DrawKey dk, uint64_t n_groups
     if (c == 0x12345u) atomicAdd(cnt, c);
 }
 
-// V2: full K1 (block queue), UNROLL level-0 blocks per lane per iteration
-template <int UNROLL>
+// V2: full K1 (block queue), UNROLL level-0 blocks per lane per iteration; MODE 1 = never push,
+// MODE 2 = push but resolve nothing (ablation)
+template <int UNROLL, int MODE = 0>
 __global__ __launch_bounds__(256) void k1_var(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
                                               uint64_t n_groups, unsigned long long* win) {
     __shared__ uint64_t qs[4][3 * kBlockQueue];
@@ -95,9 +96,21 @@ __global__ __launch_bounds__(256) void k1_var(DrawKey dk, uint32_t k, uint64_t l
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u)
             has[u] = base + u * 64 + lane < n_groups && (((g[u] << 4) + 1 < dense_lim) || any_zero_byte(w[u]));
-        push_blocks<UNROLL>(has, g, w, q, qn, lane, dk, lo, hi, dense_lim, k, hit);
+        if (MODE == 1) {
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) qn += has[u] ? 1 : 0;
+        } else if (MODE == 2) {
+            auto nohit = [&](uint32_t, uint64_t) {};
+            push_blocks<UNROLL>(has, g, w, q, qn, lane, dk, lo, 0, dense_lim, k, nohit);
+        } else {
+            push_blocks<UNROLL>(has, g, w, q, qn, lane, dk, lo, hi, dense_lim, k, hit);
+        }
     }
-    drain_blocks(q, qn, lane, dk, lo, hi, dense_lim, k, hit);
+    if (MODE == 1) {
+        if (qn == 0xFFFFFFFFu) win[0] = qn;
+    } else {
+        drain_blocks(q, qn, lane, dk, lo, hi, dense_lim, k, hit);
+    }
 }
 
 int main(int argc, char** argv) {
@@ -164,9 +177,10 @@ int main(int argc, char** argv) {
         printf("%-28s grid %6d unroll %d  %8.1f us per 1e9 indices\n", name, grid, unroll, ms / 5 * 1e3);
         return 0;
     };
-    for (int grid : {2048, 4096, 8192}) {
-        time_v(k1_var<1>, "k1 block-queue", grid, 1);
+    for (int grid : {4096, 8192}) {
         time_v(k1_var<2>, "k1 block-queue", grid, 2);
+        time_v(k1_var<2, 1>, "k1 ablate: no push", grid, 2);
+        time_v(k1_var<2, 2>, "k1 ablate: push, no resolve", grid, 2);
     }
     return 0;
 }
