@@ -230,13 +230,15 @@ struct DistinctState {
     int64_t r0 = 0, r1 = 0;
     int64_t m = 0;                // current set size
     int64_t max_h = INT64_MIN;    // valid when m == k
-    int64_t* set_h = nullptr;     // [k], ascending (h, key)
-    void* set_k = nullptr;        // [k]
-    int64_t cand_cap = 0;
+    int64_t* set_h = nullptr;     // [set_cap <= k], ascending (h, key)
+    void* set_k = nullptr;
+    int64_t set_cap = 0;
+    int64_t cand_limit = 0;       // 4k + 4096: the most candidates one filter pass may keep
+    int64_t cand_cap = 0;         // allocated (grows on demand up to cand_limit)
     int64_t* cand_h = nullptr;
     void* cand_k = nullptr;
     unsigned long long* counter = nullptr;
-    int64_t merge_cap = 0;        // k + cand_cap
+    int64_t merge_cap = 0;        // set + candidates of one merge (grows on demand)
     int64_t *mh0 = nullptr, *mh1 = nullptr;
     void *mk0 = nullptr, *mk1 = nullptr;
     uint32_t *flags = nullptr, *pos = nullptr;
@@ -270,6 +272,68 @@ static hipError_t temp_bytes_for(int64_t cap, size_t* bytes) {
     return hipSuccess;
 }
 
+// Device buffers grow on demand (geometric, capped): a sampler with a huge k that sees few
+// elements (k may be up to Int.MaxValue - 2, Sampler.scala:71) allocates for what it holds.
+static hipError_t grow(void** p, size_t old_bytes, size_t new_bytes, bool keep, hipStream_t st) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, new_bytes ? new_bytes : 16);
+    if (e != hipSuccess) return e;
+    if (keep && *p && old_bytes) {
+        e = hipMemcpyAsync(q, *p, old_bytes, hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            (void)hipFree(q);
+            return e;
+        }
+    }
+    if (*p) (void)hipFree(*p);
+    *p = q;
+    return hipSuccess;
+}
+
+static int64_t grown(int64_t cur, int64_t need, int64_t cap) {
+    int64_t c = std::max<int64_t>(cur, 1024);
+    while (c < need) c *= 2;
+    return std::min(c, cap);
+}
+
+static hipError_t ensure_caps(DistinctState* d, int64_t cand_need, int64_t merge_need, hipStream_t st) {
+    const size_t kw = (size_t)d->kw;
+    hipError_t e = hipSuccess;
+    cand_need = std::min(cand_need, d->cand_limit);
+    if (cand_need > d->cand_cap) {
+        const int64_t c = grown(d->cand_cap, cand_need, d->cand_limit);
+        if ((e = grow((void**)&d->cand_h, 0, (size_t)c * 8, false, st))) return e;
+        if ((e = grow(&d->cand_k, 0, (size_t)c * kw, false, st))) return e;
+        d->cand_cap = c;
+    }
+    const int64_t set_need = std::min<int64_t>(merge_need, d->k);
+    if (set_need > d->set_cap) {
+        const int64_t c = grown(d->set_cap, set_need, d->k);
+        if ((e = grow((void**)&d->set_h, (size_t)d->m * 8, (size_t)c * 8, true, st))) return e;
+        if ((e = grow(&d->set_k, (size_t)d->m * kw, (size_t)c * kw, true, st))) return e;
+        d->set_cap = c;
+    }
+    if (merge_need > d->merge_cap) {
+        const int64_t c = grown(d->merge_cap, merge_need, (int64_t)d->k + d->cand_limit);
+        if ((e = grow((void**)&d->mh0, 0, (size_t)c * 8, false, st))) return e;
+        if ((e = grow((void**)&d->mh1, 0, (size_t)c * 8, false, st))) return e;
+        if ((e = grow(&d->mk0, 0, (size_t)c * kw, false, st))) return e;
+        if ((e = grow(&d->mk1, 0, (size_t)c * kw, false, st))) return e;
+        if ((e = grow((void**)&d->flags, 0, (size_t)c * 4, false, st))) return e;
+        if ((e = grow((void**)&d->pos, 0, (size_t)c * 4, false, st))) return e;
+        size_t tb = 0;
+        e = d->kw == 8 ? temp_bytes_for<int64_t>(c, &tb) : temp_bytes_for<int32_t>(c, &tb);
+        if (e != hipSuccess) return e;
+        if (tb > d->temp_bytes) {
+            if ((e = grow(&d->temp, 0, tb, false, st))) return e;
+            d->temp_bytes = tb;
+        }
+        d->merge_cap = c;
+    }
+    return hipSuccess;
+}
+
 DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t r0, int64_t r1,
                                int* status) {
     DistinctState* d = new DistinctState();
@@ -278,29 +342,19 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
     d->hash_kind = hash_kind;
     d->r0 = r0;
     d->r1 = r1;
-    d->cand_cap = 4 * (int64_t)k + 4096;
-    d->merge_cap = (int64_t)k + d->cand_cap;
-    const size_t kw = (size_t)key_width;
+    d->cand_limit = 4 * (int64_t)k + 4096;
     hipError_t e = hipSuccess;
     auto A = [&](void** p, size_t bytes) {
         if (e == hipSuccess) e = hipMalloc(p, bytes ? bytes : 16);
     };
-    A((void**)&d->set_h, (size_t)k * 8);
-    A(&d->set_k, (size_t)k * kw);
-    A((void**)&d->cand_h, (size_t)d->cand_cap * 8);
-    A(&d->cand_k, (size_t)d->cand_cap * kw);
     A((void**)&d->counter, 16);
-    A((void**)&d->mh0, (size_t)d->merge_cap * 8);
-    A((void**)&d->mh1, (size_t)d->merge_cap * 8);
-    A(&d->mk0, (size_t)d->merge_cap * kw);
-    A(&d->mk1, (size_t)d->merge_cap * kw);
-    A((void**)&d->flags, (size_t)d->merge_cap * 4);
-    A((void**)&d->pos, (size_t)d->merge_cap * 4);
     A((void**)&d->d_count, 16);
     A((void**)&d->samp, 2 * kSample * 8);
-    if (e == hipSuccess)
-        e = key_width == 8 ? temp_bytes_for<int64_t>(d->merge_cap, &d->temp_bytes)
-                           : temp_bytes_for<int32_t>(d->merge_cap, &d->temp_bytes);
+    if (e == hipSuccess) {
+        size_t tb = 0;  // the threshold sample's sort
+        e = rocprim::radix_sort_keys(nullptr, tb, (int64_t*)nullptr, (int64_t*)nullptr, (size_t)kSample);
+        d->temp_bytes = tb;
+    }
     A(&d->temp, d->temp_bytes);
     if (e == hipSuccess) e = hipHostMalloc((void**)&d->h_pinned, 64, hipHostMallocDefault);
     if (e != hipSuccess) {
@@ -387,7 +441,7 @@ static hipError_t merge_into_set(DistinctState* d, const int64_t* src_h, const K
         *n_distinct = 0;
         return hipSuccess;
     }
-    if (total > d->merge_cap) return hipErrorInvalidValue;
+    if (hipError_t e0 = ensure_caps(d, 0, total, st)) return e0;
     KeyT* mk0 = (KeyT*)d->mk0;
     KeyT* mk1 = (KeyT*)d->mk1;
     hipError_t e;
@@ -457,7 +511,9 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
         return qq >= ns ? t_allowed : std::min(d->samp_host[(size_t)std::max<int64_t>(qq, 0)], t_allowed);
     };
     int64_t tinc = t_allowed;
-    if (!full && n > d->cand_cap / 2) {  // estimate a threshold that passes ~2k elements
+    const bool estimate = !full && n > d->cand_limit / 2;
+    DTRY(ensure_caps(d, estimate ? d->cand_limit : n, 0, st));
+    if (estimate) {  // estimate a threshold that passes ~2k elements
         if (int rc = take_sample()) return rc;
         q = (int64_t)((__int128)(2 * (int64_t)d->k + 1024) * ns / n) + 8;
         tinc = quantile(q);
@@ -473,7 +529,8 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
         if (c > d->cand_cap) {  // threshold too loose for the candidate buffer: tighten
             if (ns == 0) {
                 if (int rc = take_sample()) return rc;
-                q = (int64_t)((__int128)(d->cand_cap / 4) * ns / n);
+                q = (int64_t)((__int128)(d->cand_limit / 4) * ns / n);
+                DTRY(ensure_caps(d, d->cand_limit, 0, st));
             } else {
                 q /= 2;
             }
@@ -517,7 +574,7 @@ int distinct_merge(DistinctState* d, const void* keys_dev, const int64_t* hash_d
                    hipStream_t st) {
     int64_t off = 0;
     while (off < n) {  // chunks that fit the merge buffer
-        const int64_t c = std::min<int64_t>(n - off, d->cand_cap);
+        const int64_t c = std::min<int64_t>(n - off, d->cand_limit);
         int64_t nd = 0;
         hipError_t e = d->kw == 8
                            ? merge_into_set<int64_t>(d, hash_dev + off, (const int64_t*)keys_dev + off, c, &nd, st)

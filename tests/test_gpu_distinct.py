@@ -155,3 +155,16 @@ def test_distinct_merge(cuda, oracle):
     m.merge_state(torch.zeros((parts, 4096), dtype=torch.int64, device=cuda), torch.stack(ks), torch.stack(hs),
                   ns, vals.size)
     assert np.array_equal(m.result(), ref.result()[0])
+
+
+def test_maximum_sample_size(cuda, oracle):
+    """k = Int.MaxValue - 2: the distinct state grows with what it holds, not with k."""
+    from reservoir_amd import Sampler
+
+    k = 2**31 - 1 - 2
+    vals = np.concatenate([oracle.splitmix_keys(2, 300_000)] * 2)
+    d = Sampler.distinct(k, seed=3)(hash="identity")
+    d.sample_all(vals)
+    ref = oracle.Distinct(1 << 20, 3, oracle.HASH_IDENTITY)  # k above the distinct count: all kept
+    ref.sample_all(vals)
+    assert np.array_equal(d.result(), ref.result()[0])

@@ -243,3 +243,14 @@ def test_high_index_offsets(cuda, oracle, i0, k, n):
     hit = idx >= 0
     assert hit.sum() > 0
     assert np.array_equal(gkeys.cpu().numpy()[hit], res[hit])
+
+
+def test_maximum_sample_size(cuda, oracle):
+    """k = Int.MaxValue - 2 is legal (Sampler.scala:71, :80); 24 B x k of HBM state (51 GB)."""
+    from reservoir_amd import Sampler
+
+    k = 2**31 - 1 - 2
+    keys = oracle.splitmix_keys(1, 5000)
+    s = Sampler(k, seed=1)()
+    s.sample_all(keys)
+    assert np.array_equal(s.result(), keys)  # n < k: every element, in order (resultImpl :318-331)
