@@ -9,6 +9,8 @@
 //
 // None of these kernels streams the key array: a draw depends only on (seed, stream, index), so
 // only the k winning keys are ever read (DESIGN.md "Roofline").
+#include <algorithm>
+
 #include "rsv_device.h"
 #include "rsv_internal.h"
 #include "rsv_scan.h"
@@ -28,9 +30,9 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
                                                          uint64_t hi, uint64_t g_begin,
                                                          uint64_t n_groups,
                                                          unsigned long long* __restrict__ win) {
-    __shared__ uint64_t qs[kBlock / 64][3 * kBlockQueue];
+    __shared__ uint32_t qs[kBlock / 64][kBlockQueue];
     const uint32_t lane = threadIdx.x & 63;
-    uint64_t* q = qs[threadIdx.x >> 6];
+    uint32_t* q = qs[threadIdx.x >> 6];
     uint32_t qn = 0;
     auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
     const uint64_t dense_lim = 256ull * k;
@@ -38,19 +40,20 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
     for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * kK1Unroll;
          base < n_groups; base += stride) {
         u32x4 w[kK1Unroll];
-        uint64_t g[kK1Unroll];
+        uint32_t off[kK1Unroll];
 #pragma unroll
         for (int u = 0; u < kK1Unroll; ++u) {
-            g[u] = g_begin + base + u * 64 + lane;
-            w[u] = level0(dk, g[u]);
+            off[u] = (uint32_t)(base + u * 64 + lane);  // n_groups < 2^32 per launch (host splits)
+            w[u] = level0(dk, g_begin + off[u]);
         }
         bool has[kK1Unroll];
 #pragma unroll
         for (int u = 0; u < kK1Unroll; ++u)  // dense region (index < 256k): any block may hit
-            has[u] = base + u * 64 + lane < n_groups && (((g[u] << 4) + 1 < dense_lim) || any_zero_byte(w[u]));
-        push_blocks<kK1Unroll>(has, g, w, q, qn, lane, dk, lo, hi, dense_lim, k, hit);
+            has[u] = off[u] < n_groups &&
+                     ((((g_begin + off[u]) << 4) + 1 < dense_lim) || any_zero_byte(w[u]));
+        push_blocks<kK1Unroll>(has, off, q, qn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
     }
-    drain_blocks(q, qn, lane, dk, lo, hi, dense_lim, k, hit);
+    drain_blocks(q, qn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
 }
 
 template <typename KeyT>
@@ -185,12 +188,17 @@ inline unsigned grid_for(uint64_t items, unsigned cap) {
 hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
                                  unsigned long long* batch_win, hipStream_t st) {
     if (hi <= lo) return hipSuccess;
-    const uint64_t g_begin = lo >> 4, g_end = (hi + 15) >> 4;
-    const uint64_t n_groups = g_end - g_begin;
-    const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 16);
-    hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
-                       g_begin, n_groups, batch_win);
-    return hipGetLastError();
+    const uint64_t g_end = (hi + 15) >> 4;
+    constexpr uint64_t kMaxGroups = 1ull << 31;  // block offsets are 32-bit queue entries
+    for (uint64_t g_begin = lo >> 4; g_begin < g_end; g_begin += kMaxGroups) {
+        const uint64_t n_groups = std::min<uint64_t>(g_end - g_begin, kMaxGroups);
+        const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 32);
+        hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
+                           g_begin, n_groups, batch_win);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,

@@ -39,27 +39,27 @@ __device__ __forceinline__ uint32_t candidate_mask16(const u32x4& w, uint64_t i0
         if (!any_zero_byte(w)) return 0u;
         return zero_byte_mask16(w);
     }
-    const float tf = __fdividef((float)dense_lim, (float)(i0 + 1));
-    uint32_t sup;
-    if (tf <= 125.0f) {
-        const uint32_t T = (uint32_t)tf + 2u;  // >= the exact ceiling, <= 127
+    // T = ceil(dense_lim / (i0+1)): b < T <=> b (i0+1) < dense_lim, exact for the block's first
+    // index and a superset for the other 15 (the level-1 draw decides the hit exactly anyway)
+    uint32_t T = (uint32_t)__fdividef((float)dense_lim, (float)(i0 + 1));
+    if (T <= 130u) {
+        while ((uint64_t)T * (i0 + 1) < dense_lim) ++T;
+        while (T > 0 && (uint64_t)(T - 1) * (i0 + 1) >= dense_lim) --T;
+    }
+    if (T <= 127u) {
         const uint32_t C = (128u - T) * 0x01010101u;
-        sup = 0;
+        uint32_t m = 0;
 #pragma unroll
         for (uint32_t q = 0; q < 4; ++q) {
             const uint32_t x = word_of(w, q);
-            const uint32_t lt = ~(((x & 0x7F7F7F7Fu) + C) | x) & 0x80808080u;  // byte < T
-            sup |= gather_bit7(lt) << (4 * q);
+            m |= gather_bit7(~(((x & 0x7F7F7F7Fu) + C) | x) & 0x80808080u) << (4 * q);  // byte < T
         }
-    } else {
-        sup = 0xFFFFu;
+        return m;
     }
-    uint32_t m = 0;
-    while (sup) {
-        const uint32_t e = __builtin_ctz(sup);
-        sup &= sup - 1;
+    uint32_t m = 0;  // T >= 128: the first ~256k/128 indices of a stream -- exact per byte
+#pragma unroll
+    for (uint32_t e = 0; e < 16; ++e)
         if ((uint64_t)level0_byte(w, e) * (i0 + e + 1) < dense_lim) m |= 1u << e;
-    }
     return m;
 }
 
@@ -104,18 +104,19 @@ __device__ __forceinline__ void drain_queue(const DrawKey& dk, const uint64_t* q
     __builtin_amdgcn_wave_barrier();
 }
 
-// ---- block queue (K1): a wave iteration pushes whole level-0 blocks that hold a candidate ----
+// ---- block queue (K1): a wave iteration pushes the OFFSETS of level-0 blocks that hold a candidate
 // In K1's sparse region (index >= 256k) a block holds a candidate only if one of its 16 bytes is
-// zero (6% of blocks, but ~98% of wave iterations see at least one).  Decoding the candidate
-// bytes where they are found would cost the whole wave every iteration, so the iteration only
-// tests "any zero byte" and pushes the raw block (g, 4 words = 24 B); decoding and the level-1
-// draws run at drain time, 64 blocks at once.
-constexpr uint32_t kBlockQueue = 192;  // entries of 3 x u64 per wave (>= 63 + 64 U, U <= 2)
+// zero (6% of blocks, but ~98% of wave iterations see at least one), so whatever is done per
+// pushed block is paid by the whole wave nearly every iteration.  The iteration therefore only
+// tests "any zero byte" and pushes a 32-bit block offset; at drain time the wave recomputes the
+// level-0 block (one Philox per 64 pushed blocks per lane), decodes it and runs the level-1 draws,
+// 64 blocks at once.  (Pushing the raw 24-B block instead cost 28 us per 1e9 indices.)
+constexpr uint32_t kBlockQueue = 192;  // 32-bit entries per wave (>= 63 + 64 U, U <= 2)
 
 template <class Hit>
-__device__ __forceinline__ void resolve_block(const DrawKey& dk, uint64_t g, const u32x4& w,
-                                              uint64_t lo, uint64_t hi, uint64_t dense_lim,
-                                              uint32_t k, Hit& hit) {
+__device__ __forceinline__ void resolve_block(const DrawKey& dk, uint64_t g, uint64_t lo, uint64_t hi,
+                                              uint64_t dense_lim, uint32_t k, Hit& hit) {
+    const u32x4 w = level0(dk, g);
     const uint64_t i0 = g << 4;
     uint32_t mask = candidate_mask16(w, i0, dense_lim) & clip_mask16(i0, lo, hi);
     while (mask) {
@@ -126,20 +127,12 @@ __device__ __forceinline__ void resolve_block(const DrawKey& dk, uint64_t g, con
     }
 }
 
-__device__ __forceinline__ void load_block(const uint64_t* q, uint32_t pos, uint64_t& g, u32x4& w) {
-    g = q[3 * pos];
-    const uint64_t a = q[3 * pos + 1], b = q[3 * pos + 2];
-    w = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
-}
-
-// Push the U blocks of one iteration (has[u]: block u of this lane holds a candidate) with one
-// wave-uniform branch; whenever 64 blocks wait, all lanes resolve one each.  Queue capacity must be
-// >= 63 + 64 U entries.
+// Push the U blocks of one iteration (has[u]: block g_begin + off[u] holds a candidate) with one
+// wave-uniform branch; whenever 64 blocks wait, all lanes resolve one each.
 template <int U, class Hit>
-__device__ __forceinline__ void push_blocks(const bool (&has)[U], const uint64_t (&g)[U],
-                                            const u32x4 (&w)[U], uint64_t* q, uint32_t& qn,
-                                            uint32_t lane, const DrawKey& dk, uint64_t lo, uint64_t hi,
-                                            uint64_t dense_lim, uint32_t k, Hit& hit) {
+__device__ __forceinline__ void push_blocks(const bool (&has)[U], const uint32_t (&off)[U], uint32_t* q,
+                                            uint32_t& qn, uint32_t lane, const DrawKey& dk, uint64_t g_begin,
+                                            uint64_t lo, uint64_t hi, uint64_t dense_lim, uint32_t k, Hit& hit) {
     unsigned long long bal[U], any = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -150,36 +143,23 @@ __device__ __forceinline__ void push_blocks(const bool (&has)[U], const uint64_t
     const unsigned long long lt = lanemask_lt64();
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        if (has[u]) {
-            const uint32_t pos = qn + __popcll(bal[u] & lt);
-            q[3 * pos] = g[u];
-            q[3 * pos + 1] = ((uint64_t)w[u].y << 32) | w[u].x;
-            q[3 * pos + 2] = ((uint64_t)w[u].w << 32) | w[u].z;
-        }
+        if (has[u]) q[qn + __popcll(bal[u] & lt)] = off[u];
         qn += (uint32_t)__popcll(bal[u]);
     }
     while (qn >= 64) {
         qn -= 64;
         __builtin_amdgcn_wave_barrier();
-        uint64_t gg;
-        u32x4 ww;
-        load_block(q, qn + lane, gg, ww);
-        resolve_block(dk, gg, ww, lo, hi, dense_lim, k, hit);
+        resolve_block(dk, g_begin + q[qn + lane], lo, hi, dense_lim, k, hit);
         __builtin_amdgcn_wave_barrier();
     }
 }
 
 template <class Hit>
-__device__ __forceinline__ void drain_blocks(const uint64_t* q, uint32_t qn, uint32_t lane,
-                                             const DrawKey& dk, uint64_t lo, uint64_t hi,
-                                             uint64_t dense_lim, uint32_t k, Hit& hit) {
+__device__ __forceinline__ void drain_blocks(const uint32_t* q, uint32_t qn, uint32_t lane, const DrawKey& dk,
+                                             uint64_t g_begin, uint64_t lo, uint64_t hi, uint64_t dense_lim,
+                                             uint32_t k, Hit& hit) {
     __builtin_amdgcn_wave_barrier();
-    if (lane < qn) {
-        uint64_t gg;
-        u32x4 ww;
-        load_block(q, lane, gg, ww);
-        resolve_block(dk, gg, ww, lo, hi, dense_lim, k, hit);
-    }
+    if (lane < qn) resolve_block(dk, g_begin + q[lane], lo, hi, dense_lim, k, hit);
 }
 
 }  // namespace rsv

@@ -71,48 +71,6 @@ __global__ __launch_bounds__(256) void philox_only(DrawKey dk, uint64_t n_groups
     if (c == 0x12345u) atomicAdd(cnt, c);
 }
 
-// V2: full K1 (block queue), UNROLL level-0 blocks per lane per iteration; MODE 1 = never push,
-// MODE 2 = push but resolve nothing (ablation)
-template <int UNROLL, int MODE = 0>
-__global__ __launch_bounds__(256) void k1_var(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
-                                              uint64_t n_groups, unsigned long long* win) {
-    __shared__ uint64_t qs[4][3 * kBlockQueue];
-    const uint32_t lane = threadIdx.x & 63;
-    uint64_t* q = qs[threadIdx.x >> 6];
-    uint32_t qn = 0;
-    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
-    const uint64_t dense_lim = 256ull * k;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * UNROLL;
-    for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * UNROLL; base < n_groups;
-         base += stride) {
-        u32x4 w[UNROLL];
-        uint64_t g[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            g[u] = g_begin + base + u * 64 + lane;
-            w[u] = level0(dk, g[u]);
-        }
-        bool has[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u)
-            has[u] = base + u * 64 + lane < n_groups && (((g[u] << 4) + 1 < dense_lim) || any_zero_byte(w[u]));
-        if (MODE == 1) {
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) qn += has[u] ? 1 : 0;
-        } else if (MODE == 2) {
-            auto nohit = [&](uint32_t, uint64_t) {};
-            push_blocks<UNROLL>(has, g, w, q, qn, lane, dk, lo, 0, dense_lim, k, nohit);
-        } else {
-            push_blocks<UNROLL>(has, g, w, q, qn, lane, dk, lo, hi, dense_lim, k, hit);
-        }
-    }
-    if (MODE == 1) {
-        if (qn == 0xFFFFFFFFu) win[0] = qn;
-    } else {
-        drain_blocks(q, qn, lane, dk, lo, hi, dense_lim, k, hit);
-    }
-}
-
 int main(int argc, char** argv) {
     uint32_t* d;
     CK(hipMalloc(&d, 64));
@@ -163,7 +121,7 @@ int main(int argc, char** argv) {
     unsigned long long* win;
     CK(hipMalloc(&win, 1024 * 8));
     CK(hipMemset(win, 0, 1024 * 8));
-    auto time_v = [&](auto kern, const char* name, int grid, int unroll) -> int {
+    [[maybe_unused]] auto time_v = [&](auto kern, const char* name, int grid, int unroll) -> int {
         const uint64_t lo = 1024, hi = 1000000000ull;
         for (int rep = 0; rep < 2; ++rep)
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, dk, 1024u, lo, hi, 0ull, n_groups, win);
@@ -177,10 +135,6 @@ int main(int argc, char** argv) {
         printf("%-28s grid %6d unroll %d  %8.1f us per 1e9 indices\n", name, grid, unroll, ms / 5 * 1e3);
         return 0;
     };
-    for (int grid : {4096, 8192}) {
-        time_v(k1_var<2>, "k1 block-queue", grid, 2);
-        time_v(k1_var<2, 1>, "k1 ablate: no push", grid, 2);
-        time_v(k1_var<2, 2>, "k1 ablate: push, no resolve", grid, 2);
-    }
+
     return 0;
 }
