@@ -49,8 +49,8 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
         bool has[kK1Unroll];
 #pragma unroll
         for (int u = 0; u < kK1Unroll; ++u)  // dense region (index < 256k): any block may hit
-            has[u] = off[u] < n_groups &&
-                     ((((g_begin + off[u]) << 4) + 1 < dense_lim) || any_zero_byte(w[u]));
+            has[u] = (off[u] < n_groups) &  // bitwise: no short-circuit branches
+                     (((((g_begin + off[u]) << 4) + 1) < dense_lim) | any_zero_byte(w[u]));
         push_blocks<kK1Unroll>(has, off, q, qn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
     }
     drain_blocks(q, qn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
