@@ -106,10 +106,16 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RSV_BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU
+    backend = os.environ.get("RSV_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from reservoir_amd import Sampler, _native
     from reservoir_amd import distributed as D
@@ -135,7 +141,7 @@ def main() -> None:
         s.seek(offset)
         s.sample_all(keys)
         if world > 1:
-            D.combine(s, device=dev)
+            D.combine(s, device=dev, total_count=n * world)
         return s.result()
 
     for s in samplers[: args.warmup]:

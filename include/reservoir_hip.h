@@ -115,7 +115,11 @@ rsv_status rsv_result_device(rsv_sampler* s, void* out_dev, int64_t cap, int64_t
 int32_t    rsv_is_open(const rsv_sampler* s); /* Sampler.isOpen (S:67, S:193, S:380) */
 int64_t    rsv_count(const rsv_sampler* s);   /* elements sampled so far (S:203) */
 
-/* Streams: every handle owns a non-blocking HIP stream; a caller may substitute its own. */
+/* Streams: every handle owns a non-blocking HIP stream; a caller may substitute its own.  On the
+ * handle's own stream every call returns with its device work finished (ownership of caller
+ * buffers returns at once); on a caller stream, calls that take or fill DEVICE buffers
+ * (rsv_sample_batch with RSV_MEM_DEVICE, rsv_export_state, rsv_merge_state, rsv_result_device) are
+ * stream-ordered and return without a host wait. */
 rsv_status rsv_set_stream(rsv_sampler* s, void* hip_stream);
 void*      rsv_get_stream(const rsv_sampler* s);
 rsv_status rsv_synchronize(rsv_sampler* s);

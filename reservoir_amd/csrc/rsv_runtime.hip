@@ -517,7 +517,9 @@ rsv_status rsv_export_state(rsv_sampler* s, int64_t* idx_dev, void* keys_dev, in
             RSV_HIP_TRY(hipMemcpyAsync(keys_dev, s->slot_key, (size_t)s->k * s->kw, hipMemcpyDeviceToDevice, s->stream));
         *out_n = s->k;
     }
-    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    // on the handle's private stream the caller cannot order against it: wait; on a caller
+    // stream (rsv_set_stream) the copies are stream-ordered for the caller's next work
+    if (s->own_stream) RSV_HIP_TRY(hipStreamSynchronize(s->stream));
     return RSV_OK;
 }
 
@@ -543,7 +545,7 @@ rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* k
                                        s->stream));
     }
     if (total_count > s->count) s->count = total_count;
-    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    if (s->own_stream) RSV_HIP_TRY(hipStreamSynchronize(s->stream));
     return RSV_OK;
 }
 

@@ -33,29 +33,44 @@ def sample_shard(sampler, keys_local, global_offset: int) -> None:
     sampler.sample_all(keys_local)
 
 
-def combine(sampler, group=None, device=None) -> None:
+def combine(sampler, group=None, device=None, total_count: int | None = None) -> None:
     """All-gather the partial states of every rank and merge them into ``sampler`` (on all ranks).
 
-    One collective: each rank packs [idx(k) | keys(k) | hashes(k) | n | count] into one int64
-    row (3k + 2 words, 24.6 KB at k = 1024) so the exchange pays one RCCL latency, not four.
+    One collective: each rank packs its partial state into one int64 row -- element samplers
+    ``[idx(k) | keys(k)]`` (16 KB at k = 1024), distinct samplers ``[keys(k) | hashes(k) | n]`` --
+    so the exchange pays one RCCL latency.  ``total_count`` (the global stream length) saves a
+    second exchange for element samplers; without it the per-rank counts ride along in the row.
     """
     world = dist.get_world_size(group)
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
     idx, keys, hashes, n = sampler.export_state(device)
     k = keys.numel()
-    row = torch.empty(3 * k + 2, dtype=torch.int64, device=idx.device)
-    row[:k] = idx
-    row[k:2 * k] = keys.to(torch.int64)
-    row[2 * k:3 * k] = hashes
-    row[3 * k] = n
-    row[3 * k + 1] = sampler.count
-    flat = torch.empty(world * (3 * k + 2), dtype=torch.int64, device=idx.device)
+    dev = idx.device
+    if sampler.is_distinct:
+        width = 2 * k + 2
+        row = torch.empty(width, dtype=torch.int64, device=dev)
+        row[:k] = keys.to(torch.int64)
+        row[k:2 * k] = hashes
+        row[2 * k:] = torch.tensor([n, sampler.count], dtype=torch.int64).to(dev, non_blocking=True)
+    else:
+        width = 2 * k + (0 if total_count is not None else 1)
+        row = torch.empty(width, dtype=torch.int64, device=dev)
+        row[:k] = idx
+        row[k:2 * k] = keys.to(torch.int64)
+        if total_count is None:
+            row[2 * k] = sampler.count
+    flat = torch.empty(world * width, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(flat, row, group=group)  # flat output: gloo and RCCL both accept
-    rows = flat.view(world, 3 * k + 2)
-    meta = rows[:, 3 * k:].cpu()
-    part_n = meta[:, 0].tolist()
-    # elements: the stream ends at the largest rank end; distinct: counts add up
-    total = int(meta[:, 1].sum()) if sampler.is_distinct else int(meta[:, 1].max())
-    g_keys = rows[:, k:2 * k].to(keys.dtype).contiguous()
-    sampler.merge_state(rows[:, :k].contiguous(), g_keys, rows[:, 2 * k:3 * k].contiguous(), part_n, total)
+    rows = flat.view(world, width)
+    g_keys = rows[:, (0 if sampler.is_distinct else k):(k if sampler.is_distinct else 2 * k)]
+    g_keys = g_keys.to(keys.dtype).contiguous()
+    if sampler.is_distinct:
+        meta = rows[:, 2 * k:].cpu()
+        part_n = meta[:, 0].tolist()
+        total = int(meta[:, 1].sum()) if total_count is None else int(total_count)
+        sampler.merge_state(torch.empty((world, k), dtype=torch.int64, device=dev), g_keys,
+                            rows[:, k:2 * k].contiguous(), part_n, total)
+    else:
+        total = int(rows[:, 2 * k].max().item()) if total_count is None else int(total_count)
+        sampler.merge_state(rows[:, :k].contiguous(), g_keys, hashes.expand(world, k), [k] * world, total)
