@@ -96,7 +96,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1_000_000_000, help="keys per GPU")
+    ap.add_argument("--keys-per-gpu", dest="n", type=int, default=1_000_000_000)
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--seed", type=int, default=0xC0FFEE)
     ap.add_argument("--stream-id", type=int, default=0x5A5A)
