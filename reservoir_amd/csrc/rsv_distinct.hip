@@ -357,6 +357,11 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
     }
     A(&d->temp, d->temp_bytes);
     if (e == hipSuccess) e = hipHostMalloc((void**)&d->h_pinned, 64, hipHostMallocDefault);
+    // Typical k: allocate the whole working set now (nothing is allocated on the sampling path).
+    // Huge k (up to Int.MaxValue - 2): grow with what the sampler holds.
+    const int64_t full_merge = (int64_t)k + d->cand_limit;
+    const double eager_bytes = (double)full_merge * (2 * 8 + 2 * key_width + 8) + (double)d->cand_limit * (8 + key_width);
+    if (e == hipSuccess && eager_bytes < 512.0 * 1024 * 1024) e = ensure_caps(d, d->cand_limit, full_merge, 0);
     if (e != hipSuccess) {
         set_error(std::string("distinct_create: ") + hipGetErrorString(e));
         *status = e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;
