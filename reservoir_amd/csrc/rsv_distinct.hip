@@ -215,8 +215,9 @@ __global__ __launch_bounds__(kBlock) void compact_first_k(const int64_t* __restr
     if (flags[p] && (int64_t)pos[p] < k) {
         out_h[pos[p]] = h[p];
         out_k[pos[p]] = key[p];
+        if ((int64_t)pos[p] == k - 1) out_count[1] = h[p];  // the new maximum (set full)
     }
-    if (p == n - 1) *out_count = (int64_t)pos[p] + (int64_t)flags[p];
+    if (p == n - 1) out_count[0] = (int64_t)pos[p] + (int64_t)flags[p];
 }
 
 inline unsigned grid_1d(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -459,13 +460,23 @@ static hipError_t merge_into_set(DistinctState* d, const int64_t* src_h, const K
         if ((e = hipMemcpyAsync(mk0 + d->m, src_k, c * sizeof(KeyT), hipMemcpyDeviceToDevice, st))) return e;
     }
     size_t tb = d->temp_bytes;
-    // stable LSD order: by key, then by h  ->  sorted by (h, key)
-    if ((e = rocprim::radix_sort_pairs(d->temp, tb, mk0, mk1, d->mh0, d->mh1, (size_t)total, 0,
-                                       8 * (unsigned)sizeof(KeyT), st)))
-        return e;
-    tb = d->temp_bytes;
-    if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->mh1, d->mh0, mk1, mk0, (size_t)total, 0, 64, st)))
-        return e;
+    if (d->hash_kind == kHashIdentity || d->hash_kind == kHashJavaInt) {
+        // injective hash: equal h <=> equal element, so one sort by h orders (h, key)
+        if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->mh0, d->mh1, mk0, mk1, (size_t)total, 0, 64, st)))
+            return e;
+        std::swap(d->mh0, d->mh1);
+        std::swap(d->mk0, d->mk1);
+        mk0 = (KeyT*)d->mk0;
+        mk1 = (KeyT*)d->mk1;
+    } else {
+        // stable LSD order: by key, then by h  ->  sorted by (h, key)
+        if ((e = rocprim::radix_sort_pairs(d->temp, tb, mk0, mk1, d->mh0, d->mh1, (size_t)total, 0,
+                                           8 * (unsigned)sizeof(KeyT), st)))
+            return e;
+        tb = d->temp_bytes;
+        if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->mh1, d->mh0, mk1, mk0, (size_t)total, 0, 64, st)))
+            return e;
+    }
     hipLaunchKernelGGL(dedup_flags<KeyT>, dim3(grid_1d(total)), dim3(kBlock), 0, st, d->mh0, mk0, total,
                        d->flags);
     if ((e = hipGetLastError())) return e;
@@ -476,15 +487,11 @@ static hipError_t merge_into_set(DistinctState* d, const int64_t* src_h, const K
     hipLaunchKernelGGL(compact_first_k<KeyT>, dim3(grid_1d(total)), dim3(kBlock), 0, st, d->mh0, mk0,
                        d->flags, d->pos, total, (int64_t)d->k, d->set_h, (KeyT*)d->set_k, d->d_count);
     if ((e = hipGetLastError())) return e;
-    if ((e = hipMemcpyAsync(d->h_pinned, d->d_count, 8, hipMemcpyDeviceToHost, st))) return e;
+    if ((e = hipMemcpyAsync(d->h_pinned, d->d_count, 16, hipMemcpyDeviceToHost, st))) return e;
     if ((e = hipStreamSynchronize(st))) return e;
     *n_distinct = d->h_pinned[0];
     d->m = std::min<int64_t>(*n_distinct, d->k);
-    if (d->m == d->k) {
-        if ((e = hipMemcpyAsync(d->h_pinned + 1, d->set_h + d->k - 1, 8, hipMemcpyDeviceToHost, st))) return e;
-        if ((e = hipStreamSynchronize(st))) return e;
-        d->max_h = d->h_pinned[1];
-    }
+    if (d->m == d->k) d->max_h = d->h_pinned[1];
     return hipSuccess;
 }
 
@@ -518,10 +525,14 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
     int64_t tinc = t_allowed;
     const bool estimate = !full && n > d->cand_limit / 2;
     DTRY(ensure_caps(d, estimate ? d->cand_limit : n, 0, st));
-    if (estimate) {  // estimate a threshold that passes ~2k elements
-        if (int rc = take_sample()) return rc;
-        q = (int64_t)((__int128)(2 * (int64_t)d->k + 1024) * ns / n) + 8;
-        tinc = quantile(q);
+    if (estimate) {
+        // The scrambled hash of distinct elements is uniform on int64 (double byteswap64 keyed
+        // by the random r0, r1), so ~2k + 1024 elements fall below INT64_MIN + f 2^64 with
+        // f = (2k + 1024) / n.  Heavy duplication (fewer than half the elements distinct) or a
+        // degenerate precomputed hash shows up as too few / too many candidates and is corrected
+        // from a strided sample below.
+        const long double f = (long double)(2 * (int64_t)d->k + 1024) / (long double)n;
+        tinc = f >= 1.0L ? t_allowed : (int64_t)((long double)INT64_MIN + f * 18446744073709551616.0L);
     }
     for (int attempt = 0; attempt < 128; ++attempt) {
         DTRY(hipMemsetAsync(d->counter, 0, 8, st));
@@ -552,10 +563,15 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
         // bottom-k(S u C2) for C1 a subset of C2)
         if (ns == 0) {
             if (int rc = take_sample()) return rc;
-            q = 0;
+            q = (int64_t)(std::upper_bound(d->samp_host.begin(), d->samp_host.end(), tinc) - d->samp_host.begin());
         }
         q = q < 16 ? 64 : q * 4;
-        tinc = quantile(q);
+        int64_t t = quantile(q);
+        if (t <= tinc) {  // coarse sample: double the distance from INT64_MIN instead
+            const uint64_t span = (uint64_t)tinc - (uint64_t)INT64_MIN;
+            t = span >= (uint64_t)t_allowed - (uint64_t)tinc ? t_allowed : (int64_t)((uint64_t)tinc + span + 1);
+        }
+        tinc = std::min(t, t_allowed);
     }
     set_error("distinct: threshold search did not converge");
     return RSV_E_DEVICE;
