@@ -119,8 +119,13 @@ struct rsv_sampler {
     DistinctState* distinct = nullptr;
     int hash_kind = kHashIdentity;
     // host staging: per-element calls and host batches
-    uint8_t* stage_h = nullptr;  // pinned, stage_cap keys
-    int64_t* stage_hash_h = nullptr;
+    // per-element sample(): two pinned staging buffers; a full one is flushed asynchronously
+    // (H2D + kernels, no host wait) while the other fills; an event says when it is free again
+    uint8_t* stage_h[2] = {nullptr, nullptr};
+    int64_t* stage_hash_h[2] = {nullptr, nullptr};
+    hipEvent_t stage_free[2] = {nullptr, nullptr};
+    bool stage_pending[2] = {false, false};
+    int stage_cur = 0;
     int64_t stage_n = 0;
     int64_t stage_cap = 0;
     void* chunk_d = nullptr;     // device chunk for host batches
@@ -232,11 +237,21 @@ rsv_status process_host_batch(rsv_sampler* s, const void* keys, const int64_t* h
     return RSV_OK;
 }
 
+// Flush the current staging buffer: H2D into the device chunk, record "buffer free", launch the
+// batch's kernels -- all stream-ordered, no host wait -- and switch to the other buffer.
 rsv_status flush_stage(rsv_sampler* s) {
     if (s->stage_n == 0) return RSV_OK;
     const int64_t n = s->stage_n;
+    const int b = s->stage_cur;
     s->stage_n = 0;
-    return process_host_batch(s, s->stage_h, s->stage_hash_h, n);
+    if (rsv_status st = ensure_chunk(s)) return st;
+    RSV_HIP_TRY(hipMemcpyAsync(s->chunk_d, s->stage_h[b], n * s->kw, hipMemcpyHostToDevice, s->stream));
+    if (s->chunk_hash_d && s->stage_hash_h[b])
+        RSV_HIP_TRY(hipMemcpyAsync(s->chunk_hash_d, s->stage_hash_h[b], n * 8, hipMemcpyHostToDevice, s->stream));
+    RSV_HIP_TRY(hipEventRecord(s->stage_free[b], s->stream));
+    s->stage_pending[b] = true;
+    s->stage_cur = b ^ 1;
+    return process_device_batch(s, s->chunk_d, s->chunk_hash_d, n);
 }
 
 void free_all(rsv_sampler* s) {
@@ -244,9 +259,12 @@ void free_all(rsv_sampler* s) {
                   s->chunk_hash_d};
     for (void* p : ds)
         if (p) (void)hipFree(p);
-    if (s->stage_h) (void)hipHostFree(s->stage_h);
+    for (int b = 0; b < 2; ++b) {
+        if (s->stage_h[b]) (void)hipHostFree(s->stage_h[b]);
+        if (s->stage_hash_h[b]) (void)hipHostFree(s->stage_hash_h[b]);
+        if (s->stage_free[b]) (void)hipEventDestroy(s->stage_free[b]);
+    }
     if (s->result_h) (void)hipHostFree(s->result_h);
-    if (s->stage_hash_h) (void)hipHostFree(s->stage_hash_h);
     if (s->distinct) distinct_destroy(s->distinct);
     if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
 }
@@ -373,13 +391,21 @@ rsv_status rsv_sample(rsv_sampler* s, const void* key, const int64_t* hash) {
     const bool pre = s->cfg.kind == RSV_KIND_DISTINCT && s->hash_kind == kHashPrecomputed;
     if (pre && !hash) return fail(RSV_E_NULL_POINTER, "hash is NULL for RSV_HASH_PRECOMPUTED");
     DeviceGuard g(s->device);
-    if (!s->stage_h) {
-        RSV_HIP_TRY(hipHostMalloc((void**)&s->stage_h, kStageKeys * s->kw, hipHostMallocDefault));
-        if (pre) RSV_HIP_TRY(hipHostMalloc((void**)&s->stage_hash_h, kStageKeys * 8, hipHostMallocDefault));
+    if (!s->stage_h[0]) {
+        for (int b = 0; b < 2; ++b) {
+            RSV_HIP_TRY(hipHostMalloc((void**)&s->stage_h[b], kStageKeys * s->kw, hipHostMallocDefault));
+            if (pre) RSV_HIP_TRY(hipHostMalloc((void**)&s->stage_hash_h[b], kStageKeys * 8, hipHostMallocDefault));
+            RSV_HIP_TRY(hipEventCreateWithFlags(&s->stage_free[b], hipEventDisableTiming));
+        }
         s->stage_cap = kStageKeys;
     }
-    memcpy(s->stage_h + s->stage_n * s->kw, key, s->kw);
-    if (pre) s->stage_hash_h[s->stage_n] = *hash;
+    const int b = s->stage_cur;
+    if (s->stage_n == 0 && s->stage_pending[b]) {  // its previous batch's H2D must have read it
+        RSV_HIP_TRY(hipEventSynchronize(s->stage_free[b]));
+        s->stage_pending[b] = false;
+    }
+    memcpy(s->stage_h[b] + s->stage_n * s->kw, key, s->kw);
+    if (pre) s->stage_hash_h[b][s->stage_n] = *hash;
     if (++s->stage_n == s->stage_cap) return flush_stage(s);
     return RSV_OK;
 }
