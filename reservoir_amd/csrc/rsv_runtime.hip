@@ -385,12 +385,12 @@ void rsv_destroy(rsv_sampler* s) {
     delete s;
 }
 
-rsv_status rsv_sample(rsv_sampler* s, const void* key, const int64_t* hash) {
-    if (rsv_status st = check_open(s)) return st;
-    if (!key) return fail(RSV_E_NULL_POINTER, "key is NULL");
-    const bool pre = s->cfg.kind == RSV_KIND_DISTINCT && s->hash_kind == kHashPrecomputed;
-    if (pre && !hash) return fail(RSV_E_NULL_POINTER, "hash is NULL for RSV_HASH_PRECOMPUTED");
+// Slow part of rsv_sample: (re)arm a staging buffer, or flush a full one.  Runs once per batch.
+static rsv_status stage_slow(rsv_sampler* s, bool pre) {
     DeviceGuard g(s->device);
+    if (s->stage_n == s->stage_cap && s->stage_cap) {
+        if (rsv_status st = flush_stage(s)) return st;
+    }
     if (!s->stage_h[0]) {
         for (int b = 0; b < 2; ++b) {
             RSV_HIP_TRY(hipHostMalloc((void**)&s->stage_h[b], kStageKeys * s->kw, hipHostMallocDefault));
@@ -404,9 +404,23 @@ rsv_status rsv_sample(rsv_sampler* s, const void* key, const int64_t* hash) {
         RSV_HIP_TRY(hipEventSynchronize(s->stage_free[b]));
         s->stage_pending[b] = false;
     }
-    memcpy(s->stage_h[b] + s->stage_n * s->kw, key, s->kw);
+    return RSV_OK;
+}
+
+rsv_status rsv_sample(rsv_sampler* s, const void* key, const int64_t* hash) {
+    // per-element hot path (the akka operator calls this per element): no HIP call here
+    if (!s || !s->open) return check_open(s);
+    if (!key) return fail(RSV_E_NULL_POINTER, "key is NULL");
+    const bool pre = s->hash_kind == kHashPrecomputed && s->cfg.kind == RSV_KIND_DISTINCT;
+    if (pre && !hash) return fail(RSV_E_NULL_POINTER, "hash is NULL for RSV_HASH_PRECOMPUTED");
+    if (s->stage_n == 0 || s->stage_n == s->stage_cap) {
+        if (rsv_status st = stage_slow(s, pre)) return st;
+    }
+    const int b = s->stage_cur;
+    if (s->kw == 8) memcpy(s->stage_h[b] + s->stage_n * 8, key, 8);
+    else memcpy(s->stage_h[b] + s->stage_n * 4, key, 4);
     if (pre) s->stage_hash_h[b][s->stage_n] = *hash;
-    if (++s->stage_n == s->stage_cap) return flush_stage(s);
+    ++s->stage_n;
     return RSV_OK;
 }
 
