@@ -9,8 +9,6 @@
 //
 // None of these kernels streams the key array: a draw depends only on (seed, stream, index), so
 // only the k winning keys are ever read (DESIGN.md "Roofline").
-#include <stdlib.h>
-
 #include <algorithm>
 
 #include "rsv_device.h"
@@ -258,8 +256,7 @@ hipError_t launch_k1_resolve(const DrawParams& dp, uint32_t k, uint64_t lo, uint
                              unsigned long long* batch_win, const void* keys, int key_width, int64_t base,
                              int64_t n, void* slot_key, int64_t* slot_idx, unsigned int* done, hipStream_t st,
                              bool* fused) {
-    static const bool no_fuse = getenv("RSV_K1_UNFUSED") != nullptr;  // A/B switch for measurements
-    *fused = hi > lo && k <= kFuseMaxK && done != nullptr && !no_fuse;
+    *fused = hi > lo && k <= kFuseMaxK && done != nullptr;
     if (!*fused) return launch_k1_last_writer(dp, k, lo, hi, batch_win, st);
     if (key_width == 8) {
         const FusedResolve<int64_t> fr{(const int64_t*)keys, base, n, (int64_t*)slot_key, slot_idx, done};
