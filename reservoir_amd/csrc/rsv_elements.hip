@@ -28,10 +28,9 @@ constexpr int kK1Unroll = 2;  // level-0 blocks per lane per iteration (two Phil
 
 // Resolve fused into K1 (k <= kFuseMaxK): the last workgroup to finish applies the fill phase
 // and the winners of the batch, saving a kernel boundary and a launch per batch.  Hand-off per
-// MI355X_MICROARCH.md "inter-workgroup visibility" (valid form "8-B agent atomics both sides"):
-// every wave drains its winner atomics (vmcnt(0)), the workgroup barriers, one lane takes an
-// agent-scope ticket; the last ticket holder reads the table with agent-scope atomic loads.
-// (A release fence per workgroup instead cost ~14 us per launch: more than the launch it saves.)
+// MI355X_MICROARCH.md "inter-workgroup visibility": every wave drains its atomics (vmcnt(0)),
+// the workgroup barriers, one lane releases (agent) and takes a ticket; the last ticket holder
+// acquires (agent) and reads the winner table with agent-scope atomic loads.
 constexpr uint32_t kFuseMaxK = 1u << 16;
 
 template <typename KeyT>
@@ -94,11 +93,14 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
         __shared__ uint32_t last;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's winner atomics are done
         __syncthreads();
-        // the winner table is written only by agent-scope atomics and read only by agent-scope
-        // atomic loads ("8-B agent atomics both sides"), so no release/acquire fence is needed
-        if (threadIdx.x == 0) last = atomicAdd(fr.done, 1u) == gridDim.x - 1 ? 1u : 0u;
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            last = atomicAdd(fr.done, 1u) == gridDim.x - 1 ? 1u : 0u;
+        }
         __syncthreads();
         if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             for (uint32_t j = threadIdx.x; j < k; j += blockDim.x)
                 resolve_slot<KeyT>(j, fr.keys, fr.base, fr.n, win, fr.slot_key, fr.slot_idx, true);
             if (threadIdx.x == 0) *fr.done = 0u;  // re-armed for the next launch
