@@ -26,45 +26,10 @@ constexpr int kBlock = 256;
 // atomicMax on the k-slot winner table: 14k atomics per 1e9 indices at k = 1024.
 constexpr int kK1Unroll = 2;  // level-0 blocks per lane per iteration (two Philox chains in flight)
 
-// Resolve fused into K1 (k <= kFuseMaxK): the last workgroup to finish applies the fill phase
-// and the winners of the batch, saving a kernel boundary and a launch per batch.  Hand-off per
-// MI355X_MICROARCH.md "inter-workgroup visibility": every wave drains its atomics (vmcnt(0)),
-// the workgroup barriers, one lane releases (agent) and takes a ticket; the last ticket holder
-// acquires (agent) and reads the winner table with agent-scope atomic loads.
-constexpr uint32_t kFuseMaxK = 1u << 16;
-
-template <typename KeyT>
-struct FusedResolve {
-    const KeyT* keys;
-    int64_t base, n;
-    KeyT* slot_key;
-    int64_t* slot_idx;
-    unsigned int* done;  // ticket counter, zero between launches
-};
-
-template <typename KeyT>
-__device__ __forceinline__ void resolve_slot(uint32_t j, const KeyT* __restrict__ keys, int64_t base, int64_t n,
-                                             unsigned long long* __restrict__ win, KeyT* __restrict__ slot_key,
-                                             int64_t* __restrict__ slot_idx, bool atomic_read) {
-    if ((int64_t)j >= base && (int64_t)j < base + n) {  // fill phase (Sampler.scala:253-255)
-        slot_key[j] = keys[j - base];
-        if (slot_idx) slot_idx[j] = j;
-    }
-    const unsigned long long wi =
-        atomic_read ? __hip_atomic_load(&win[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : win[j];
-    if (wi) {  // last eviction into slot j in this batch (Sampler.scala:243-246)
-        slot_key[j] = keys[(int64_t)wi - base];
-        if (slot_idx) slot_idx[j] = (int64_t)wi;
-        win[j] = 0;
-    }
-}
-
-template <typename KeyT, bool FUSE>
 __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k, uint64_t lo,
                                                          uint64_t hi, uint64_t g_begin,
                                                          uint64_t n_groups,
-                                                         unsigned long long* __restrict__ win,
-                                                         FusedResolve<KeyT> fr) {
+                                                         unsigned long long* __restrict__ win) {
     __shared__ uint32_t qs[kBlock / 64][kBlockQueue];
     const uint32_t lane = threadIdx.x & 63;
     uint32_t* q = qs[threadIdx.x >> 6];
@@ -89,23 +54,6 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
         push_blocks<kK1Unroll>(has, off, q, qn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
     }
     drain_blocks(q, qn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
-    if constexpr (FUSE) {
-        __shared__ uint32_t last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's winner atomics are done
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            last = atomicAdd(fr.done, 1u) == gridDim.x - 1 ? 1u : 0u;
-        }
-        __syncthreads();
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            for (uint32_t j = threadIdx.x; j < k; j += blockDim.x)
-                resolve_slot<KeyT>(j, fr.keys, fr.base, fr.n, win, fr.slot_key, fr.slot_idx, true);
-            if (threadIdx.x == 0) *fr.done = 0u;  // re-armed for the next launch
-        }
-    }
 }
 
 template <typename KeyT>
@@ -115,7 +63,17 @@ __global__ __launch_bounds__(kBlock) void resolve_kernel(const KeyT* __restrict_
                                                          KeyT* __restrict__ slot_key,
                                                          int64_t* __restrict__ slot_idx) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < k) resolve_slot<KeyT>(j, keys, base, n, win, slot_key, slot_idx, false);
+    if (j >= k) return;
+    if ((int64_t)j >= base && (int64_t)j < base + n) {  // fill phase (Sampler.scala:253-255)
+        slot_key[j] = keys[j - base];
+        if (slot_idx) slot_idx[j] = j;
+    }
+    const unsigned long long wi = win[j];
+    if (wi) {  // last eviction into slot j in this batch (Sampler.scala:243-246)
+        slot_key[j] = keys[(int64_t)wi - base];
+        if (slot_idx) slot_idx[j] = (int64_t)wi;
+        win[j] = 0;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void replay_kernel(const int64_t* __restrict__ ev_pos,
@@ -227,45 +185,20 @@ inline unsigned grid_for(uint64_t items, unsigned cap) {
 
 }  // namespace
 
-template <typename KeyT>
-static hipError_t k1_launches(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
-                              unsigned long long* batch_win, const FusedResolve<KeyT>* fr, hipStream_t st) {
+hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
+                                 unsigned long long* batch_win, hipStream_t st) {
+    if (hi <= lo) return hipSuccess;
     const uint64_t g_end = (hi + 15) >> 4;
     constexpr uint64_t kMaxGroups = 1ull << 31;  // block offsets are 32-bit queue entries
     for (uint64_t g_begin = lo >> 4; g_begin < g_end; g_begin += kMaxGroups) {
         const uint64_t n_groups = std::min<uint64_t>(g_end - g_begin, kMaxGroups);
         const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 32);
-        const bool last_chunk = g_begin + n_groups >= g_end;
-        if (fr && last_chunk)
-            hipLaunchKernelGGL((k1_last_writer<KeyT, true>), dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo,
-                               hi, g_begin, n_groups, batch_win, *fr);
-        else
-            hipLaunchKernelGGL((k1_last_writer<KeyT, false>), dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo,
-                               hi, g_begin, n_groups, batch_win, FusedResolve<KeyT>{});
+        hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
+                           g_begin, n_groups, batch_win);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
-}
-
-hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
-                                 unsigned long long* batch_win, hipStream_t st) {
-    if (hi <= lo) return hipSuccess;
-    return k1_launches<int64_t>(dp, k, lo, hi, batch_win, nullptr, st);
-}
-
-hipError_t launch_k1_resolve(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
-                             unsigned long long* batch_win, const void* keys, int key_width, int64_t base,
-                             int64_t n, void* slot_key, int64_t* slot_idx, unsigned int* done, hipStream_t st,
-                             bool* fused) {
-    *fused = hi > lo && k <= kFuseMaxK && done != nullptr;
-    if (!*fused) return launch_k1_last_writer(dp, k, lo, hi, batch_win, st);
-    if (key_width == 8) {
-        const FusedResolve<int64_t> fr{(const int64_t*)keys, base, n, (int64_t*)slot_key, slot_idx, done};
-        return k1_launches<int64_t>(dp, k, lo, hi, batch_win, &fr, st);
-    }
-    const FusedResolve<int32_t> fr{(const int32_t*)keys, base, n, (int32_t*)slot_key, slot_idx, done};
-    return k1_launches<int32_t>(dp, k, lo, hi, batch_win, &fr, st);
 }
 
 hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,

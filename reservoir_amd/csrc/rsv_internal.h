@@ -65,12 +65,6 @@ struct DrawParams {
 // batch_win[k] (0 = no writer in this batch; atomicMax keeps the largest index).
 hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
                                  unsigned long long* batch_win, hipStream_t st);
-// K1 with the resolve fused into its last workgroup when k is small enough (*fused = true);
-// otherwise plain K1 and the caller launches launch_resolve.  `done` = zeroed ticket counter.
-hipError_t launch_k1_resolve(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
-                             unsigned long long* batch_win, const void* keys, int key_width, int64_t base,
-                             int64_t n, void* slot_key, int64_t* slot_idx, unsigned int* done, hipStream_t st,
-                             bool* fused);
 // Resolve: fill phase for slots in [base, base+n) and winners of batch_win; resets batch_win.
 // slot_idx may be null.
 hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,

@@ -108,7 +108,7 @@ struct rsv_sampler {
     // ELEMENTS
     void* slot_key = nullptr;
     int64_t* slot_idx = nullptr;
-    unsigned long long* batch_win = nullptr;  // k winner slots + the fused-resolve ticket counter
+    unsigned long long* batch_win = nullptr;
     AlgoLState algo_l;
     std::vector<int64_t> ev_pos_h;
     std::vector<int32_t> ev_slot_h;
@@ -203,13 +203,10 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
     } else {
         const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
         const uint64_t lo = std::max<uint64_t>((uint64_t)base, s->k), hi = (uint64_t)(base + n);
-        bool fused = false;
         s->timer.mark(s->stream);
-        RSV_HIP_TRY(launch_k1_resolve(dp, s->k, lo, hi, s->batch_win, keys, s->kw, base, n, s->slot_key,
-                                      s->slot_idx, (unsigned int*)(s->batch_win + s->k), s->stream, &fused));
+        RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
         s->timer.mark(s->stream);
-        if (!fused)
-            RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, s->stream));
+        RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, s->stream));
     }
     s->count = base + n;
     return RSV_OK;
@@ -353,10 +350,10 @@ rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out) {
         const size_t k = s->k;
         e = hipMalloc(&s->slot_key, k * s->kw);
         if (e == hipSuccess) e = hipMalloc((void**)&s->slot_idx, k * 8);
-        if (e == hipSuccess) e = hipMalloc((void**)&s->batch_win, (k + 1) * 8);
+        if (e == hipSuccess) e = hipMalloc((void**)&s->batch_win, k * 8);
         if (e == hipSuccess) e = hipMemsetAsync(s->slot_key, 0, k * s->kw, s->stream);
         if (e == hipSuccess) e = hipMemsetAsync(s->slot_idx, 0xFF, k * 8, s->stream);  // -1 = empty
-        if (e == hipSuccess) e = hipMemsetAsync(s->batch_win, 0, (k + 1) * 8, s->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(s->batch_win, 0, k * 8, s->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
         if (e != hipSuccess)
             return bail(e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE,
