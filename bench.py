@@ -79,6 +79,23 @@ def cpu_baseline(k: int, n_stream: int, seed: int) -> dict:
     }
 
 
+def valu_roofline(n: int, k1_s: float) -> dict:
+    """K1's binding limit: Philox4x32-10 evaluations per second vs the gfx950 VALU peak.
+
+    Per call: 20 v_mad_u64_u32 (3.2 full-rate issue slots each, measured by tools/micro_k1.hip)
+    + 20 v_bitop3 = 84 slots; peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 84.  Calls per launch
+    (expected): one level-0 call per 16 indices, a recompute for the 6.07 % of blocks holding a zero
+    byte, and one level-1 call per candidate (1 in 256 indices).
+    """
+    level0 = n / 16
+    calls = level0 * (1 + (1 - (255 / 256) ** 16)) + n / 256
+    peak = 256 * 4 * 32 * 2.4e9 / 84 / 1e9
+    achieved = calls / k1_s / 1e9
+    return {"bound": "valu", "achieved": round(achieved, 1), "peak": round(peak, 1),
+            "unit": "GPhilox/s", "frac": round(achieved / peak, 4),
+            "calls_per_launch": int(calls)}
+
+
 def load_traffic(n: int):
     """HBM bytes per K1 launch from the committed PMC pass (profiles/), if one matches n."""
     path = os.path.join(ROOT, "profiles", "pmc_k1.json")
@@ -209,8 +226,9 @@ def main() -> None:
                 "launch_avg_us": round(k1_s * 1e6, 2),
                 "note": "achieved charges 8 B per element (SURVEY.md 8(d)); K1 reads no key "
                         "(draws depend only on the index), so it is bound by Philox integer "
-                        "VALU work, not HBM -- see DESIGN.md Roofline",
+                        "VALU work, not HBM -- see the valu_roofline object and DESIGN.md",
             },
+            "valu_roofline": valu_roofline(n, k1_s),
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(k, n, args.seed)
