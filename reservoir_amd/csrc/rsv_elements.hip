@@ -96,7 +96,10 @@ __global__ __launch_bounds__(kBlock) void export_draws_kernel(DrawKey dk, uint64
     out[t] = exact_j(dk, i, level0_byte(w, (uint32_t)(i & 15)));
 }
 
-// K2: one wave per stream; the wave's k-entry last-writer table lives in LDS.
+// K2: one wave per stream; the wave's k-entry last-writer table and candidate queue live in LDS.
+// A wave touches only its own LDS region, and LDS operations of one wave execute in order, so the
+// waves of a workgroup never synchronise with each other (no __syncthreads); each wave walks its
+// own sequence of streams and prefetches the next stream's offsets.
 template <typename KeyT>
 __global__ __launch_bounds__(kBlock) void k2_segmented(const KeyT* __restrict__ keys,
                                                        const int64_t* __restrict__ offsets, int64_t S,
@@ -110,44 +113,51 @@ __global__ __launch_bounds__(kBlock) void k2_segmented(const KeyT* __restrict__ 
     unsigned long long* tab = lds_tab + (size_t)wave * (k + kQueue);
     uint64_t* q = (uint64_t*)(tab + k);
     const uint64_t dense_lim = 256ull * k;
-    for (int64_t sb = (int64_t)blockIdx.x * wpb; sb < S; sb += (int64_t)gridDim.x * wpb) {
-        const int64_t s = sb + wave;
-        const bool active = s < S;
+    const int64_t wave_stride = (int64_t)gridDim.x * wpb;
+    int64_t s = (int64_t)blockIdx.x * wpb + wave;
+    int64_t off = 0, end = 0;
+    if (s < S) {
+        off = offsets[s];
+        end = offsets[s + 1];
+    }
+    for (; s < S; s += wave_stride) {
+        const int64_t len = end - off;
+        const int64_t s_next = s + wave_stride;
+        int64_t off_next = 0, end_next = 0;
+        if (s_next < S) {  // prefetch: the loads are in flight during this stream's work
+            off_next = offsets[s_next];
+            end_next = offsets[s_next + 1];
+        }
         for (uint32_t j = lane; j < k; j += 64) tab[j] = 0;
-        __syncthreads();
-        int64_t off = 0, len = 0;
-        if (active) {
-            off = offsets[s];
-            len = offsets[s + 1] - off;
-            const uint64_t stream = stream_base + (uint64_t)s;
-            const DrawKey dk{k0, k1, (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)stream),
-                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(stream >> 32))};
-            const uint64_t n_groups = ((uint64_t)len + 15) >> 4;
-            auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&tab[j], (unsigned long long)i); };
-            uint32_t qn = 0;
-            for (uint64_t gb = k >> 4; gb < n_groups; gb += 64) {
-                const uint64_t g = gb + lane;
-                const uint64_t i0 = g << 4;
-                const u32x4 w = level0(dk, g);
-                uint32_t mask = 0;
-                if (g < n_groups) {
-                    mask = candidate_mask16(w, i0, dense_lim);
-                    if (mask) mask &= clip_mask16(i0, k, (uint64_t)len);
-                }
-                enqueue_block(dk, w, i0, mask, q, qn, lane, k, hit);
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t stream = stream_base + (uint64_t)s;
+        const DrawKey dk{k0, k1, (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)stream),
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(stream >> 32))};
+        const uint64_t n_groups = ((uint64_t)len + 15) >> 4;
+        auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&tab[j], (unsigned long long)i); };
+        uint32_t qn = 0;
+        for (uint64_t gb = k >> 4; gb < n_groups; gb += 64) {
+            const uint64_t g = gb + lane;
+            const uint64_t i0 = g << 4;
+            const u32x4 w = level0(dk, g);
+            uint32_t mask = 0;
+            if (g < n_groups) {
+                mask = candidate_mask16(w, i0, dense_lim);
+                if (mask) mask &= clip_mask16(i0, k, (uint64_t)len);
             }
-            drain_queue(dk, q, qn, lane, k, hit);
+            enqueue_block(dk, w, i0, mask, q, qn, lane, k, hit);
         }
-        __syncthreads();
-        if (active) {
-            KeyT* o = out + s * (int64_t)k;
-            for (uint32_t j = lane; j < k; j += 64) {
-                const unsigned long long wi = tab[j];
-                o[j] = wi ? keys[off + (int64_t)wi] : ((int64_t)j < len ? keys[off + j] : (KeyT)0);
-            }
-            if (lane == 0) counts[s] = len < (int64_t)k ? len : (int64_t)k;
+        drain_queue(dk, q, qn, lane, k, hit);
+        __builtin_amdgcn_wave_barrier();
+        KeyT* o = out + s * (int64_t)k;
+        for (uint32_t j = lane; j < k; j += 64) {
+            const unsigned long long wi = tab[j];
+            o[j] = wi ? keys[off + (int64_t)wi] : ((int64_t)j < len ? keys[off + j] : (KeyT)0);
         }
-        __syncthreads();
+        if (lane == 0) counts[s] = len < (int64_t)k ? len : (int64_t)k;
+        __builtin_amdgcn_wave_barrier();
+        off = off_next;
+        end = end_next;
     }
 }
 
