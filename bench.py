@@ -1,8 +1,8 @@
 """Headline benchmark: C2 = one stream of 1e9 int64 keys per GPU, k = 1024, Algorithm R (philox_r).
 
-A step is one full pass of the hot path over the batch: a fresh Sampler (Sampler.apply) samples
-the device-resident keys (K1 last-writer kernel + resolve), then result() brings the k-slot
-reservoir to the host.  With N GPUs the stream is N x 1e9 elements split by index range (each
+A step is one full pass of the hot path over the batch: a fresh Sampler (Sampler.apply, created
+and closed inside the step) samples the device-resident keys (K1 last-writer kernel + resolve),
+then result() brings the k-slot reservoir to the host.  With N GPUs the stream is N x 1e9 elements split by index range (each
 rank seeks to its offset, weak scaling) and the per-rank reservoirs are combined with one RCCL
 all_gather + merge kernel inside the step.
 
@@ -141,36 +141,40 @@ def main() -> None:
     offset = rank * n
     keys = torch.empty(n, dtype=torch.int64, device=dev)
     splitmix_fill(keys, 0x5EED0000 + offset)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def make():
-        s = Sampler(k, seed=args.seed, stream_id=args.stream_id, device=local)()
-        s.set_stream(stream.cuda_stream)
-        return s
-
-    samplers = [make() for _ in range(args.warmup + args.steps)]
     L = _native.load()
-    for s in samplers[args.warmup:]:
-        N_ok = L.rsv_profile_enable(s.handle, 1)
-        _native.check(N_ok)
+    prof = [0.0, 0]  # K1 milliseconds, launches (timed steps)
 
-    def step(s):
+    def step(timed: bool):
+        # a fresh Sampler per step (Sampler.apply): creation and close are inside the step
+        s = Sampler(k, seed=args.seed, stream_id=args.stream_id, device=local)()
+        s.set_stream(stream)
+        if timed:
+            _native.check(L.rsv_profile_enable(s.handle, 1))
         s.seek(offset)
         s.sample_all(keys)
         if world > 1:
             D.combine(s, device=dev, total_count=n * world)
-        return s.result()
+        r = s.result()
+        if timed:  # HIP events already complete (result() waited for the stream)
+            ms, cnt = C.c_double(), C.c_int64()
+            _native.check(L.rsv_profile_read(s.handle, C.byref(ms), C.byref(cnt)))
+            prof[0] += ms.value
+            prof[1] += cnt.value
+        s.close()
+        return r
 
-    for s in samplers[: args.warmup]:
-        step(s)
+    for _ in range(args.warmup):
+        step(False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = None
-    for s in samplers[args.warmup:]:
-        res = step(s)
+    for _ in range(args.steps):
+        res = step(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -182,13 +186,7 @@ def main() -> None:
         elapsed = float(t.item())
 
     # K1 launch time (HIP events on the launch stream), averaged over the timed steps
-    tot_ms, launches = 0.0, 0
-    for s in samplers[args.warmup:]:
-        ms, cnt = C.c_double(), C.c_int64()
-        _native.check(L.rsv_profile_read(s.handle, C.byref(ms), C.byref(cnt)))
-        tot_ms += ms.value
-        launches += cnt.value
-    k1_s = tot_ms / max(launches, 1) / 1e3
+    k1_s = prof[0] / max(prof[1], 1) / 1e3
     assert res is not None and res.size == k
 
     if rank == 0:
@@ -209,8 +207,8 @@ def main() -> None:
             "data": "synthetic",
             "config": {
                 "workload": "C2: single stream, 1e9 int64 keys per GPU (splitmix64), k=1024, "
-                            "Algorithm R last-writer (engine philox_r); step = fresh Sampler, "
-                            "sampleAll over device-resident keys, result() to host",
+                            "Algorithm R last-writer (engine philox_r); step = create Sampler, "
+                            "sampleAll over device-resident keys, result() to host, close",
                 "keys_per_gpu": n, "k": k, "stream_elements": n * world,
                 "parallelism": f"index-range split over {world} GPU(s), RCCL all_gather combine"
                                if world > 1 else "single GPU",
@@ -233,8 +231,6 @@ def main() -> None:
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(k, n, args.seed)
         print(json.dumps(line), flush=True)
-    for s in samplers:
-        s.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -277,17 +277,16 @@ static hipError_t temp_bytes_for(int64_t cap, size_t* bytes) {
 // elements (k may be up to Int.MaxValue - 2, Sampler.scala:71) allocates for what it holds.
 static hipError_t grow(void** p, size_t old_bytes, size_t new_bytes, bool keep, hipStream_t st) {
     void* q = nullptr;
-    hipError_t e = hipMalloc(&q, new_bytes ? new_bytes : 16);
+    hipError_t e = pool_device_alloc(&q, new_bytes ? new_bytes : 16);
     if (e != hipSuccess) return e;
-    if (keep && *p && old_bytes) {
-        e = hipMemcpyAsync(q, *p, old_bytes, hipMemcpyDeviceToDevice, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) {
-            (void)hipFree(q);
-            return e;
-        }
+    if (keep && *p && old_bytes) e = hipMemcpyAsync(q, *p, old_bytes, hipMemcpyDeviceToDevice, st);
+    // queued work may still read the old block: wait before it goes back to the pool
+    if (e == hipSuccess && *p) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        pool_device_free(q);
+        return e;
     }
-    if (*p) (void)hipFree(*p);
+    pool_device_free(*p);
     *p = q;
     return hipSuccess;
 }
@@ -346,7 +345,7 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
     d->cand_limit = 4 * (int64_t)k + 4096;
     hipError_t e = hipSuccess;
     auto A = [&](void** p, size_t bytes) {
-        if (e == hipSuccess) e = hipMalloc(p, bytes ? bytes : 16);
+        if (e == hipSuccess) e = pool_device_alloc(p, bytes ? bytes : 16);
     };
     A((void**)&d->counter, 16);
     A((void**)&d->d_count, 16);
@@ -357,7 +356,7 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
         d->temp_bytes = tb;
     }
     A(&d->temp, d->temp_bytes);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&d->h_pinned, 64, hipHostMallocDefault);
+    if (e == hipSuccess) e = pool_host_alloc((void**)&d->h_pinned, 64, hipHostMallocDefault);
     // Typical k: allocate the whole working set now (nothing is allocated on the sampling path).
     // Huge k (up to Int.MaxValue - 2): grow with what the sampler holds.
     const int64_t full_merge = (int64_t)k + d->cand_limit;
@@ -377,9 +376,8 @@ void distinct_destroy(DistinctState* d) {
     if (!d) return;
     void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->counter, d->mh0, d->mh1, d->mk0,
                   d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp};
-    for (void* p : ps)
-        if (p) (void)hipFree(p);
-    if (d->h_pinned) (void)hipHostFree(d->h_pinned);
+    for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
+    pool_host_free(d->h_pinned);
     delete d;
 }
 

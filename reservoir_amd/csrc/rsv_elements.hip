@@ -30,30 +30,9 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
                                                          uint64_t hi, uint64_t g_begin,
                                                          uint64_t n_groups,
                                                          unsigned long long* __restrict__ win) {
-    __shared__ uint32_t qs[kBlock / 64][kBlockQueue];
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t* q = qs[threadIdx.x >> 6];
-    uint32_t qn = 0;
-    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
-    const uint64_t dense_lim = 256ull * k;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * kK1Unroll;
-    for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * kK1Unroll;
-         base < n_groups; base += stride) {
-        u32x4 w[kK1Unroll];
-        uint32_t off[kK1Unroll];
-#pragma unroll
-        for (int u = 0; u < kK1Unroll; ++u) {
-            off[u] = (uint32_t)(base + u * 64 + lane);  // n_groups < 2^32 per launch (host splits)
-            w[u] = level0(dk, g_begin + off[u]);
-        }
-        bool has[kK1Unroll];
-#pragma unroll
-        for (int u = 0; u < kK1Unroll; ++u)  // dense region (index < 256k): any block may hit
-            has[u] = (off[u] < n_groups) &  // bitwise: no short-circuit branches
-                     (((((g_begin + off[u]) << 4) + 1) < dense_lim) | any_zero_byte(w[u]));
-        push_blocks<kK1Unroll>(has, off, q, qn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
-    }
-    drain_blocks(q, qn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
+    __shared__ uint32_t qs[kBlock / 64][63 + 64 * kK1Unroll + 1];
+    __shared__ uint64_t cqs[kBlock / 64][kQueue];
+    k1_body<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
 }
 
 template <typename KeyT>
@@ -221,6 +200,46 @@ hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t
     else
         hipLaunchKernelGGL(resolve_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, st,
                            (const int32_t*)keys, base, n, k, batch_win, (int32_t*)slot_key, slot_idx);
+    return hipGetLastError();
+}
+
+// fresh handle: batch_win = 0, slot_idx = -1 (empty), slot_key = 0
+__global__ __launch_bounds__(kBlock) void init_slots_kernel(uint8_t* slot_key, int key_width, int64_t* slot_idx,
+                                                            unsigned long long* win, uint32_t k) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += stride) {
+        win[j] = 0;
+        slot_idx[j] = -1;
+        if (key_width == 8)
+            ((int64_t*)slot_key)[j] = 0;
+        else
+            ((int32_t*)slot_key)[j] = 0;
+    }
+}
+
+hipError_t launch_init_slots(void* slot_key, int key_width, int64_t* slot_idx, unsigned long long* win, uint32_t k,
+                             hipStream_t st) {
+    const unsigned grid = (unsigned)std::min<uint64_t>((k + kBlock - 1) / kBlock, 256 * 64);
+    hipLaunchKernelGGL(init_slots_kernel, dim3(grid), dim3(kBlock), 0, st, (uint8_t*)slot_key, key_width, slot_idx,
+                       win, k);
+    return hipGetLastError();
+}
+
+// result() tail: copy the k-slot reservoir straight into coherent pinned host memory, then publish
+// `gen` in the host flag with a system-scope release.  The host spins on the flag: ~7 us less
+// than hipMemcpyAsync D2H + hipStreamSynchronize for an 8 KB reservoir (tools/probe_latency.hip).
+__global__ __launch_bounds__(1024) void publish_kernel(const uint32_t* __restrict__ src, uint32_t* dst,
+                                                      int64_t words, uint32_t* flag, uint32_t gen) {
+    for (int64_t i = threadIdx.x; i < words; i += blockDim.x) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_publish(const void* src, int64_t bytes, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)src, (uint32_t*)dst_host_dev,
+                       bytes / 4, flag_dev, gen);
     return hipGetLastError();
 }
 

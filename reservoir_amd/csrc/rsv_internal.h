@@ -21,9 +21,23 @@ void set_error(const std::string& msg);
         }                                                                                     \
     } while (0)
 
+// ---- resource pool (rsv_pool.hip): device / pinned host buffers, streams, events ------------
+// Allocation is on the current device.  A buffer may only be released once no queued work can
+// touch it (synchronize its stream first).
+hipError_t pool_device_alloc(void** p, size_t bytes);
+void pool_device_free(void* p);
+hipError_t pool_host_alloc(void** p, size_t bytes, unsigned flags);
+void pool_host_free(void* p);
+void pool_trim();  // free every idle cached buffer
+hipError_t pool_stream(hipStream_t* out);  // non-blocking stream of the current device
+void pool_release_stream(int device, hipStream_t st);
+hipError_t pool_event(hipEvent_t* out, unsigned flags);
+void pool_release_event(int device, hipEvent_t e, unsigned flags);
+
 // HIP-event timing of a handle's hot kernel (rsv_profile_enable / rsv_profile_read)
 struct KernelTimer {
     bool on = false;
+    int device = 0;
     std::vector<hipEvent_t> ev;  // start/stop pairs, recycled after each drain
     size_t used = 0;
     double total_ms = 0;
@@ -32,7 +46,7 @@ struct KernelTimer {
         if (!on) return;
         if (used == ev.size()) {
             hipEvent_t e;
-            if (hipEventCreate(&e) != hipSuccess) return;
+            if (pool_event(&e, hipEventDefault) != hipSuccess) return;
             ev.push_back(e);
         }
         (void)hipEventRecord(ev[used++], st);
@@ -51,7 +65,7 @@ struct KernelTimer {
         return hipSuccess;
     }
     ~KernelTimer() {
-        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ev) pool_release_event(device, e, hipEventDefault);
     }
 };
 
@@ -67,6 +81,10 @@ hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, 
                                  unsigned long long* batch_win, hipStream_t st);
 // Resolve: fill phase for slots in [base, base+n) and winners of batch_win; resets batch_win.
 // slot_idx may be null.
+hipError_t launch_init_slots(void* slot_key, int key_width, int64_t* slot_idx, unsigned long long* win, uint32_t k,
+                             hipStream_t st);
+hipError_t launch_publish(const void* src, int64_t bytes, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen,
+                          hipStream_t st);
 hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,
                           unsigned long long* batch_win, void* slot_key, int64_t* slot_idx,
                           hipStream_t st);

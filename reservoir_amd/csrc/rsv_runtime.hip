@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -106,6 +107,8 @@ struct rsv_sampler {
     int kw = 8;
     uint32_t k = 0;
     // ELEMENTS
+    void* slots = nullptr;  // one pooled block: batch_win[k] | slot_idx[k] | slot_key[k]
+    bool slots_ready = false;  // initialised by init_slots_kernel on first use (stream-ordered)
     void* slot_key = nullptr;
     int64_t* slot_idx = nullptr;
     unsigned long long* batch_win = nullptr;
@@ -132,6 +135,13 @@ struct rsv_sampler {
     int64_t* chunk_hash_d = nullptr;
     int64_t chunk_cap = 0;
     void* result_h = nullptr;  // pinned staging for result() (k keys)
+    // small reservoirs: result_h is coherent + mapped and publish_kernel writes it directly,
+    // followed by result_gen in result_flag (same allocation); the host spins on the flag
+    bool result_publish = false;
+    void* result_dev = nullptr;  // device alias of result_h
+    uint32_t* result_flag = nullptr;
+    uint32_t* result_flag_dev = nullptr;
+    uint32_t result_gen = 0;
     KernelTimer timer;
 };
 
@@ -167,20 +177,31 @@ rsv_status check_open(const rsv_sampler* s) {  // SingleUse.checkOpen, Sampler.s
 rsv_status ensure_events(rsv_sampler* s, int64_t n) {
     if (n <= s->ev_cap) return RSV_OK;
     int64_t cap = std::max<int64_t>(n, 2 * s->ev_cap);
-    if (s->ev_pos_d) (void)hipFree(s->ev_pos_d);
-    if (s->ev_slot_d) (void)hipFree(s->ev_slot_d);
+    if (s->ev_pos_d || s->ev_slot_d) RSV_HIP_TRY(hipStreamSynchronize(s->stream));  // before reuse elsewhere
+    pool_device_free(s->ev_pos_d);
+    pool_device_free(s->ev_slot_d);
     s->ev_pos_d = nullptr;
     s->ev_slot_d = nullptr;
     s->ev_cap = 0;
-    RSV_HIP_TRY(hipMalloc((void**)&s->ev_pos_d, cap * 8));
-    RSV_HIP_TRY(hipMalloc((void**)&s->ev_slot_d, cap * 4));
+    RSV_HIP_TRY(pool_device_alloc((void**)&s->ev_pos_d, cap * 8));
+    RSV_HIP_TRY(pool_device_alloc((void**)&s->ev_slot_d, cap * 4));
     s->ev_cap = cap;
+    return RSV_OK;
+}
+
+// slot arrays of a fresh handle: slot_key = 0, slot_idx = -1 (empty), batch_win = 0, on the
+// handle's current stream before its first use (creation itself enqueues no device work)
+rsv_status ensure_slots(rsv_sampler* s) {
+    if (s->slots_ready || s->cfg.kind != RSV_KIND_ELEMENTS) return RSV_OK;
+    RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream));
+    s->slots_ready = true;
     return RSV_OK;
 }
 
 // one batch of n keys already in device memory, at global indices [count, count+n)
 rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t* hashes, int64_t n) {
     if (n <= 0) return RSV_OK;
+    if (rsv_status st = ensure_slots(s)) return st;
     const int64_t base = s->count;
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
         int rc = distinct_sample_device(s->distinct, keys, hashes, n, s->stream);
@@ -214,9 +235,9 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
 
 rsv_status ensure_chunk(rsv_sampler* s) {
     if (s->chunk_d) return RSV_OK;
-    RSV_HIP_TRY(hipMalloc(&s->chunk_d, kChunkKeys * s->kw));
+    RSV_HIP_TRY(pool_device_alloc(&s->chunk_d, kChunkKeys * s->kw));
     if (s->cfg.kind == RSV_KIND_DISTINCT && s->hash_kind == kHashPrecomputed)
-        RSV_HIP_TRY(hipMalloc((void**)&s->chunk_hash_d, kChunkKeys * 8));
+        RSV_HIP_TRY(pool_device_alloc((void**)&s->chunk_hash_d, kChunkKeys * 8));
     s->chunk_cap = kChunkKeys;
     return RSV_OK;
 }
@@ -255,18 +276,17 @@ rsv_status flush_stage(rsv_sampler* s) {
 }
 
 void free_all(rsv_sampler* s) {
-    void* ds[] = {s->slot_key, s->slot_idx, s->batch_win, s->ev_pos_d, s->ev_slot_d, s->chunk_d,
-                  s->chunk_hash_d};
-    for (void* p : ds)
-        if (p) (void)hipFree(p);
+    // callers have synchronized the stream: nothing queued touches these any more
+    void* ds[] = {s->slots, s->ev_pos_d, s->ev_slot_d, s->chunk_d, s->chunk_hash_d};
+    for (void* p : ds) pool_device_free(p);
     for (int b = 0; b < 2; ++b) {
-        if (s->stage_h[b]) (void)hipHostFree(s->stage_h[b]);
-        if (s->stage_hash_h[b]) (void)hipHostFree(s->stage_hash_h[b]);
-        if (s->stage_free[b]) (void)hipEventDestroy(s->stage_free[b]);
+        pool_host_free(s->stage_h[b]);
+        pool_host_free(s->stage_hash_h[b]);
+        pool_release_event(s->device, s->stage_free[b], hipEventDisableTiming);
     }
-    if (s->result_h) (void)hipHostFree(s->result_h);
+    pool_host_free(s->result_h);
     if (s->distinct) distinct_destroy(s->distinct);
-    if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
+    if (s->stream && s->own_stream) pool_release_stream(s->device, s->stream);
 }
 
 int resolve_hash_kind(int32_t hk, int kw) {
@@ -343,18 +363,18 @@ rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out) {
         delete s;
         return fail(st, msg);
     };
-    hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    s->timer.device = dev;
+    hipError_t e = pool_stream(&s->stream);
     if (e != hipSuccess) return bail(RSV_E_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
     s->own_stream = true;
     if (cfg->kind == RSV_KIND_ELEMENTS) {
         const size_t k = s->k;
-        e = hipMalloc(&s->slot_key, k * s->kw);
-        if (e == hipSuccess) e = hipMalloc((void**)&s->slot_idx, k * 8);
-        if (e == hipSuccess) e = hipMalloc((void**)&s->batch_win, k * 8);
-        if (e == hipSuccess) e = hipMemsetAsync(s->slot_key, 0, k * s->kw, s->stream);
-        if (e == hipSuccess) e = hipMemsetAsync(s->slot_idx, 0xFF, k * 8, s->stream);  // -1 = empty
-        if (e == hipSuccess) e = hipMemsetAsync(s->batch_win, 0, k * 8, s->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+        e = pool_device_alloc(&s->slots, k * 16 + ((k * s->kw + 7) & ~(size_t)7));
+        if (e == hipSuccess) {
+            s->batch_win = (unsigned long long*)s->slots;
+            s->slot_idx = (int64_t*)((uint8_t*)s->slots + k * 8);
+            s->slot_key = (uint8_t*)s->slots + k * 16;
+        }
         if (e != hipSuccess)
             return bail(e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE,
                         std::string("allocating reservoir: ") + hipGetErrorString(e));
@@ -393,9 +413,9 @@ static rsv_status stage_slow(rsv_sampler* s, bool pre) {
     }
     if (!s->stage_h[0]) {
         for (int b = 0; b < 2; ++b) {
-            RSV_HIP_TRY(hipHostMalloc((void**)&s->stage_h[b], kStageKeys * s->kw, hipHostMallocDefault));
-            if (pre) RSV_HIP_TRY(hipHostMalloc((void**)&s->stage_hash_h[b], kStageKeys * 8, hipHostMallocDefault));
-            RSV_HIP_TRY(hipEventCreateWithFlags(&s->stage_free[b], hipEventDisableTiming));
+            RSV_HIP_TRY(pool_host_alloc((void**)&s->stage_h[b], kStageKeys * s->kw, hipHostMallocDefault));
+            if (pre) RSV_HIP_TRY(pool_host_alloc((void**)&s->stage_hash_h[b], kStageKeys * 8, hipHostMallocDefault));
+            RSV_HIP_TRY(pool_event(&s->stage_free[b], hipEventDisableTiming));
         }
         s->stage_cap = kStageKeys;
     }
@@ -438,6 +458,42 @@ rsv_status rsv_sample_batch(rsv_sampler* s, const void* keys, int64_t n, int32_t
     return fail(RSV_E_ILLEGAL_ARGUMENT, "mem must be RSV_MEM_HOST or RSV_MEM_DEVICE");
 }
 
+static constexpr int64_t kPublishMaxBytes = 1 << 20;
+
+static rsv_status ensure_result_buffer(rsv_sampler* s) {
+    if (s->result_h) return RSV_OK;
+    const size_t bytes = (size_t)s->k * s->kw;
+    if ((int64_t)bytes <= kPublishMaxBytes) {
+        const size_t flag_off = (bytes + 63) & ~(size_t)63;
+        RSV_HIP_TRY(pool_host_alloc(&s->result_h, flag_off + 64, hipHostMallocCoherent | hipHostMallocMapped));
+        void* dev = nullptr;
+        RSV_HIP_TRY(hipHostGetDevicePointer(&dev, s->result_h, 0));
+        s->result_dev = dev;
+        s->result_flag = (uint32_t*)((uint8_t*)s->result_h + flag_off);
+        s->result_flag_dev = (uint32_t*)((uint8_t*)dev + flag_off);
+        *s->result_flag = s->result_gen;
+        s->result_publish = true;
+    } else {
+        RSV_HIP_TRY(pool_host_alloc(&s->result_h, bytes, hipHostMallocDefault));
+    }
+    return RSV_OK;
+}
+
+// Wait until publish_kernel has stored `gen` (acquire).  Spins for up to ~2 ms -- the K1 pass of a
+// 1e9-element batch still in flight ahead of it is ~0.13 ms -- then falls back to a blocking stream
+// synchronize, which also reports a failed kernel instead of waiting forever.
+static rsv_status wait_flag(rsv_sampler* s, uint32_t gen) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(s->result_flag, __ATOMIC_ACQUIRE) == gen) return RSV_OK;
+        __builtin_ia32_pause();
+        if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+    }
+    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    if (__atomic_load_n(s->result_flag, __ATOMIC_ACQUIRE) == gen) return RSV_OK;
+    return fail(RSV_E_DEVICE, "result publish flag not set after stream synchronize");
+}
+
 static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* out_n, bool device_out) {
     if (rsv_status st = check_open(s)) return st;
     if (!out_n) return fail(RSV_E_NULL_POINTER, "out_n is NULL");
@@ -473,8 +529,18 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
         src = s->slot_key;
         if (m && device_out) {
             RSV_HIP_TRY(hipMemcpyAsync(out, src, m * s->kw, hipMemcpyDeviceToDevice, s->stream));
-        } else if (m) {  // through a pinned buffer: a pageable D2H costs a staged copy
-            if (!s->result_h) RSV_HIP_TRY(hipHostMalloc(&s->result_h, (size_t)s->k * s->kw, hipHostMallocDefault));
+        } else if (m) {
+            if (rsv_status st = ensure_result_buffer(s)) return st;
+            if (s->result_publish) {  // publish kernel + flag spin (no D2H copy, no stream sync)
+                const uint32_t gen = ++s->result_gen;
+                RSV_HIP_TRY(launch_publish(src, m * s->kw, s->result_dev, s->result_flag_dev, gen, s->stream));
+                if (rsv_status st = wait_flag(s, gen)) return st;
+                memcpy(out, s->result_h, (size_t)m * s->kw);
+                *out_n = m;
+                if (!s->cfg.reusable) s->open = false;
+                return RSV_OK;
+            }
+            // large reservoirs through a pinned buffer: a pageable D2H costs a staged copy
             RSV_HIP_TRY(hipMemcpyAsync(s->result_h, src, m * s->kw, hipMemcpyDeviceToHost, s->stream));
         }
     }
@@ -501,7 +567,7 @@ rsv_status rsv_set_stream(rsv_sampler* s, void* hip_stream) {
     if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
     DeviceGuard g(s->device);
     RSV_HIP_TRY(hipStreamSynchronize(s->stream));
-    if (s->own_stream) (void)hipStreamDestroy(s->stream);
+    if (s->own_stream) pool_release_stream(s->device, s->stream);
     s->stream = (hipStream_t)hip_stream;
     s->own_stream = false;
     return RSV_OK;
@@ -535,8 +601,10 @@ rsv_status rsv_seek(rsv_sampler* s, int64_t index) {
     if (rsv_status st = check_open(s)) return st;
     if (s->cfg.kind != RSV_KIND_ELEMENTS || s->cfg.engine != RSV_ENGINE_PHILOX_R)
         return fail(RSV_E_UNSUPPORTED, "rsv_seek needs an ELEMENTS sampler on RSV_ENGINE_PHILOX_R");
-    DeviceGuard g(s->device);
-    if (rsv_status st = flush_stage(s)) return st;
+    if (s->stage_n) {  // only staged per-element samples need the device here
+        DeviceGuard g(s->device);
+        if (rsv_status st = flush_stage(s)) return st;
+    }
     if (index < s->count) return fail(RSV_E_ILLEGAL_ARGUMENT, "rsv_seek cannot move backwards");
     s->count = index;
     return RSV_OK;
@@ -552,6 +620,7 @@ rsv_status rsv_export_state(rsv_sampler* s, int64_t* idx_dev, void* keys_dev, in
         if (int rc = distinct_export(s->distinct, keys_dev, hash_dev, s->stream)) return (rsv_status)rc;
         *out_n = distinct_size(s->distinct);
     } else {
+        if (rsv_status st = ensure_slots(s)) return st;
         if (idx_dev) RSV_HIP_TRY(hipMemcpyAsync(idx_dev, s->slot_idx, s->k * 8ull, hipMemcpyDeviceToDevice, s->stream));
         if (keys_dev)
             RSV_HIP_TRY(hipMemcpyAsync(keys_dev, s->slot_key, (size_t)s->k * s->kw, hipMemcpyDeviceToDevice, s->stream));
@@ -581,6 +650,7 @@ rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* k
     } else {
         if (part_len < (int64_t)s->k) return fail(RSV_E_ILLEGAL_ARGUMENT, "part_len < k");
         if (parts > 0 && !idx_dev) return fail(RSV_E_NULL_POINTER, "idx_dev is NULL");
+        if (rsv_status st = ensure_slots(s)) return st;
         RSV_HIP_TRY(launch_merge_slots(idx_dev, keys_dev, s->kw, parts, part_len, s->k, s->slot_idx, s->slot_key,
                                        s->stream));
     }

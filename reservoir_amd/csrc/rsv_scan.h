@@ -111,28 +111,36 @@ __device__ __forceinline__ void drain_queue(const DrawKey& dk, const uint64_t* q
 // tests "any zero byte" and pushes a 32-bit block offset; at drain time the wave recomputes the
 // level-0 block (one Philox per 64 pushed blocks per lane), decodes it and runs the level-1 draws,
 // 64 blocks at once.  (Pushing the raw 24-B block instead cost 28 us per 1e9 indices.)
-constexpr uint32_t kBlockQueue = 192;  // 32-bit entries per wave (>= 63 + 64 U, U <= 2)
 
+// Resolve queued block g (valid lanes only; the call is wave-uniform): the block's FIRST candidate
+// is evaluated in place by every lane at once; further candidates of the same block (about 3 % of
+// sparse blocks -- but 86 % of 64-block drains hold one) go to the per-candidate queue `cq`, so a
+// lone second candidate does not cost the whole wave another level-1 Philox.
 template <class Hit>
-__device__ __forceinline__ void resolve_block(const DrawKey& dk, uint64_t g, uint64_t lo, uint64_t hi,
-                                              uint64_t dense_lim, uint32_t k, Hit& hit) {
+__device__ __forceinline__ void resolve_block(const DrawKey& dk, bool valid, uint64_t g, uint64_t lo,
+                                              uint64_t hi, uint64_t dense_lim, uint32_t k, uint64_t* cq,
+                                              uint32_t& cqn, uint32_t lane, Hit& hit) {
     const u32x4 w = level0(dk, g);
     const uint64_t i0 = g << 4;
-    uint32_t mask = candidate_mask16(w, i0, dense_lim) & clip_mask16(i0, lo, hi);
-    while (mask) {
+    uint32_t mask = valid ? candidate_mask16(w, i0, dense_lim) : 0u;
+    if (i0 < lo || i0 + 16 > hi) mask &= clip_mask16(i0, lo, hi);
+    if (mask) {
         const uint32_t e = __builtin_ctz(mask);
         mask &= mask - 1;
         const uint64_t j = exact_j(dk, i0 + e, level0_byte(w, e));
         if (j < k) hit((uint32_t)j, i0 + e);
     }
+    enqueue_block(dk, w, i0, mask, cq, cqn, lane, k, hit);
 }
 
 // Push the U blocks of one iteration (has[u]: block g_begin + off[u] holds a candidate) with one
-// wave-uniform branch; whenever 64 blocks wait, all lanes resolve one each.
+// wave-uniform branch; whenever 64 blocks wait, all lanes resolve one each.  The queue holds
+// < 64 waiting + 64 U pushed entries.
 template <int U, class Hit>
 __device__ __forceinline__ void push_blocks(const bool (&has)[U], const uint32_t (&off)[U], uint32_t* q,
-                                            uint32_t& qn, uint32_t lane, const DrawKey& dk, uint64_t g_begin,
-                                            uint64_t lo, uint64_t hi, uint64_t dense_lim, uint32_t k, Hit& hit) {
+                                            uint32_t& qn, uint64_t* cq, uint32_t& cqn, uint32_t lane,
+                                            const DrawKey& dk, uint64_t g_begin, uint64_t lo, uint64_t hi,
+                                            uint64_t dense_lim, uint32_t k, Hit& hit) {
     unsigned long long bal[U], any = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -149,17 +157,52 @@ __device__ __forceinline__ void push_blocks(const bool (&has)[U], const uint32_t
     while (qn >= 64) {
         qn -= 64;
         __builtin_amdgcn_wave_barrier();
-        resolve_block(dk, g_begin + q[qn + lane], lo, hi, dense_lim, k, hit);
+        resolve_block(dk, true, g_begin + q[qn + lane], lo, hi, dense_lim, k, cq, cqn, lane, hit);
         __builtin_amdgcn_wave_barrier();
     }
 }
 
 template <class Hit>
-__device__ __forceinline__ void drain_blocks(const uint32_t* q, uint32_t qn, uint32_t lane, const DrawKey& dk,
-                                             uint64_t g_begin, uint64_t lo, uint64_t hi, uint64_t dense_lim,
-                                             uint32_t k, Hit& hit) {
+__device__ __forceinline__ void drain_blocks(const uint32_t* q, uint32_t qn, uint64_t* cq, uint32_t& cqn,
+                                             uint32_t lane, const DrawKey& dk, uint64_t g_begin, uint64_t lo,
+                                             uint64_t hi, uint64_t dense_lim, uint32_t k, Hit& hit) {
     __builtin_amdgcn_wave_barrier();
-    if (lane < qn) resolve_block(dk, g_begin + q[lane], lo, hi, dense_lim, k, hit);
+    const bool valid = lane < qn;
+    resolve_block(dk, valid, g_begin + (valid ? q[lane] : 0u), lo, hi, dense_lim, k, cq, cqn, lane, hit);
+    drain_queue(dk, cq, cqn, lane, k, hit);
+}
+
+// K1 main loop: grid-stride over level-0 blocks (16 indices each), U blocks per lane per
+// iteration; wave-uniform so the queue can run full-wave level-1 evaluations.  Hits (k ln(n/k) of
+// them) go straight to global atomicMax on the k-slot winner table: ~14k atomics per 1e9 indices
+// at k = 1024.  `q` = this wave's block queue (>= 63 + 64 U entries), `cq` its candidate queue
+// (kQueue entries).
+template <int U>
+__device__ __forceinline__ void k1_body(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                        uint64_t n_groups, unsigned long long* __restrict__ win, uint32_t* q,
+                                        uint64_t* cq) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t qn = 0, cqn = 0;
+    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
+    const uint64_t dense_lim = 256ull * k;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * U;
+    for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U; base < n_groups;
+         base += stride) {
+        u32x4 w[U];
+        uint32_t off[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            off[u] = (uint32_t)(base + u * 64 + lane);  // n_groups < 2^32 per launch (host splits)
+            w[u] = level0(dk, g_begin + off[u]);
+        }
+        bool has[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)  // dense region (index < 256k): any block may hit
+            has[u] = (off[u] < n_groups) &  // bitwise: no short-circuit branches
+                     (((((g_begin + off[u]) << 4) + 1) < dense_lim) | any_zero_byte(w[u]));
+        push_blocks<U>(has, off, q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
+    }
+    drain_blocks(q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
 }
 
 }  // namespace rsv

@@ -65,6 +65,14 @@ def _is_torch_cuda(x) -> bool:
     return t.__module__.startswith("torch") and t.__name__ == "Tensor" and getattr(x, "is_cuda", False)
 
 
+def _current_raw_stream(torch, t) -> int:
+    """torch's current HIP stream on t's device as an integer handle (cheap form when available)."""
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if raw is not None:
+        return int(raw(t.device.index))
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
 class GpuSampler:
     """A ``Sampler[A, B]`` whose state lives on an MI355X (one opaque C-ABI handle)."""
 
@@ -163,10 +171,10 @@ class GpuSampler:
         if _is_torch_cuda(elements) and self._map is identity and not self._precomputed:
             import torch
 
-            t = elements.contiguous()
-            cur = torch.cuda.current_stream(t.device)
-            if cur.cuda_stream != self.stream:
-                cur.synchronize()  # the tensor was produced on torch's stream
+            t = elements if elements.is_contiguous() else elements.contiguous()
+            cur = _current_raw_stream(torch, t)
+            if cur != self._stream:
+                torch.cuda.current_stream(t.device).synchronize()  # produced on torch's stream
             if t.element_size() != self._width:
                 raise IllegalArgumentException("device tensor dtype does not match key_type")
             N.check(self._L.rsv_sample_batch(self._h, C.c_void_p(t.data_ptr()), t.numel(),
@@ -194,7 +202,7 @@ class GpuSampler:
         out = np.empty(self._k, dtype=self._dtype)
         n = C.c_int64(0)
         N.check(self._L.rsv_result(self._h, out.ctypes.data_as(C.c_void_p), self._k, C.byref(n)))
-        return out[: n.value].copy()
+        return out if n.value == self._k else out[: n.value].copy()
 
     def result_device(self, out_tensor) -> int:
         """Write the result into a device tensor (no host round trip); returns its length."""

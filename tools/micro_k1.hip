@@ -71,6 +71,14 @@ __global__ __launch_bounds__(256) void philox_only(DrawKey dk, uint64_t n_groups
     if (c == 0x12345u) atomicAdd(cnt, c);
 }
 
+template <int U>
+__global__ __launch_bounds__(256) void k1_var(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                              uint64_t n_groups, unsigned long long* win) {
+    __shared__ uint32_t qs[4][63 + 64 * U + 1];
+    __shared__ uint64_t cqs[4][kQueue];
+    k1_body<U>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
+}
+
 int main(int argc, char** argv) {
     uint32_t* d;
     CK(hipMalloc(&d, 64));
@@ -135,6 +143,11 @@ int main(int argc, char** argv) {
         printf("%-28s grid %6d unroll %d  %8.1f us per 1e9 indices\n", name, grid, unroll, ms / 5 * 1e3);
         return 0;
     };
+    for (int grid : {4096, 8192, 16384}) {
+        time_v(k1_var<1>, "k1 product body", grid / 1, 1);
+        time_v(k1_var<2>, "k1 product body", grid / 2, 2);
+        time_v(k1_var<4>, "k1 product body", grid / 4, 4);
+    }
 
     return 0;
 }

@@ -55,3 +55,35 @@ small = keys[:1_000_000]
 run("1e6 keys: sample_all + result", lambda s: (s.sample_all(small), s.result()))
 tiny = keys[:1000]
 run("1e3 keys: sample_all + result", lambda s: (s.sample_all(tiny), s.result()))
+
+
+def timed_loop(label, body, reps=50):
+    for _ in range(5):
+        body()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        body()
+    torch.cuda.synchronize()
+    print(f"{label:40s} {(time.perf_counter() - t0) / reps * 1e6:8.1f} us/step", flush=True)
+
+
+timed_loop("create(private stream) + close", lambda: Sampler(k, seed=1, stream_id=2)().close())
+timed_loop("create + set_stream + close", lambda: mk().close())
+rs = Sampler(k, seed=1, stream_id=2, reusable=True)()
+rs.set_stream(st.cuda_stream)
+timed_loop("reusable: 1e3 keys sample_all + result", lambda: (rs.sample_all(tiny), rs.result()))
+timed_loop("reusable: 1e9 keys sample_all + result", lambda: (rs.sample_all(keys), rs.result()))
+
+
+def full(x):
+    s = mk()
+    s.seek(0)
+    s.sample_all(x)
+    r = s.result()
+    s.close()
+    return r
+
+
+timed_loop("full step incl create/close, 1e3", lambda: full(tiny))
+timed_loop("full step incl create/close, 1e9", lambda: full(keys))
