@@ -35,23 +35,27 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
     k1_body<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
 }
 
+// Per slot j: the batch's last writer (win[j], then cleared), else the fill of j < k from this
+// batch, else -- first batch of a handle whose slots were never initialised (`fresh`) -- empty.
 template <typename KeyT>
 __global__ __launch_bounds__(kBlock) void resolve_kernel(const KeyT* __restrict__ keys, int64_t base,
                                                          int64_t n, uint32_t k,
                                                          unsigned long long* __restrict__ win,
                                                          KeyT* __restrict__ slot_key,
-                                                         int64_t* __restrict__ slot_idx) {
+                                                         int64_t* __restrict__ slot_idx, int fresh) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= k) return;
-    if ((int64_t)j >= base && (int64_t)j < base + n) {  // fill phase (Sampler.scala:253-255)
-        slot_key[j] = keys[j - base];
-        if (slot_idx) slot_idx[j] = j;
-    }
     const unsigned long long wi = win[j];
     if (wi) {  // last eviction into slot j in this batch (Sampler.scala:243-246)
         slot_key[j] = keys[(int64_t)wi - base];
         if (slot_idx) slot_idx[j] = (int64_t)wi;
         win[j] = 0;
+    } else if ((int64_t)j >= base && (int64_t)j < base + n) {  // fill phase (Sampler.scala:253-255)
+        slot_key[j] = keys[j - base];
+        if (slot_idx) slot_idx[j] = j;
+    } else if (fresh) {
+        slot_key[j] = 0;
+        if (slot_idx) slot_idx[j] = -1;
     }
 }
 
@@ -191,15 +195,15 @@ hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, 
 }
 
 hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,
-                          unsigned long long* batch_win, void* slot_key, int64_t* slot_idx,
+                          unsigned long long* batch_win, void* slot_key, int64_t* slot_idx, bool fresh,
                           hipStream_t st) {
     const unsigned grid = (unsigned)((k + kBlock - 1) / kBlock);
     if (key_width == 8)
         hipLaunchKernelGGL(resolve_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, st,
-                           (const int64_t*)keys, base, n, k, batch_win, (int64_t*)slot_key, slot_idx);
+                           (const int64_t*)keys, base, n, k, batch_win, (int64_t*)slot_key, slot_idx, (int)fresh);
     else
         hipLaunchKernelGGL(resolve_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, st,
-                           (const int32_t*)keys, base, n, k, batch_win, (int32_t*)slot_key, slot_idx);
+                           (const int32_t*)keys, base, n, k, batch_win, (int32_t*)slot_key, slot_idx, (int)fresh);
     return hipGetLastError();
 }
 

@@ -86,7 +86,7 @@ hipError_t launch_init_slots(void* slot_key, int key_width, int64_t* slot_idx, u
 hipError_t launch_publish(const void* src, int64_t bytes, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen,
                           hipStream_t st);
 hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,
-                          unsigned long long* batch_win, void* slot_key, int64_t* slot_idx,
+                          unsigned long long* batch_win, void* slot_key, int64_t* slot_idx, bool fresh,
                           hipStream_t st);
 // K1': events (1-based pos, slot) -> batch_win
 hipError_t launch_replay_events(const int64_t* ev_pos, const int32_t* ev_slot, int64_t n_events,

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -108,7 +109,10 @@ struct rsv_sampler {
     uint32_t k = 0;
     // ELEMENTS
     void* slots = nullptr;  // one pooled block: batch_win[k] | slot_idx[k] | slot_key[k]
-    bool slots_ready = false;  // initialised by init_slots_kernel on first use (stream-ordered)
+    // device-state knowledge, in stream order: batch_win all zero (resolve leaves it so) / slot
+    // arrays initialised.  Creation enqueues no device work; the first batch initialises.
+    bool win_zero = false;
+    bool slots_init = false;
     void* slot_key = nullptr;
     int64_t* slot_idx = nullptr;
     unsigned long long* batch_win = nullptr;
@@ -192,17 +196,61 @@ rsv_status ensure_events(rsv_sampler* s, int64_t n) {
 // slot arrays of a fresh handle: slot_key = 0, slot_idx = -1 (empty), batch_win = 0, on the
 // handle's current stream before its first use (creation itself enqueues no device work)
 rsv_status ensure_slots(rsv_sampler* s) {
-    if (s->slots_ready || s->cfg.kind != RSV_KIND_ELEMENTS) return RSV_OK;
+    if (s->slots_init || s->cfg.kind != RSV_KIND_ELEMENTS) return RSV_OK;
     RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream));
-    s->slots_ready = true;
+    s->slots_init = s->win_zero = true;
     return RSV_OK;
+}
+
+// Slot blocks whose batch_win is known zero (their last sampler ended on a resolve): a new handle
+// of the same (k, key width) takes one and skips the init kernel -- its first resolve marks the
+// untouched slots empty instead (resolve_kernel `fresh`).
+struct CleanSlots {
+    void* p;
+    uint32_t k;
+    int kw;
+    int device;
+};
+std::mutex g_clean_mu;
+std::vector<CleanSlots>& clean_slots() {
+    static auto* v = new std::vector<CleanSlots>();  // leaked on purpose, like the pool
+    return *v;
+}
+
+void* take_clean_slots(uint32_t k, int kw, int device) {
+    std::lock_guard<std::mutex> lk(g_clean_mu);
+    auto& v = clean_slots();
+    for (size_t i = v.size(); i-- > 0;)
+        if (v[i].k == k && v[i].kw == kw && v[i].device == device) {
+            void* p = v[i].p;
+            v.erase(v.begin() + (ptrdiff_t)i);
+            return p;
+        }
+    return nullptr;
+}
+
+bool give_clean_slots(void* p, uint32_t k, int kw, int device) {
+    if ((uint64_t)k * (16 + kw) > (64ull << 20)) return false;
+    std::lock_guard<std::mutex> lk(g_clean_mu);
+    auto& v = clean_slots();
+    if (v.size() >= 32) return false;
+    v.push_back(CleanSlots{p, k, kw, device});
+    return true;
 }
 
 // one batch of n keys already in device memory, at global indices [count, count+n)
 rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t* hashes, int64_t n) {
     if (n <= 0) return RSV_OK;
-    if (rsv_status st = ensure_slots(s)) return st;
     const int64_t base = s->count;
+    bool fresh = false;
+    if (s->cfg.kind == RSV_KIND_ELEMENTS) {
+        if (!s->win_zero) {  // never-used block: full init
+            RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream));
+            s->slots_init = s->win_zero = true;
+        }
+        fresh = !s->slots_init;
+        s->win_zero = false;  // until this batch's resolve is enqueued
+    }
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
         int rc = distinct_sample_device(s->distinct, keys, hashes, n, s->stream);
         if (rc != RSV_OK) return (rsv_status)rc;
@@ -219,7 +267,8 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
             RSV_HIP_TRY(launch_replay_events(s->ev_pos_d, s->ev_slot_d, ne, s->k, s->batch_win, s->stream));
             s->timer.mark(s->stream);
         }
-        RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, s->stream));
+        RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, fresh,
+                                   s->stream));
         if (ne) RSV_HIP_TRY(hipStreamSynchronize(s->stream));  // host event vectors are reused
     } else {
         const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
@@ -227,8 +276,10 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
         s->timer.mark(s->stream);
         RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
         s->timer.mark(s->stream);
-        RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, s->stream));
+        RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, fresh,
+                                   s->stream));
     }
+    if (s->cfg.kind == RSV_KIND_ELEMENTS) s->slots_init = s->win_zero = true;
     s->count = base + n;
     return RSV_OK;
 }
@@ -277,6 +328,7 @@ rsv_status flush_stage(rsv_sampler* s) {
 
 void free_all(rsv_sampler* s) {
     // callers have synchronized the stream: nothing queued touches these any more
+    if (s->slots && s->win_zero && give_clean_slots(s->slots, s->k, s->kw, s->device)) s->slots = nullptr;
     void* ds[] = {s->slots, s->ev_pos_d, s->ev_slot_d, s->chunk_d, s->chunk_hash_d};
     for (void* p : ds) pool_device_free(p);
     for (int b = 0; b < 2; ++b) {
@@ -369,7 +421,11 @@ rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out) {
     s->own_stream = true;
     if (cfg->kind == RSV_KIND_ELEMENTS) {
         const size_t k = s->k;
-        e = pool_device_alloc(&s->slots, k * 16 + ((k * s->kw + 7) & ~(size_t)7));
+        s->slots = take_clean_slots(s->k, s->kw, dev);
+        if (s->slots)
+            s->win_zero = true;
+        else
+            e = pool_device_alloc(&s->slots, k * 16 + ((k * s->kw + 7) & ~(size_t)7));
         if (e == hipSuccess) {
             s->batch_win = (unsigned long long*)s->slots;
             s->slot_idx = (int64_t*)((uint8_t*)s->slots + k * 8);
@@ -689,7 +745,7 @@ rsv_status rsv_replay_events(const void* keys_dev, int64_t n, int32_t key_width,
     RSV_HIP_TRY(hipMallocAsync((void**)&win, (size_t)k * 8, st));
     hipError_t e = hipMemsetAsync(win, 0, (size_t)k * 8, st);
     if (e == hipSuccess) e = launch_replay_events(ev_pos_dev, ev_slot_dev, n_events, (uint32_t)k, win, st);
-    if (e == hipSuccess) e = launch_resolve(keys_dev, key_width, base_index, n, (uint32_t)k, win, reservoir_dev, nullptr, st);
+    if (e == hipSuccess) e = launch_resolve(keys_dev, key_width, base_index, n, (uint32_t)k, win, reservoir_dev, nullptr, false, st);
     hipError_t e2 = hipFreeAsync(win, st);
     RSV_HIP_TRY(e);
     RSV_HIP_TRY(e2);

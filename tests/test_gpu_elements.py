@@ -254,3 +254,31 @@ def test_maximum_sample_size(cuda, oracle):
     s = Sampler(k, seed=1)()
     s.sample_all(keys)
     assert np.array_equal(s.result(), keys)  # n < k: every element, in order (resultImpl :318-331)
+
+
+@pytest.mark.parametrize("kt", ["long", "int"])
+def test_recycled_handle_resources(cuda, oracle, kt):
+    """Samplers created after others were closed reuse their pooled slot blocks (rsv_pool.hip and
+    the clean-slot cache): no state may leak from the previous owner -- partial fills, empty
+    slots in export_state, and full parity all hold for every generation."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    k = 300
+    dt = np.int64 if kt == "long" else np.int32
+    for gen in range(6):
+        n = [100_000, 50, 0, 299, 300, 7_777][gen]
+        keys = oracle.splitmix_keys(40_000 + gen, n).astype(dt)
+        want, _ = oracle.algo_r(1234 + gen, gen, k, keys.astype(np.int64))
+        s = Sampler(k, seed=1234 + gen, stream_id=gen, key_type=kt)()
+        if n:
+            s.sample_all(_dev_keys(torch, cuda, keys))
+        idx, kk, _, cnt = s.export_state(cuda)
+        m = min(n, k)
+        idx = idx.cpu().numpy()
+        assert (idx[m:] == -1).all() and (idx[:m] >= 0).all()
+        got = s.result()
+        assert got.size == m
+        assert np.array_equal(got, want[:m].astype(dt))
+        s.close()
