@@ -175,6 +175,9 @@ class GpuSampler:
             cur = _current_raw_stream(torch, t)
             if cur != self._stream:
                 torch.cuda.current_stream(t.device).synchronize()  # produced on torch's stream
+                # and torch must not hand the block to another tensor while this handle's stream
+                # still reads it (the caller may drop `elements` as soon as we return)
+                t.record_stream(torch.cuda.ExternalStream(self._stream, device=t.device))
             if t.element_size() != self._width:
                 raise IllegalArgumentException("device tensor dtype does not match key_type")
             N.check(self._L.rsv_sample_batch(self._h, C.c_void_p(t.data_ptr()), t.numel(),
