@@ -146,6 +146,16 @@ rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* k
                            const int64_t* hash_dev, const int64_t* part_n_host, int32_t parts,
                            int64_t part_len, int64_t total_count);
 
+/* Packed form of the two calls above for ELEMENTS samplers, the one-collective combine of
+ * reservoir_amd/distributed.py: row_dev[0..k) = global index per slot (-1 = empty),
+ * row_dev[k..2k) = the slot's key widened to int64 (sign-extended for 4-byte keys).  One kernel,
+ * no host wait on a caller stream. */
+rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev);
+/* Merge `parts` packed rows (row p at rows_dev + p*row_stride, row_stride >= 2k), e.g. the output
+ * of an all-gather of every rank's rsv_export_packed row: per slot the largest global index wins. */
+rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t parts, int64_t row_stride,
+                            int64_t total_count);
+
 /* ---- Stateless batch entry points --------------------------------------------------------- */
 /* Segmented sampling: S independent Algorithm-R samplers (no reference counterpart; = S separate
  * Sampler instances, S:196-332).  Stream s samples keys_dev[offsets[s] .. offsets[s+1]) with

@@ -26,7 +26,8 @@ EXPORTED_SYMBOLS = (
     "rsv_destroy", "rsv_sample", "rsv_sample_batch", "rsv_result", "rsv_result_device",
     "rsv_is_open", "rsv_count", "rsv_set_stream", "rsv_get_stream", "rsv_synchronize", "rsv_seek",
     "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
-    "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read",
+    "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
+    "rsv_merge_packed",
 )
 
 
@@ -101,6 +102,8 @@ def load():
     L.rsv_seek.argtypes = [vp, i64]
     L.rsv_export_state.argtypes = [vp, vp, vp, vp, C.POINTER(i64)]
     L.rsv_merge_state.argtypes = [vp, vp, vp, vp, vp, i32, i64, i64]
+    L.rsv_export_packed.argtypes = [vp, vp]
+    L.rsv_merge_packed.argtypes = [vp, vp, i32, i64, i64]
     L.rsv_sample_segmented.argtypes = [vp, vp, i64, i32, i32, u64, u64, vp, vp, vp]
     L.rsv_replay_events.argtypes = [vp, i64, i32, i64, vp, vp, i64, i32, vp, vp]
     L.rsv_export_draws.argtypes = [u64, u64, u64, i64, vp, vp]
@@ -109,7 +112,8 @@ def load():
     for name in ("rsv_config_init", "rsv_create", "rsv_sample", "rsv_sample_batch", "rsv_result",
                  "rsv_result_device", "rsv_set_stream", "rsv_synchronize", "rsv_seek",
                  "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
-                 "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read"):
+                 "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
+                 "rsv_merge_packed"):
         getattr(L, name).restype = i32
     if L.rsv_abi_version() != 1:
         raise ImportError("libreservoir_hip.so ABI version mismatch")

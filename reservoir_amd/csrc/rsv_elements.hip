@@ -9,6 +9,8 @@
 //
 // None of these kernels streams the key array: a draw depends only on (seed, stream, index), so
 // only the k winning keys are ever read (DESIGN.md "Roofline").
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 
 #include "rsv_device.h"
@@ -165,6 +167,38 @@ __global__ __launch_bounds__(kBlock) void merge_slots_kernel(const int64_t* __re
     slot_key[j] = key;
 }
 
+// packed multi-GPU row: [slot_idx(k) | keys widened to int64 (k)]
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void export_packed_kernel(const int64_t* __restrict__ slot_idx,
+                                                               const KeyT* __restrict__ slot_key, uint32_t k,
+                                                               int64_t* __restrict__ row) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    row[j] = slot_idx[j];
+    row[k + j] = (int64_t)slot_key[j];
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void merge_packed_kernel(const int64_t* __restrict__ rows, int32_t parts,
+                                                              int64_t stride, uint32_t k,
+                                                              int64_t* __restrict__ slot_idx,
+                                                              KeyT* __restrict__ slot_key) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    int64_t best = slot_idx[j];
+    KeyT key = slot_key[j];
+    for (int32_t p = 0; p < parts; ++p) {
+        const int64_t* r = rows + (int64_t)p * stride;
+        const int64_t idx = r[j];
+        if (idx > best) {
+            best = idx;
+            key = (KeyT)r[k + j];
+        }
+    }
+    slot_idx[j] = best;
+    slot_key[j] = key;
+}
+
 inline DrawKey make_key(const DrawParams& dp) {
     return DrawKey{(uint32_t)dp.seed, (uint32_t)(dp.seed >> 32), (uint32_t)dp.stream,
                    (uint32_t)(dp.stream >> 32)};
@@ -179,15 +213,22 @@ inline unsigned grid_for(uint64_t items, unsigned cap) {
 }  // namespace
 
 hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
-                                 unsigned long long* batch_win, hipStream_t st) {
-    if (hi <= lo) return hipSuccess;
+                                 unsigned long long* batch_win, hipStream_t st, hipEvent_t ev_start,
+                                 hipEvent_t ev_stop) {
+    if (hi <= lo) {  // nothing to draw: the timer pair still needs both events recorded
+        if (ev_start) (void)hipEventRecord(ev_start, st);
+        if (ev_stop) (void)hipEventRecord(ev_stop, st);
+        return hipSuccess;
+    }
     const uint64_t g_end = (hi + 15) >> 4;
     constexpr uint64_t kMaxGroups = 1ull << 31;  // block offsets are 32-bit queue entries
     for (uint64_t g_begin = lo >> 4; g_begin < g_end; g_begin += kMaxGroups) {
         const uint64_t n_groups = std::min<uint64_t>(g_end - g_begin, kMaxGroups);
         const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 32);
-        hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
-                           g_begin, n_groups, batch_win);
+        const bool first = g_begin == (lo >> 4), last = g_begin + n_groups >= g_end;
+        hipExtLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, first ? ev_start : nullptr,
+                              last ? ev_stop : nullptr, 0, make_key(dp), k, lo, hi, g_begin, n_groups,
+                              batch_win);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -302,6 +343,30 @@ hipError_t launch_merge_slots(const int64_t* idx_parts, const void* key_parts, i
     else
         hipLaunchKernelGGL(merge_slots_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, st, idx_parts,
                            (const int32_t*)key_parts, parts, part_len, k, slot_idx, (int32_t*)slot_key);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_packed(const int64_t* slot_idx, const void* slot_key, int key_width, uint32_t k,
+                                int64_t* row, hipStream_t st) {
+    const unsigned grid = (unsigned)((k + kBlock - 1) / kBlock);
+    if (key_width == 8)
+        hipLaunchKernelGGL(export_packed_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, st, slot_idx,
+                           (const int64_t*)slot_key, k, row);
+    else
+        hipLaunchKernelGGL(export_packed_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, st, slot_idx,
+                           (const int32_t*)slot_key, k, row);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_packed(const int64_t* rows, int32_t parts, int64_t stride, uint32_t k, int64_t* slot_idx,
+                               void* slot_key, int key_width, hipStream_t st) {
+    const unsigned grid = (unsigned)((k + kBlock - 1) / kBlock);
+    if (key_width == 8)
+        hipLaunchKernelGGL(merge_packed_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, st, rows, parts, stride, k,
+                           slot_idx, (int64_t*)slot_key);
+    else
+        hipLaunchKernelGGL(merge_packed_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, st, rows, parts, stride, k,
+                           slot_idx, (int32_t*)slot_key);
     return hipGetLastError();
 }
 

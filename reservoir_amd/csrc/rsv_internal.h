@@ -42,14 +42,28 @@ struct KernelTimer {
     size_t used = 0;
     double total_ms = 0;
     int64_t launches = 0;
-    void mark(hipStream_t st) {
-        if (!on) return;
+    hipEvent_t next() {
         if (used == ev.size()) {
             hipEvent_t e;
-            if (pool_event(&e, hipEventDefault) != hipSuccess) return;
+            if (pool_event(&e, hipEventDefault) != hipSuccess) return nullptr;
             ev.push_back(e);
         }
-        (void)hipEventRecord(ev[used++], st);
+        return ev[used++];
+    }
+    void mark(hipStream_t st) {
+        if (!on) return;
+        if (hipEvent_t e = next()) (void)hipEventRecord(e, st);
+    }
+    // start/stop events for hipExtLaunchKernelGGL: recorded by the dispatch packet itself, so the
+    // timed launch runs back to back with its neighbours (a separate hipEventRecord costs a ~5 us
+    // barrier packet between K1 and resolve).  Both null when timing is off.
+    void launch_pair(hipEvent_t& start, hipEvent_t& stop) {
+        start = stop = nullptr;
+        if (!on) return;
+        start = next();
+        stop = start ? next() : nullptr;
+        if (!stop) start = nullptr;
+        if (start == nullptr && used % 2) --used;  // keep (start, stop) pairs aligned
     }
     hipError_t drain() {
         for (size_t i = 0; i + 1 < used; i += 2) {
@@ -77,8 +91,10 @@ struct DrawParams {
 // ---- elements (Algorithm R, draw format R1) -------------------------------------------------
 // K1: per-slot last writer of the index range [lo, hi) (only indices >= k can evict) into
 // batch_win[k] (0 = no writer in this batch; atomicMax keeps the largest index).
+// ev_start / ev_stop (may be null): recorded by the first / last dispatch (hipExtLaunchKernelGGL)
 hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
-                                 unsigned long long* batch_win, hipStream_t st);
+                                 unsigned long long* batch_win, hipStream_t st,
+                                 hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 // Resolve: fill phase for slots in [base, base+n) and winners of batch_win; resets batch_win.
 // slot_idx may be null.
 hipError_t launch_init_slots(void* slot_key, int key_width, int64_t* slot_idx, unsigned long long* win, uint32_t k,
@@ -101,6 +117,12 @@ hipError_t launch_segmented(const void* keys, int key_width, const int64_t* offs
 hipError_t launch_merge_slots(const int64_t* idx_parts, const void* key_parts, int key_width,
                               int32_t parts, int64_t part_len, uint32_t k, int64_t* slot_idx,
                               void* slot_key, hipStream_t st);
+
+// packed combine rows: [slot_idx(k) | keys as int64 (k)]
+hipError_t launch_export_packed(const int64_t* slot_idx, const void* slot_key, int key_width, uint32_t k,
+                                int64_t* row, hipStream_t st);
+hipError_t launch_merge_packed(const int64_t* rows, int32_t parts, int64_t stride, uint32_t k, int64_t* slot_idx,
+                               void* slot_key, int key_width, hipStream_t st);
 
 // ---- distinct (bottom-k over the scrambled hash) --------------------------------------------
 struct DistinctState;  // defined in rsv_distinct.hip

@@ -273,9 +273,9 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
     } else {
         const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
         const uint64_t lo = std::max<uint64_t>((uint64_t)base, s->k), hi = (uint64_t)(base + n);
-        s->timer.mark(s->stream);
-        RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
-        s->timer.mark(s->stream);
+        hipEvent_t t0, t1;
+        s->timer.launch_pair(t0, t1);
+        RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream, t0, t1));
         RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, fresh,
                                    s->stream));
     }
@@ -710,6 +710,39 @@ rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* k
         RSV_HIP_TRY(launch_merge_slots(idx_dev, keys_dev, s->kw, parts, part_len, s->k, s->slot_idx, s->slot_key,
                                        s->stream));
     }
+    if (total_count > s->count) s->count = total_count;
+    if (s->own_stream) RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    return RSV_OK;
+}
+
+static rsv_status check_packed(rsv_sampler* s) {
+    if (rsv_status st = check_open(s)) return st;
+    if (s->cfg.kind != RSV_KIND_ELEMENTS) return fail(RSV_E_UNSUPPORTED, "packed rows hold ELEMENTS samplers only");
+    return RSV_OK;
+}
+
+rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev) {
+    if (rsv_status st = check_packed(s)) return st;
+    if (!row_dev) return fail(RSV_E_NULL_POINTER, "row_dev is NULL");
+    DeviceGuard g(s->device);
+    if (rsv_status st = flush_stage(s)) return st;
+    if (rsv_status st = ensure_slots(s)) return st;
+    RSV_HIP_TRY(launch_export_packed(s->slot_idx, s->slot_key, s->kw, s->k, row_dev, s->stream));
+    if (s->own_stream) RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    return RSV_OK;
+}
+
+rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t parts, int64_t row_stride,
+                            int64_t total_count) {
+    if (rsv_status st = check_packed(s)) return st;
+    if (parts < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative parts");
+    if (row_stride < 2 * (int64_t)s->k) return fail(RSV_E_ILLEGAL_ARGUMENT, "row_stride < 2k");
+    if (parts > 0 && !rows_dev) return fail(RSV_E_NULL_POINTER, "rows_dev is NULL");
+    DeviceGuard g(s->device);
+    if (rsv_status st = flush_stage(s)) return st;
+    if (rsv_status st = ensure_slots(s)) return st;
+    if (parts > 0)
+        RSV_HIP_TRY(launch_merge_packed(rows_dev, parts, row_stride, s->k, s->slot_idx, s->slot_key, s->kw, s->stream));
     if (total_count > s->count) s->count = total_count;
     if (s->own_stream) RSV_HIP_TRY(hipStreamSynchronize(s->stream));
     return RSV_OK;

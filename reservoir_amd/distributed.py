@@ -44,33 +44,39 @@ def combine(sampler, group=None, device=None, total_count: int | None = None) ->
     world = dist.get_world_size(group)
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+    if not sampler.is_distinct:
+        _combine_elements(sampler, world, group, device, total_count)
+        return
     idx, keys, hashes, n = sampler.export_state(device)
     k = keys.numel()
     dev = idx.device
-    if sampler.is_distinct:
-        width = 2 * k + 2
-        row = torch.empty(width, dtype=torch.int64, device=dev)
-        row[:k] = keys.to(torch.int64)
-        row[k:2 * k] = hashes
-        row[2 * k:] = torch.tensor([n, sampler.count], dtype=torch.int64).to(dev, non_blocking=True)
-    else:
-        width = 2 * k + (0 if total_count is not None else 1)
-        row = torch.empty(width, dtype=torch.int64, device=dev)
-        row[:k] = idx
-        row[k:2 * k] = keys.to(torch.int64)
-        if total_count is None:
-            row[2 * k] = sampler.count
+    width = 2 * k + 2
+    row = torch.empty(width, dtype=torch.int64, device=dev)
+    row[:k] = keys.to(torch.int64)
+    row[k:2 * k] = hashes
+    row[2 * k:] = torch.tensor([n, sampler.count], dtype=torch.int64).to(dev, non_blocking=True)
     flat = torch.empty(world * width, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(flat, row, group=group)  # flat output: gloo and RCCL both accept
     rows = flat.view(world, width)
-    g_keys = rows[:, (0 if sampler.is_distinct else k):(k if sampler.is_distinct else 2 * k)]
-    g_keys = g_keys.to(keys.dtype).contiguous()
-    if sampler.is_distinct:
-        meta = rows[:, 2 * k:].cpu()
-        part_n = meta[:, 0].tolist()
-        total = int(meta[:, 1].sum()) if total_count is None else int(total_count)
-        sampler.merge_state(torch.empty((world, k), dtype=torch.int64, device=dev), g_keys,
-                            rows[:, k:2 * k].contiguous(), part_n, total)
-    else:
-        total = int(rows[:, 2 * k].max().item()) if total_count is None else int(total_count)
-        sampler.merge_state(rows[:, :k].contiguous(), g_keys, hashes.expand(world, k), [k] * world, total)
+    g_keys = rows[:, :k].to(keys.dtype).contiguous()
+    meta = rows[:, 2 * k:].cpu()
+    part_n = meta[:, 0].tolist()
+    total = int(meta[:, 1].sum()) if total_count is None else int(total_count)
+    sampler.merge_state(torch.empty((world, k), dtype=torch.int64, device=dev), g_keys,
+                        rows[:, k:2 * k].contiguous(), part_n, total)
+
+
+def _combine_elements(sampler, world, group, device, total_count) -> None:
+    """Element sampler: one kernel packs ``[idx(k) | keys(k)]`` (+ the count when the global
+    length is unknown), one all-gather, one merge kernel over the gathered rows in place."""
+    k = sampler.max_sample_size
+    width = 2 * k + (0 if total_count is not None else 1)
+    row = torch.empty(width, dtype=torch.int64, device=device)
+    sampler.export_packed(row)
+    if total_count is None:
+        row[2 * k] = sampler.count
+    flat = torch.empty(world * width, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(flat, row, group=group)
+    rows = flat.view(world, width)
+    total = int(rows[:, 2 * k].max().item()) if total_count is None else int(total_count)
+    sampler.merge_packed(rows, total)

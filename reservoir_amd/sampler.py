@@ -245,6 +245,18 @@ class GpuSampler:
                                          C.byref(n)))
         return idx, keys, hashes, n.value
 
+    def export_packed(self, row) -> None:
+        """Element samplers: write ``[idx(k) | keys as int64 (k)]`` into the int64 device tensor
+        ``row`` (one kernel, stream-ordered on a caller stream)."""
+        N.check(self._L.rsv_export_packed(self._h, C.c_void_p(row.data_ptr())))
+
+    def merge_packed(self, rows, total_count: int) -> None:
+        """Element samplers: merge the packed rows of a ``[parts, width]`` int64 device tensor."""
+        if rows.dim() != 2 or not rows.is_contiguous():
+            raise IllegalArgumentException("rows must be a contiguous [parts, width] tensor")
+        N.check(self._L.rsv_merge_packed(self._h, C.c_void_p(rows.data_ptr()), int(rows.shape[0]),
+                                         int(rows.shape[1]), int(total_count)))
+
     def merge_state(self, idx, keys, hashes, part_n, total_count: int) -> None:
         """Merge gathered partial states ([parts, k] device tensors) into this sampler."""
         parts = int(keys.shape[0])

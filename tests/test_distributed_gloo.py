@@ -54,6 +54,19 @@ class OracleElements:
             self.res[better] = keys[p].numpy()[better]
         self.count = max(self.count, total)
 
+    # packed row protocol of GpuSampler.export_packed / merge_packed: [idx(k) | keys(k)]
+    @property
+    def max_sample_size(self):
+        return self.k
+
+    def export_packed(self, row):
+        row[: self.k] = torch.from_numpy(self.idx)
+        row[self.k: 2 * self.k] = torch.from_numpy(self.res)
+
+    def merge_packed(self, rows, total):
+        k = self.k
+        self.merge_state(rows[:, :k], rows[:, k:2 * k], None, None, total)
+
     def result(self):
         return self.res[: min(self.count, self.k)].copy()
 
@@ -111,6 +124,10 @@ def _worker(rank, world, port, n, k, q):
         s = OracleElements(k, 0xC0FFEE, 0x5A5A)
         D.sample_shard(s, keys[lo:hi], lo)
         D.combine(s, device="cpu")
+        s2 = OracleElements(k, 0xC0FFEE, 0x5A5A)  # bench.py's form: global length known
+        D.sample_shard(s2, keys[lo:hi], lo)
+        D.combine(s2, device="cpu", total_count=n)
+        assert s2.result().tolist() == s.result().tolist() and s2.count == n
         vals = np.random.default_rng(3).integers(-2**63, 2**63 - 1, size=n, dtype=np.int64)
         vals = np.concatenate([vals, vals[: n // 3]])
         dlo, dhi = D.shard_range(vals.size, rank, world)

@@ -192,6 +192,38 @@ def test_index_range_split_merge(cuda, oracle):
     assert np.array_equal(merged.result(), want)
 
 
+@pytest.mark.parametrize("key_type", ["long", "int"])
+def test_index_range_split_packed(cuda, oracle, key_type):
+    """The packed rows of distributed.combine: export_packed -> stacked rows -> merge_packed,
+    with a stride wider than 2k (the count column) and one part merged into a non-empty sampler."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    n, k, parts = 700_001, 777, 4
+    keys = oracle.splitmix_keys(77, n)
+    if key_type == "int":
+        keys = keys.astype(np.int32)  # wraps: negative Int keys exercise the sign-extended rows
+    want, _ = oracle.algo_r(5, 9, k, keys.astype(np.int64))
+    kd = torch.from_numpy(keys).to(cuda)
+    bounds = np.linspace(0, n, parts + 1).astype(np.int64)
+    rows = torch.full((parts - 1, 2 * k + 1), -7, dtype=torch.int64, device=cuda)
+    for p in range(parts - 1):
+        s = Sampler(k, seed=5, stream_id=9, key_type=key_type)()
+        s.seek(int(bounds[p]))
+        s.sample_all(kd[bounds[p]:bounds[p + 1]])
+        s.export_packed(rows[p])
+        s.close()
+    last = Sampler(k, seed=5, stream_id=9, key_type=key_type)()
+    last.seek(int(bounds[-2]))
+    last.sample_all(kd[bounds[-2]:])
+    last.merge_packed(rows, n)
+    assert last.count == n
+    got = last.result()
+    assert got.dtype == keys.dtype
+    assert np.array_equal(got.astype(np.int64), want)
+
+
 @pytest.mark.slow
 def test_full_size_split_invariance(cuda):
     """C2 size (1e9 keys, k = 1024): one pass == 7 ragged batches == 4-way index split."""
