@@ -9,8 +9,6 @@
 //
 // None of these kernels streams the key array: a draw depends only on (seed, stream, index), so
 // only the k winning keys are ever read (DESIGN.md "Roofline").
-#include <hip/hip_ext.h>
-
 #include <algorithm>
 
 #include "rsv_device.h"
@@ -59,6 +57,42 @@ __global__ __launch_bounds__(kBlock) void resolve_kernel(const KeyT* __restrict_
         slot_key[j] = 0;
         if (slot_idx) slot_idx[j] = -1;
     }
+}
+
+// resolve + publish in one dispatch (reservoirs of <= 8192 keys): one workgroup walks the k slots
+// as resolve_kernel does, writes the first m final slot keys straight into coherent host memory,
+// then publishes `gen` in the host flag with a system-scope release (as publish_kernel).
+template <typename KeyT>
+__global__ __launch_bounds__(1024) void resolve_publish_kernel(const KeyT* __restrict__ keys, int64_t base,
+                                                               int64_t n, uint32_t k,
+                                                               unsigned long long* __restrict__ win,
+                                                               KeyT* __restrict__ slot_key,
+                                                               int64_t* __restrict__ slot_idx, int fresh,
+                                                               int64_t m, KeyT* dst, uint32_t* flag, uint32_t gen) {
+    for (uint32_t j = threadIdx.x; j < k; j += blockDim.x) {
+        const unsigned long long wi = win[j];
+        KeyT v;
+        if (wi) {
+            v = keys[(int64_t)wi - base];
+            slot_key[j] = v;
+            slot_idx[j] = (int64_t)wi;
+            win[j] = 0;
+        } else if ((int64_t)j >= base && (int64_t)j < base + n) {
+            v = keys[j - base];
+            slot_key[j] = v;
+            slot_idx[j] = j;
+        } else if (fresh) {
+            v = 0;
+            slot_key[j] = 0;
+            slot_idx[j] = -1;
+        } else {
+            v = slot_key[j];
+        }
+        if ((int64_t)j < m) dst[j] = v;
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(kBlock) void replay_kernel(const int64_t* __restrict__ ev_pos,
@@ -213,22 +247,15 @@ inline unsigned grid_for(uint64_t items, unsigned cap) {
 }  // namespace
 
 hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
-                                 unsigned long long* batch_win, hipStream_t st, hipEvent_t ev_start,
-                                 hipEvent_t ev_stop) {
-    if (hi <= lo) {  // nothing to draw: the timer pair still needs both events recorded
-        if (ev_start) (void)hipEventRecord(ev_start, st);
-        if (ev_stop) (void)hipEventRecord(ev_stop, st);
-        return hipSuccess;
-    }
+                                 unsigned long long* batch_win, hipStream_t st) {
+    if (hi <= lo) return hipSuccess;
     const uint64_t g_end = (hi + 15) >> 4;
     constexpr uint64_t kMaxGroups = 1ull << 31;  // block offsets are 32-bit queue entries
     for (uint64_t g_begin = lo >> 4; g_begin < g_end; g_begin += kMaxGroups) {
         const uint64_t n_groups = std::min<uint64_t>(g_end - g_begin, kMaxGroups);
         const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 32);
-        const bool first = g_begin == (lo >> 4), last = g_begin + n_groups >= g_end;
-        hipExtLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, first ? ev_start : nullptr,
-                              last ? ev_stop : nullptr, 0, make_key(dp), k, lo, hi, g_begin, n_groups,
-                              batch_win);
+        hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
+                           g_begin, n_groups, batch_win);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -289,6 +316,21 @@ hipError_t launch_publish(const void* src, int64_t bytes, void* dst_host_dev, ui
                           hipStream_t st) {
     hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)src, (uint32_t*)dst_host_dev,
                        bytes / 4, flag_dev, gen);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve_publish(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,
+                                  unsigned long long* batch_win, void* slot_key, int64_t* slot_idx, bool fresh,
+                                  int64_t m, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st) {
+    const unsigned threads = std::min<unsigned>(1024, std::max<unsigned>(64, (k + 63) / 64 * 64));
+    if (key_width == 8)
+        hipLaunchKernelGGL(resolve_publish_kernel<int64_t>, dim3(1), dim3(threads), 0, st, (const int64_t*)keys, base,
+                           n, k, batch_win, (int64_t*)slot_key, slot_idx, (int)fresh, m, (int64_t*)dst_host_dev,
+                           flag_dev, gen);
+    else
+        hipLaunchKernelGGL(resolve_publish_kernel<int32_t>, dim3(1), dim3(threads), 0, st, (const int32_t*)keys, base,
+                           n, k, batch_win, (int32_t*)slot_key, slot_idx, (int)fresh, m, (int32_t*)dst_host_dev,
+                           flag_dev, gen);
     return hipGetLastError();
 }
 

@@ -146,6 +146,11 @@ struct rsv_sampler {
     uint32_t* result_flag = nullptr;
     uint32_t* result_flag_dev = nullptr;
     uint32_t result_gen = 0;
+    // small reservoirs: every batch's resolve also publishes the reservoir (resolve_publish
+    // kernel), so result() only waits for generation pub_gen -- while pub_valid says no other
+    // kernel (merge, init) has changed the slots since
+    uint32_t pub_gen = 0;
+    bool pub_valid = false;
     KernelTimer timer;
 };
 
@@ -199,6 +204,7 @@ rsv_status ensure_slots(rsv_sampler* s) {
     if (s->slots_init || s->cfg.kind != RSV_KIND_ELEMENTS) return RSV_OK;
     RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream));
     s->slots_init = s->win_zero = true;
+    s->pub_valid = false;
     return RSV_OK;
 }
 
@@ -238,6 +244,50 @@ bool give_clean_slots(void* p, uint32_t k, int kw, int device) {
     return true;
 }
 
+constexpr int64_t kPublishMaxBytes = 1 << 20;
+
+rsv_status ensure_result_buffer(rsv_sampler* s) {
+    if (s->result_h) return RSV_OK;
+    const size_t bytes = (size_t)s->k * s->kw;
+    if ((int64_t)bytes <= kPublishMaxBytes) {
+        const size_t flag_off = (bytes + 63) & ~(size_t)63;
+        RSV_HIP_TRY(pool_host_alloc(&s->result_h, flag_off + 64, hipHostMallocCoherent | hipHostMallocMapped));
+        void* dev = nullptr;
+        RSV_HIP_TRY(hipHostGetDevicePointer(&dev, s->result_h, 0));
+        s->result_dev = dev;
+        s->result_flag = (uint32_t*)((uint8_t*)s->result_h + flag_off);
+        s->result_flag_dev = (uint32_t*)((uint8_t*)dev + flag_off);
+        *s->result_flag = s->result_gen;
+        s->result_publish = true;
+    } else {
+        RSV_HIP_TRY(pool_host_alloc(&s->result_h, bytes, hipHostMallocDefault));
+    }
+    return RSV_OK;
+}
+
+constexpr uint32_t kFusedPublishMaxK = 8192;  // resolve_publish: one workgroup, <= 8 slots per lane
+
+// The batch's resolve: fill phase + winners into the slots; for reservoirs of <= 8192 keys it
+// also writes the first min(count, k) keys into the coherent result buffer and publishes
+// generation ++result_gen there (one dispatch instead of resolve now + publish at result()).
+rsv_status resolve_batch(rsv_sampler* s, const void* keys, int64_t base, int64_t n, bool fresh) {
+    if (s->k <= kFusedPublishMaxK) {
+        if (rsv_status st = ensure_result_buffer(s)) return st;
+        if (s->result_publish) {
+            const uint32_t gen = ++s->result_gen;
+            const int64_t m = std::min<int64_t>(base + n, (int64_t)s->k);
+            RSV_HIP_TRY(launch_resolve_publish(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx,
+                                               fresh, m, s->result_dev, s->result_flag_dev, gen, s->stream));
+            s->pub_gen = gen;
+            s->pub_valid = true;
+            return RSV_OK;
+        }
+    }
+    RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, fresh, s->stream));
+    s->pub_valid = false;
+    return RSV_OK;
+}
+
 // one batch of n keys already in device memory, at global indices [count, count+n)
 rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t* hashes, int64_t n) {
     if (n <= 0) return RSV_OK;
@@ -267,17 +317,15 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
             RSV_HIP_TRY(launch_replay_events(s->ev_pos_d, s->ev_slot_d, ne, s->k, s->batch_win, s->stream));
             s->timer.mark(s->stream);
         }
-        RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, fresh,
-                                   s->stream));
+        if (rsv_status st = resolve_batch(s, keys, base, n, fresh)) return st;
         if (ne) RSV_HIP_TRY(hipStreamSynchronize(s->stream));  // host event vectors are reused
     } else {
         const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
         const uint64_t lo = std::max<uint64_t>((uint64_t)base, s->k), hi = (uint64_t)(base + n);
-        hipEvent_t t0, t1;
-        s->timer.launch_pair(t0, t1);
-        RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream, t0, t1));
-        RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, fresh,
-                                   s->stream));
+        s->timer.mark(s->stream);
+        RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
+        s->timer.mark(s->stream);
+        if (rsv_status st = resolve_batch(s, keys, base, n, fresh)) return st;
     }
     if (s->cfg.kind == RSV_KIND_ELEMENTS) s->slots_init = s->win_zero = true;
     s->count = base + n;
@@ -514,27 +562,6 @@ rsv_status rsv_sample_batch(rsv_sampler* s, const void* keys, int64_t n, int32_t
     return fail(RSV_E_ILLEGAL_ARGUMENT, "mem must be RSV_MEM_HOST or RSV_MEM_DEVICE");
 }
 
-static constexpr int64_t kPublishMaxBytes = 1 << 20;
-
-static rsv_status ensure_result_buffer(rsv_sampler* s) {
-    if (s->result_h) return RSV_OK;
-    const size_t bytes = (size_t)s->k * s->kw;
-    if ((int64_t)bytes <= kPublishMaxBytes) {
-        const size_t flag_off = (bytes + 63) & ~(size_t)63;
-        RSV_HIP_TRY(pool_host_alloc(&s->result_h, flag_off + 64, hipHostMallocCoherent | hipHostMallocMapped));
-        void* dev = nullptr;
-        RSV_HIP_TRY(hipHostGetDevicePointer(&dev, s->result_h, 0));
-        s->result_dev = dev;
-        s->result_flag = (uint32_t*)((uint8_t*)s->result_h + flag_off);
-        s->result_flag_dev = (uint32_t*)((uint8_t*)dev + flag_off);
-        *s->result_flag = s->result_gen;
-        s->result_publish = true;
-    } else {
-        RSV_HIP_TRY(pool_host_alloc(&s->result_h, bytes, hipHostMallocDefault));
-    }
-    return RSV_OK;
-}
-
 // Wait until publish_kernel has stored `gen` (acquire).  Spins for up to ~2 ms -- the K1 pass of a
 // 1e9-element batch still in flight ahead of it is ~0.13 ms -- then falls back to a blocking stream
 // synchronize, which also reports a failed kernel instead of waiting forever.
@@ -588,8 +615,13 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
         } else if (m) {
             if (rsv_status st = ensure_result_buffer(s)) return st;
             if (s->result_publish) {  // publish kernel + flag spin (no D2H copy, no stream sync)
-                const uint32_t gen = ++s->result_gen;
-                RSV_HIP_TRY(launch_publish(src, m * s->kw, s->result_dev, s->result_flag_dev, gen, s->stream));
+                uint32_t gen = s->pub_gen;
+                if (!s->pub_valid) {  // the last batch's resolve did not publish the current slots
+                    gen = ++s->result_gen;
+                    RSV_HIP_TRY(launch_publish(src, m * s->kw, s->result_dev, s->result_flag_dev, gen, s->stream));
+                    s->pub_gen = gen;
+                    s->pub_valid = true;
+                }
                 if (rsv_status st = wait_flag(s, gen)) return st;
                 memcpy(out, s->result_h, (size_t)m * s->kw);
                 *out_n = m;
@@ -709,6 +741,7 @@ rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* k
         if (rsv_status st = ensure_slots(s)) return st;
         RSV_HIP_TRY(launch_merge_slots(idx_dev, keys_dev, s->kw, parts, part_len, s->k, s->slot_idx, s->slot_key,
                                        s->stream));
+        s->pub_valid = false;
     }
     if (total_count > s->count) s->count = total_count;
     if (s->own_stream) RSV_HIP_TRY(hipStreamSynchronize(s->stream));
@@ -741,8 +774,10 @@ rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t par
     DeviceGuard g(s->device);
     if (rsv_status st = flush_stage(s)) return st;
     if (rsv_status st = ensure_slots(s)) return st;
-    if (parts > 0)
+    if (parts > 0) {
         RSV_HIP_TRY(launch_merge_packed(rows_dev, parts, row_stride, s->k, s->slot_idx, s->slot_key, s->kw, s->stream));
+        s->pub_valid = false;
+    }
     if (total_count > s->count) s->count = total_count;
     if (s->own_stream) RSV_HIP_TRY(hipStreamSynchronize(s->stream));
     return RSV_OK;
