@@ -46,7 +46,7 @@ typedef enum rsv_kind {
 typedef enum rsv_engine {
     /* Algorithm R, data-parallel: element i >= k replaces slot j_i = floor(U_i (i+1) / 2^64) when
      * j_i < k, U_i a counter-based Philox4x32-10 draw of (seed, stream_id, i) (draw
-     * format R1).  Bit-identical for any batching and any index-range split over GPUs. */
+     * format R2).  Bit-identical for any batching and any index-range split over GPUs. */
     RSV_ENGINE_PHILOX_R = 0,
     /* The reference's own Algorithm L (S:224-246) driven by java.util.Random(seed), exactly as
      * SamplerTest.useConsistentRandom seeds it; the eviction events are replayed on the GPU.
@@ -173,7 +173,7 @@ rsv_status rsv_replay_events(const void* keys_dev, int64_t n, int32_t key_width,
                              const int64_t* ev_pos_dev, const int32_t* ev_slot_dev, int64_t n_events,
                              int32_t k, void* reservoir_dev, void* hip_stream);
 
-/* Export the per-element draw sequence j_i (format R1) for indices [i0, i0+n) into j_dev. */
+/* Export the per-element draw sequence j_i (format R2) for indices [i0, i0+n) into j_dev. */
 rsv_status rsv_export_draws(uint64_t seed, uint64_t stream_id, uint64_t i0, int64_t n,
                             uint64_t* j_dev, void* hip_stream);
 

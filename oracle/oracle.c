@@ -327,7 +327,7 @@ int64_t or_distinct_r0(const or_distinct* d) { return d->r0; }
 int64_t or_distinct_r1(const or_distinct* d) { return d->r1; }
 
 /* ------------------------------------------------------------------------------------------ */
-/* Philox4x32-10 (Salmon et al., SC'11; Random123 philox.h) and draw format R1                 */
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 philox.h) and draw format R2                 */
 /* ------------------------------------------------------------------------------------------ */
 void or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
     uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
@@ -343,9 +343,10 @@ void or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-/* Draw format R1 (DESIGN.md "Draw format"):
+/* Draw format R2 (DESIGN.md "Draw format"):
  *   key = (lo32(seed), hi32(seed)); ctr = (lo32(g), hi32(g) | domain bit 31, lo32(stream), hi32(stream))
- *   level 0: g = i >> 4, domain 0; b_i = byte (i & 15) of the 16-byte output (little endian words)
+ *   level 0: g = i >> 4, domain 0; the 128 output bits are 8 bit-planes of 16 bits, plane p =
+ *            bits [16 (p & 1), 16 (p & 1) + 16) of word p >> 1; b_i = sum_p bit (i & 15) of plane p << p
  *   level 1: g = i >> 1, domain 1; L_i = (w[2(i&1)] << 32) | w[2(i&1)+1]
  *   U_i = (b_i << 56) | (L_i >> 8);  j_i = floor(U_i * (i+1) / 2^64)                        */
 static void philox_at(uint64_t seed, uint64_t stream, uint64_t g, uint32_t dom, uint32_t out[4]) {
@@ -358,7 +359,8 @@ static void philox_at(uint64_t seed, uint64_t stream, uint64_t g, uint32_t dom, 
 uint64_t or_draw_u64(uint64_t seed, uint64_t stream, uint64_t i) {
     uint32_t w0[4], w1[4];
     philox_at(seed, stream, i >> 4, 0, w0);
-    uint64_t b = (w0[(i >> 2) & 3] >> (8 * (i & 3))) & 0xFF;
+    uint64_t b = 0;
+    for (int p = 0; p < 8; p++) b |= (uint64_t)((w0[p >> 1] >> (16 * (p & 1) + (i & 15))) & 1) << p;
     philox_at(seed, stream, i >> 1, 1, w1);
     uint64_t L = ((uint64_t)w1[2 * (i & 1)] << 32) | w1[2 * (i & 1) + 1];
     return (b << 56) | (L >> 8);

@@ -80,13 +80,13 @@ int64_t or_distinct_r0(const or_distinct* d);
 int64_t or_distinct_r1(const or_distinct* d);
 int64_t or_distinct_scramble(int64_t r0, int64_t r1, int64_t hashed);
 
-/* ---- Philox4x32-10 (Random123) and the build's own Algorithm-R draw format "R1" ---- */
+/* ---- Philox4x32-10 (Random123) and the build's own Algorithm-R draw format "R2" ---- */
 void     or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 uint64_t or_draw_u64(uint64_t seed, uint64_t stream, uint64_t i);          /* U_i */
 uint64_t or_draw_j(uint64_t seed, uint64_t stream, uint64_t i);            /* j_i = floor(U_i (i+1) / 2^64) */
 void     or_export_draws(uint64_t seed, uint64_t stream, uint64_t i0, int64_t n, uint64_t* out_j);
 
-/* Sequential Algorithm R fed with the R1 draw sequence (the P2 contract).
+/* Sequential Algorithm R fed with the R2 draw sequence (the P2 contract).
  * keys[0..n) are the elements at global indices [i0, i0+n); res[k] holds the state
  * (caller initialises it for i0 > 0).  Returns number of replacements. */
 int64_t or_algo_r(uint64_t seed, uint64_t stream, int32_t k, uint64_t i0,

@@ -217,7 +217,7 @@ def export_draws(seed: int, stream: int, i0: int, n: int) -> np.ndarray:
 
 
 def algo_r(seed: int, stream: int, k: int, keys, i0: int = 0, res=None):
-    """Sequential Algorithm R with draw format R1. Returns (reservoir[min(i0+n,k)], replacements)."""
+    """Sequential Algorithm R with draw format R2. Returns (reservoir[min(i0+n,k)], replacements)."""
     keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
     if res is None:
         res = np.zeros(k, dtype=np.int64)

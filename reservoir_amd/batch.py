@@ -5,7 +5,7 @@ libreservoir_hip.so.  Every function raises if the engine is unavailable.
 
     sample_segmented  -- K2: S independent samplers in one launch (one wave per stream)
     replay_events     -- K1': apply the reference's Algorithm-L eviction events on the GPU
-    export_draws      -- the per-element draw sequence j_i of draw format R1
+    export_draws      -- the per-element draw sequence j_i of draw format R2
 """
 from __future__ import annotations
 

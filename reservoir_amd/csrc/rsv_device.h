@@ -1,16 +1,19 @@
-// rsv_device.h -- device helpers shared by the gfx950 kernels: Philox4x32-10, draw format R1,
+// rsv_device.h -- device helpers shared by the gfx950 kernels: Philox4x32-10, draw format R2,
 // and the scrambled hash of Sampler.distinct.
 //
-// Draw format R1 (DESIGN.md "Draw format"): for element index i of Philox stream s under key
+// Draw format R2 (DESIGN.md "Draw format"): for element index i of Philox stream s under key
 // (seed), U_i is a 64-bit uniform assembled from two counter-based Philox4x32-10 calls:
-//   level 0: ctr = (g0, g0>>32, s, s>>32), g0 = i >> 4   -> 16 bytes shared by 16 indices;
-//            b_i = byte (i & 15) (little-endian words) is the top byte of U_i
+//   level 0: ctr = (g0, g0>>32, s, s>>32), g0 = i >> 4   -> 128 bits shared by 16 indices, read
+//            as 8 bit-planes of 16 bits (plane p = bits [16 (p&1), 16 (p&1) + 16) of word p>>1);
+//            b_i = the byte whose bit p is bit (i & 15) of plane p -- the top byte of U_i
 //   level 1: ctr = (g1, (g1>>32) | 1<<31, s, s>>32), g1 = i >> 1 -> two 64-bit words;
 //            L_i = word (i & 1) = (w[2(i&1)] << 32) | w[2(i&1)+1]
 //   U_i = (b_i << 56) | (L_i >> 8),  j_i = floor(U_i * (i+1) / 2^64)   (uniform on [0, i])
 // Element i >= k replaces slot j_i iff j_i < k (Algorithm R).  Since U_i >= b_i * 2^56, a
 // necessary condition for j_i < k is b_i * (i+1) < 256 k; the kernels test that on level-0
-// bytes only and evaluate level 1 for the ~1/256 candidates that pass.
+// bits only and evaluate level 1 for the ~1/256 candidates that pass.  The bit-sliced layout makes
+// the sparse-region test "some b_i of the block is 0" one OR over the four words and a fold of
+// the two 16-bit halves (5 VALU ops for 16 indices; per-byte SWAR took 11).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -65,9 +68,12 @@ __device__ __forceinline__ uint32_t word_of(const u32x4& w, uint32_t q) {
     return q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
 }
 
-// byte e (0..15) of a level-0 block
+// b_e (e = 0..15) of a level-0 block: bit e of each of the 8 planes
 __device__ __forceinline__ uint32_t level0_byte(const u32x4& w, uint32_t e) {
-    return (word_of(w, e >> 2) >> (8 * (e & 3))) & 0xFFu;
+    // planes 2q (bit 0 after the shift) and 2q+1 (bit 16) of word q, interleaved into bits 2q, 2q+1
+    const uint32_t u = ((w.x >> e) & 0x10001u) | (((w.y >> e) & 0x10001u) << 2) |
+                       (((w.z >> e) & 0x10001u) << 4) | (((w.w >> e) & 0x10001u) << 6);
+    return (u & 0x55u) | ((u >> 15) & 0xAAu);
 }
 
 // exact j_i given b_i (level-1 evaluated here)
@@ -80,27 +86,30 @@ __device__ __forceinline__ uint64_t exact_j(const DrawKey& dk, uint64_t i, uint3
     return __umul64hi(U, i + 1);
 }
 
-// 16-bit mask of zero bytes of a level-0 block (exact: no false positives)
-__device__ __forceinline__ uint32_t zero_byte_mask16(const u32x4& w) {
-    uint32_t m = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t x = word_of(w, q);
-        const uint32_t y = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte
-        // gather bits 7, 15, 23, 31 -> 4 bits
-        m |= (((y >> 7) & 1u) | ((y >> 14) & 2u) | ((y >> 21) & 4u) | ((y >> 28) & 8u)) << (4 * q);
-    }
-    return m;
+// OR of the 8 planes folded onto bits 0..15 and 16..31 alike: bit e clear <=> b_e == 0
+__device__ __forceinline__ uint32_t planes_or(const u32x4& w) {
+    const uint32_t x = w.x | w.y | w.z | w.w;
+    return x | __builtin_amdgcn_alignbit(x, x, 16);  // x | rotate(x, 16)
 }
 
-// true iff some byte of the block is zero (sparse-region pre-test).  haszero(x) =
-// (x - 0x01010101) & ~x & 0x80808080 is non-zero exactly when x has a zero byte (its false
-// positives only occur above a true zero byte); hipcc folds the and-not-and into one v_bitop3.
-__device__ __forceinline__ uint32_t haszero_bits(uint32_t x) {
-    return (x - 0x01010101u) & ~x & 0x80808080u;
-}
-__device__ __forceinline__ bool any_zero_byte(const u32x4& w) {
-    return (haszero_bits(w.x) | haszero_bits(w.y) | haszero_bits(w.z) | haszero_bits(w.w)) != 0u;
+// 16-bit mask of the zero bytes b_e == 0 of a level-0 block (exact)
+__device__ __forceinline__ uint32_t zero_byte_mask16(const u32x4& w) { return ~planes_or(w) & 0xFFFFu; }
+
+// true iff some b_e of the block is zero (the sparse-region candidate test)
+__device__ __forceinline__ bool any_zero_byte(const u32x4& w) { return planes_or(w) != 0xFFFFFFFFu; }
+
+// 16-bit mask of b_e < T (T in [0, 256]): bit-sliced compare, most significant plane first
+__device__ __forceinline__ uint32_t lt_mask16(const u32x4& w, uint32_t T) {
+    if (T >= 256u) return 0xFFFFu;
+    uint32_t lt = 0, eq = 0xFFFFu;
+#pragma unroll
+    for (int p = 7; p >= 0; --p) {
+        const uint32_t plane = (word_of(w, (uint32_t)p >> 1) >> (16 * (p & 1))) & 0xFFFFu;
+        const uint32_t tm = 0u - ((T >> p) & 1u);  // all ones where T has bit p
+        lt |= eq & ~plane & tm;
+        eq &= ~(plane ^ tm);
+    }
+    return lt & 0xFFFFu;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1,5 +1,5 @@
 // rsv_elements.hip -- gfx950 kernels for the element sampler (Sampler.apply, Sampler.scala:196-332)
-// reformulated as data-parallel Algorithm R with counter-based draws (format R1, rsv_device.h).
+// reformulated as data-parallel Algorithm R with counter-based draws (format R2, rsv_device.h).
 //
 //   K1  k1_last_writer   single stream: per-slot last writer (max index) of an index range
 //   --  resolve          fill phase + gather of the winning keys into the reservoir
@@ -21,18 +21,19 @@ namespace {
 
 constexpr int kBlock = 256;
 
-// K1: grid-stride over level-0 blocks (16 indices each); wave-uniform loop so the candidate
-// queue can run full-wave level-1 evaluations.  Hits (k ln(n/k) of them) go straight to global
-// atomicMax on the k-slot winner table: 14k atomics per 1e9 indices at k = 1024.
+// K1: grid-stride over level-0 blocks (16 indices each); one bit per block marks a zero byte, and
+// every 16 iterations the marked blocks go through the wave's LDS queue so the level-1 draws run
+// with all 64 lanes busy (rsv_scan.h k1_body_bits).  Hits (k ln(n/k) of them) go straight to
+// global atomicMax on the k-slot winner table: 14k atomics per 1e9 indices at k = 1024.
 constexpr int kK1Unroll = 2;  // level-0 blocks per lane per iteration (two Philox chains in flight)
 
 __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k, uint64_t lo,
                                                          uint64_t hi, uint64_t g_begin,
                                                          uint64_t n_groups,
                                                          unsigned long long* __restrict__ win) {
-    __shared__ uint32_t qs[kBlock / 64][63 + 64 * kK1Unroll + 1];
+    __shared__ uint32_t qs[kBlock / 64][63 + 64 + 1];
     __shared__ uint64_t cqs[kBlock / 64][kQueue];
-    k1_body<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
+    k1_body_bits<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
 }
 
 // Per slot j: the batch's last writer (win[j], then cleared), else the fill of j < k from this
@@ -253,7 +254,8 @@ hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, 
     constexpr uint64_t kMaxGroups = 1ull << 31;  // block offsets are 32-bit queue entries
     for (uint64_t g_begin = lo >> 4; g_begin < g_end; g_begin += kMaxGroups) {
         const uint64_t n_groups = std::min<uint64_t>(g_end - g_begin, kMaxGroups);
-        const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 32);
+        // two resident rounds of 4-wave workgroups (8 waves per SIMD): measured best (tools/micro_k1)
+        const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 16);
         hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
                            g_begin, n_groups, batch_win);
         hipError_t e = hipGetLastError();

@@ -78,7 +78,7 @@ struct DrawParams {
     uint64_t stream;
 };
 
-// ---- elements (Algorithm R, draw format R1) -------------------------------------------------
+// ---- elements (Algorithm R, draw format R2) -------------------------------------------------
 // K1: per-slot last writer of the index range [lo, hi) (only indices >= k can evict) into
 // batch_win[k] (0 = no writer in this batch; atomicMax keeps the largest index).
 hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,

@@ -6,6 +6,8 @@
 // iteration holds one (64 lanes x 16 indices / 256), so the whole wave pays a second Philox for a
 // single active lane -- measured 383 us vs ~120 us for the level-0 work alone at 1e9 indices.
 #pragma once
+#include <algorithm>
+
 #include "rsv_device.h"
 
 namespace rsv {
@@ -25,42 +27,20 @@ __device__ __forceinline__ uint32_t clip_mask16(uint64_t i0, uint64_t lo, uint64
     return m;
 }
 
-// Candidate mask of one level-0 block: bit e set iff b_{i0+e} * (i0+e+1) < 256k (a necessary
-// condition for j < k).  Beyond index 256k-1 this is simply "byte == 0" (1 in 256).  In the dense
-// region (K2's whole 4096-element streams at k = 64) a SWAR test "byte < T" with the block's
-// threshold T = ceil(256k / (i0+1)) (computed in fp32, rounded up) gives a superset with three
-// VALU ops per word; the few set bits are then checked exactly.
-__device__ __forceinline__ uint32_t gather_bit7(uint32_t y) {  // bits 7, 15, 23, 31 -> 0..3
-    return ((y >> 7) & 1u) | ((y >> 14) & 2u) | ((y >> 21) & 4u) | ((y >> 28) & 8u);
-}
-
+// Candidate mask of one level-0 block: bit e set if b_{i0+e} * (i0+e+1) < 256k may hold (a
+// necessary condition for j < k).  Beyond index 256k-1 this is exactly "b == 0" (1 in 256).  In
+// the dense region (K2's whole 4096-element streams at k = 64) the bit-sliced test "b < T" with
+// the block's threshold T = ceil(256k / (i0+1)) gives a superset for the block's 16 indices (exact
+// for the first); the level-1 draw decides every candidate exactly.
 __device__ __forceinline__ uint32_t candidate_mask16(const u32x4& w, uint64_t i0, uint64_t dense_lim) {
-    if (i0 + 1 >= dense_lim) {
-        if (!any_zero_byte(w)) return 0u;
-        return zero_byte_mask16(w);
-    }
-    // T = ceil(dense_lim / (i0+1)): b < T <=> b (i0+1) < dense_lim, exact for the block's first
-    // index and a superset for the other 15 (the level-1 draw decides the hit exactly anyway)
-    uint32_t T = (uint32_t)__fdividef((float)dense_lim, (float)(i0 + 1));
-    if (T <= 130u) {
-        while ((uint64_t)T * (i0 + 1) < dense_lim) ++T;
-        while (T > 0 && (uint64_t)(T - 1) * (i0 + 1) >= dense_lim) --T;
-    }
-    if (T <= 127u) {
-        const uint32_t C = (128u - T) * 0x01010101u;
-        uint32_t m = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            const uint32_t x = word_of(w, q);
-            m |= gather_bit7(~(((x & 0x7F7F7F7Fu) + C) | x) & 0x80808080u) << (4 * q);  // byte < T
-        }
-        return m;
-    }
-    uint32_t m = 0;  // T >= 128: the first ~256k/128 indices of a stream -- exact per byte
-#pragma unroll
-    for (uint32_t e = 0; e < 16; ++e)
-        if ((uint64_t)level0_byte(w, e) * (i0 + e + 1) < dense_lim) m |= 1u << e;
-    return m;
+    if (i0 + 1 >= dense_lim) return zero_byte_mask16(w);
+    // T = ceil(dense_lim / (i0+1)): the fp32 estimate is within a few units; correct it exactly
+    const float Tf = __fdividef((float)dense_lim, (float)(i0 + 1));
+    if (Tf > 300.0f) return 0xFFFFu;  // T > 256: every byte qualifies
+    uint64_t T = (uint64_t)Tf;
+    while (T * (i0 + 1) < dense_lim) ++T;
+    while (T > 0 && (T - 1) * (i0 + 1) >= dense_lim) --T;
+    return lt_mask16(w, T > 256 ? 256u : (uint32_t)T);
 }
 
 // Evaluate queue entry q[pos] (level 1) and report a hit (j < k) to `hit(j, i)`.
@@ -201,6 +181,82 @@ __device__ __forceinline__ void k1_body(const DrawKey& dk, uint32_t k, uint64_t 
             has[u] = (off[u] < n_groups) &  // bitwise: no short-circuit branches
                      (((((g_begin + off[u]) << 4) + 1) < dense_lim) | any_zero_byte(w[u]));
         push_blocks<U>(has, off, q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
+    }
+    drain_blocks(q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
+}
+
+// ---- K1 with deferred pushes -------------------------------------------------------------------
+// The per-iteration push above runs on ~every iteration (some lane of the wave nearly always holds
+// a candidate block) and cost ~28 us per 1e9 indices.  Here each lane only ORs one bit per block
+// into a register mask; every W = 32 / U iterations the wave pushes the set bits in rounds -- each
+// round every lane with bits left pushes its lowest one (ballot + prefix count), so a round is one
+// wave-uniform step and the queue needs room for just one round (64) beyond a partial batch.
+// Bit b of a window starting at `base0` is the block at offset base0 + (b / U) * stride + (b % U) * 64
+// + lane (all 32-bit: offsets < 2^31 per launch, stride * W < 2^32).
+template <int U, class Hit>
+__device__ __forceinline__ void push_bits(uint32_t bits, uint32_t base0, uint32_t stride, uint32_t* q, uint32_t& qn,
+                                          uint64_t* cq, uint32_t& cqn, uint32_t lane, const DrawKey& dk,
+                                          uint64_t g_begin, uint64_t lo, uint64_t hi, uint64_t dense_lim, uint32_t k,
+                                          Hit& hit) {
+    const unsigned long long lt = lanemask_lt64();
+    while (__any(bits != 0)) {
+        const bool has = bits != 0;
+        const unsigned long long bal = __ballot(has);
+        if (has) {
+            const uint32_t b = __builtin_ctz(bits);
+            bits &= bits - 1;
+            q[qn + __popcll(bal & lt)] = base0 + (b / U) * stride + (b % U) * 64u + lane;
+        }
+        qn += (uint32_t)__popcll(bal);
+        if (qn >= 64) {
+            qn -= 64;
+            __builtin_amdgcn_wave_barrier();
+            resolve_block(dk, true, g_begin + q[qn + lane], lo, hi, dense_lim, k, cq, cqn, lane, hit);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+template <int U>
+__device__ __forceinline__ void k1_body_bits(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi,
+                                             uint64_t g_begin, uint64_t n_groups,
+                                             unsigned long long* __restrict__ win, uint32_t* q, uint64_t* cq) {
+    constexpr int W = 32 / U;  // iterations per push window (one bit per block)
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t qn = 0, cqn = 0;
+    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
+    const uint64_t dense_lim = 256ull * k;
+    const uint32_t ng = (uint32_t)n_groups;  // < 2^31 per launch (host splits)
+    // first offset whose block lies wholly in the sparse region (16 g + 1 >= 256 k): from there on
+    // a block holds a candidate iff one of its 16 level-0 bytes is zero
+    const uint64_t g_sparse = (dense_lim + 14) >> 4;
+    const uint32_t off_sparse = g_sparse <= g_begin ? 0u : (uint32_t)std::min<uint64_t>(g_sparse - g_begin, ng);
+    const uint32_t stride = gridDim.x * blockDim.x * U;
+    uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
+    // per-lane level-0 counter kept in VGPRs and stepped by `stride` (rebuilding it from a
+    // scalar base every iteration made the compiler pad SALU->VALU hazards with 15 s_nop)
+    uint64_t gl = g_begin + base + lane;
+    while (base < ng) {  // wave-uniform
+        const uint32_t base0 = base;
+        uint32_t bits = 0;
+        for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride) {
+            u32x4 w[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) w[u] = level0(dk, gl + u * 64);
+            if (base >= off_sparse && base + U * 64 <= ng) {  // steady state: zero-byte test only
+#pragma unroll
+                for (int u = 0; u < U; ++u) bits |= (uint32_t)any_zero_byte(w[u]) << (t * U + u);
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t off = base + u * 64 + lane;
+                    const bool has =
+                        (off < ng) & (((((g_begin + off) << 4) + 1) < dense_lim) | any_zero_byte(w[u]));
+                    bits |= (uint32_t)has << (t * U + u);
+                }
+            }
+        }
+        push_bits<U>(bits, base0, stride, q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
     }
     drain_blocks(q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
 }

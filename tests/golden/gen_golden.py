@@ -58,7 +58,7 @@ def main():
         "survey_k20": algo_l_case(20, 3000, 0),
         "algo_l": [algo_l_case(5, 10, 0), algo_l_case(100, 100_000, 42), algo_l_case(64, 10_000, 7),
                    algo_l_case(1000, 50_000, 123), algo_l_case(1, 1000, 9), algo_l_case(3, 3, 1)],
-        "draws_r1": [draws_case(0, 0, 0, 48), draws_case(0xC0FFEE, 0x5A5A, 1000, 32),
+        "draws": [draws_case(0, 0, 0, 48), draws_case(0xC0FFEE, 0x5A5A, 1000, 32),
                      draws_case(1, 2, 2**32 - 7, 16), draws_case(2**63 + 5, 2**40 + 3, 2**40, 16)],
         "algo_r": [algo_r_case(0xC0FFEE, 0, 64, 5000, 0x5EED0000), algo_r_case(7, 3, 5, 10, 1),
                    algo_r_case(11, 0, 1000, 20_000, 99), algo_r_case(0, 0, 1, 777, 5)],

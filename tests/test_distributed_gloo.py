@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 class OracleElements:
-    """Algorithm R (draw format R1) shard sampler on the oracle."""
+    """Algorithm R (draw format R2) shard sampler on the oracle."""
 
     is_distinct = False
 

@@ -1,7 +1,7 @@
 """Element sampler (Sampler.apply) on the GPU: parity with the oracle, boundaries, lifecycle.
 
 Parity contract P2: the "philox_r" engine equals the sequential Algorithm R
-restatement fed the same draw sequence (format R1), bit-exactly, for every batching and split.
+restatement fed the same draw sequence (format R2), bit-exactly, for every batching and split.
 """
 import json
 import os
@@ -83,7 +83,7 @@ def test_int_keys_and_map(cuda, oracle):
 def test_draw_export_matches_oracle(cuda, oracle):
     from reservoir_amd import batch
 
-    for case in GOLDEN["draws_r1"]:
+    for case in GOLDEN["draws"]:
         j = batch.export_draws(case["seed"], case["stream"], case["i0"], case["n"]).cpu().numpy()
         assert [int(x) for x in j.astype(np.uint64)] == case["j"]
     j = batch.export_draws(17, 3, 10_000, 100_000).cpu().numpy().astype(np.uint64)

@@ -81,7 +81,7 @@ def test_golden_algo_l(oracle, case):
     assert [[int(p), int(q)] for p, q in zip(pos[:16], slot[:16])] == case["events_head"]
 
 
-@pytest.mark.parametrize("case", GOLDEN["draws_r1"], ids=lambda c: f"i0_{c['i0']}")
+@pytest.mark.parametrize("case", GOLDEN["draws"], ids=lambda c: f"i0_{c['i0']}")
 def test_golden_draws(oracle, case):
     j = oracle.export_draws(case["seed"], case["stream"], case["i0"], case["n"])
     assert [int(x) for x in j] == case["j"]

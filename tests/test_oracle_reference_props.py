@@ -105,7 +105,7 @@ def test_distinct_colliding_hash_keeps_everything_below_max(oracle):
 
 
 def test_algo_r_draw_uniformity(oracle):
-    """Draw format R1: j_i uniform on [0, i] (chi-square over 32 bins at i = 31)."""
+    """Draw format R2: j_i uniform on [0, i] (chi-square over 32 bins at i = 31)."""
     # index 31 in many independent streams
     j = np.array([oracle.draw_j(1234, s, 31) for s in range(64000)])
     assert j.min() >= 0 and j.max() <= 31

@@ -4,6 +4,8 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <vector>
+
 #include "../reservoir_amd/csrc/rsv_device.h"
 #include "../reservoir_amd/csrc/rsv_scan.h"
 
@@ -79,6 +81,14 @@ __global__ __launch_bounds__(256) void k1_var(DrawKey dk, uint32_t k, uint64_t l
     k1_body<U>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
 }
 
+template <int U>
+__global__ __launch_bounds__(256) void k1_var_bits(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                                   uint64_t n_groups, unsigned long long* win) {
+    __shared__ uint32_t qs[4][63 + 64 + 1];
+    __shared__ uint64_t cqs[4][kQueue];
+    k1_body_bits<U>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
+}
+
 int main(int argc, char** argv) {
     uint32_t* d;
     CK(hipMalloc(&d, 64));
@@ -150,6 +160,37 @@ int main(int argc, char** argv) {
                ms / 5 * 1e3, ms1 * 1e3);
         return 0;
     };
+    if (argc > 1 && argv[1][0] == 'p') {  // one launch of each variant, for rocprofv3 --pmc passes
+        hipLaunchKernelGGL(philox_only, dim3(8192), dim3(256), 0, 0, dk, n_groups, cnt);
+        hipLaunchKernelGGL(k1_level0_only, dim3(8192), dim3(256), 0, 0, dk, n_groups, cnt);
+        hipLaunchKernelGGL(k1_var<2>, dim3(4096), dim3(256), 0, 0, dk, 1024u, 1024ull, 1000000000ull, 0ull,
+                           n_groups, win);
+        hipLaunchKernelGGL(k1_var_bits<2>, dim3(4096), dim3(256), 0, 0, dk, 1024u, 1024ull, 1000000000ull, 0ull,
+                           n_groups, win);
+        CK(hipDeviceSynchronize());
+        return 0;
+    }
+    if (argc > 1) {  // A/B: per-iteration pushes vs deferred bit-mask pushes (+ identical winners)
+        std::vector<unsigned long long> ref(1024), got(1024);
+        auto run_once = [&](auto kern, int grid, std::vector<unsigned long long>& out) -> int {
+            CK(hipMemset(win, 0, 1024 * 8));
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, dk, 1024u, 1024ull, 1000000000ull, 0ull, n_groups,
+                               win);
+            CK(hipMemcpy(out.data(), win, 1024 * 8, hipMemcpyDeviceToHost));
+            return 0;
+        };
+        if (run_once(k1_var<2>, 8192, ref)) return 1;
+        for (int grid : {2048, 4096, 8192, 16384}) {
+            time_v(k1_var<2>, "k1 per-iteration push", grid / 2, 2);
+            time_v(k1_var_bits<1>, "k1 bit-mask push", grid, 1);
+            time_v(k1_var_bits<2>, "k1 bit-mask push", grid / 2, 2);
+            if (run_once(k1_var_bits<2>, grid / 2, got)) return 1;
+            printf("  winners identical: %s\n", ref == got ? "yes" : "NO");
+            if (run_once(k1_var_bits<1>, grid, got)) return 1;
+            printf("  winners identical (U=1): %s\n", ref == got ? "yes" : "NO");
+        }
+        return 0;
+    }
     for (int grid : {4096, 8192, 16384}) {
         time_v(k1_var<1>, "k1 product body", grid / 1, 1);
         time_v(k1_var<2>, "k1 product body", grid / 2, 2);
