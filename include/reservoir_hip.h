@@ -62,6 +62,22 @@ typedef enum rsv_hash_kind {
     RSV_HASH_PRECOMPUTED = 4  /* caller passes int64 hashes beside the keys (arbitrary JVM `hash`) */
 } rsv_hash_kind;
 
+/* How a DISTINCT sampler resolves elements whose scrambled hashes tie.  The reference keeps the
+ * elements of its max-heap (S:389-409): with an injective hash that is the bottom-k of the hashes,
+ * independent of arrival order; with a colliding hash (Long#hashCode folds to 32 bits) the members of
+ * the boundary hash bucket depend on arrival order and on PriorityQueue tie-breaking. */
+typedef enum rsv_distinct_order {
+    /* ORDERED for RSV_HASH_JAVA_LONG / PRECOMPUTED (may collide), SET for IDENTITY / JAVA_INT */
+    RSV_DISTINCT_AUTO = 0,
+    /* bottom-k by (hash, key): order-independent and mergeable across GPUs; equal to the
+     * reference's set whenever no distinct elements share the final maximum hash */
+    RSV_DISTINCT_SET = 1,
+    /* the reference's sequential semantics for any hash: the GPU filters each chunk of the batch
+     * against the current maximum (a superset of what the reference inserts), the host replays
+     * the survivors in arrival order through an exact RandomValues replica (heap + hash set) */
+    RSV_DISTINCT_ORDERED = 2
+} rsv_distinct_order;
+
 typedef enum rsv_mem { RSV_MEM_HOST = 0, RSV_MEM_DEVICE = 1 } rsv_mem;
 
 typedef struct rsv_config {
@@ -74,7 +90,7 @@ typedef struct rsv_config {
     int32_t  engine;          /* rsv_engine (ELEMENTS only) */
     int32_t  hash_kind;       /* rsv_hash_kind (DISTINCT only) */
     int32_t  device;          /* HIP device ordinal; -1 = the calling thread's current device */
-    int32_t  reserved0;
+    int32_t  distinct_order;  /* rsv_distinct_order (DISTINCT only) */
     uint64_t seed;            /* PHILOX_R: Philox key; JAVA_L / DISTINCT: java.util.Random seed (S:199, S:385-388) */
     uint64_t stream_id;       /* PHILOX_R: Philox stream (independent sampler id) */
 } rsv_config;

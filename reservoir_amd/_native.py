@@ -19,6 +19,7 @@ KIND_ELEMENTS, KIND_DISTINCT = 0, 1
 ENGINE_PHILOX_R, ENGINE_JAVA_L = 0, 1
 HASH_DEFAULT, HASH_IDENTITY, HASH_JAVA_LONG, HASH_JAVA_INT, HASH_PRECOMPUTED = range(5)
 MEM_HOST, MEM_DEVICE = 0, 1
+DISTINCT_AUTO, DISTINCT_SET, DISTINCT_ORDERED = 0, 1, 2
 
 # every symbol include/reservoir_hip.h declares
 EXPORTED_SYMBOLS = (
@@ -42,7 +43,7 @@ class RsvConfig(C.Structure):
         ("engine", C.c_int32),
         ("hash_kind", C.c_int32),
         ("device", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("distinct_order", C.c_int32),
         ("seed", C.c_uint64),
         ("stream_id", C.c_uint64),
     ]

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <algorithm>
 #include <vector>
@@ -181,6 +182,58 @@ __global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ key
     out.flush();
 }
 
+// Ordered-mode filter (RSV_DISTINCT_ORDERED): elements [0, n) of one chunk with h <= tinc, each
+// with its chunk-relative index so the host can replay them in arrival order.  Per-wave LDS staging
+// and one reservation atomic per 64 survivors, as k3_filter; plain grid-stride loads (the ordered
+// path is bound by the host replay, not by this pass).
+template <typename KeyT, int HASH>
+__global__ __launch_bounds__(kBlock) void k3_filter_idx(const KeyT* __restrict__ keys,
+                                                        const int64_t* __restrict__ hashes, int64_t n,
+                                                        int64_t r0, int64_t r1, int64_t tinc,
+                                                        int64_t* __restrict__ cand_h, KeyT* __restrict__ cand_k,
+                                                        uint32_t* __restrict__ cand_i,
+                                                        unsigned long long* __restrict__ counter, int64_t cap) {
+    __shared__ int64_t sh_h[kBlock / 64][128];
+    __shared__ KeyT sh_k[kBlock / 64][128];
+    __shared__ uint32_t sh_i[kBlock / 64][128];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t qn = 0;
+    auto write64 = [&](uint32_t from, uint32_t cnt) {
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(counter, (unsigned long long)cnt);
+        base = __shfl(base, 0);
+        if (lane < cnt && (int64_t)(base + lane) < cap) {
+            cand_h[base + lane] = sh_h[w][from + lane];
+            cand_k[base + lane] = sh_k[w][from + lane];
+            cand_i[base + lane] = sh_i[w][from + lane];
+        }
+    };
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx - lane < n; idx += T) {
+        const bool ok = idx < n;
+        const KeyT key = ok ? keys[idx] : (KeyT)0;
+        const int64_t h = ok ? elem_hash<KeyT, HASH>(keys, hashes, idx, key, r0, r1) : 0;
+        const bool c = ok && h <= tinc;
+        const unsigned long long bal = __ballot(c);
+        if (bal == 0) continue;
+        if (c) {
+            const uint32_t p = qn + __popcll(bal & lanemask_lt());
+            sh_h[w][p] = h;
+            sh_k[w][p] = key;
+            sh_i[w][p] = (uint32_t)idx;
+        }
+        qn += (uint32_t)__popcll(bal);
+        if (qn >= 64) {
+            qn -= 64;
+            __builtin_amdgcn_wave_barrier();
+            write64(qn, 64);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (qn) write64(0, qn);
+}
+
 template <typename KeyT, int HASH>
 __global__ __launch_bounds__(kBlock) void sample_hash_kernel(const KeyT* __restrict__ keys,
                                                              const int64_t* __restrict__ hashes,
@@ -224,6 +277,127 @@ inline unsigned grid_1d(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 
 }  // namespace
 
+// Exact host replica of the reference's RandomValues state (Sampler.scala:389-409): a 1-indexed
+// binary max-heap on the hash with scala 2.13 mutable.PriorityQueue's fixUp / fixDown tie behaviour
+// (addOne: sift up while parent < child; dequeue: last to the root, sift down to the larger child,
+// left on ties, stop when parent >= child), an open-addressing element set, and maxHash.  Used by
+// RSV_DISTINCT_ORDERED, which replays the GPU-filtered survivors of each chunk in arrival order.
+// (Product implementation; the oracle under oracle/ is an independent restatement for the tests.)
+struct HostValues {
+    struct Ent {
+        int64_t elem, h;
+    };
+    struct Slot {  // one cache access per probe: key and occupancy side by side
+        int64_t key;
+        int64_t used;
+    };
+    int64_t k = 0;
+    // heap as two arrays (index 0 unused): the sift loops compare hashes only
+    std::vector<int64_t> hh{0}, he{0};
+    int64_t max_hash = INT64_MIN;  // Sampler.scala:392
+    std::vector<Slot> slots;
+    uint64_t mask = 0;
+
+    int64_t size() const { return (int64_t)hh.size() - 1; }
+    static uint64_t mix(int64_t v) {
+        uint64_t z = (uint64_t)v * 0x9E3779B97F4A7C15ull;
+        return z ^ (z >> 29);
+    }
+    void set_reserve(int64_t n) {
+        uint64_t cap = 16;
+        while (cap < 2 * (uint64_t)n + 2) cap <<= 1;
+        if (cap <= mask + 1 && !slots.empty()) return;
+        std::vector<Slot> old;
+        old.swap(slots);
+        slots.assign(cap, Slot{0, 0});
+        mask = cap - 1;
+        for (const Slot& x : old)
+            if (x.used) set_add(x.key);
+    }
+    bool contains(int64_t v) const {
+        for (uint64_t q = mix(v) & mask;; q = (q + 1) & mask) {
+            if (!slots[q].used) return false;
+            if (slots[q].key == v) return true;
+        }
+    }
+    void set_add(int64_t v) {
+        uint64_t q = mix(v) & mask;
+        while (slots[q].used) q = (q + 1) & mask;
+        slots[q] = Slot{v, 1};
+    }
+    void set_remove(int64_t v) {
+        uint64_t p = mix(v) & mask;
+        while (!slots[p].used || slots[p].key != v) p = (p + 1) & mask;
+        slots[p].used = 0;
+        for (uint64_t q = (p + 1) & mask; slots[q].used; q = (q + 1) & mask) {  // backward-shift deletion
+            const uint64_t home = mix(slots[q].key) & mask;
+            const bool move = p <= q ? (home <= p || home > q) : (home <= p && home > q);
+            if (move) {
+                slots[p] = slots[q];
+                slots[q].used = 0;
+                p = q;
+            }
+        }
+    }
+    void pq_add(int64_t elem, int64_t h) {
+        hh.push_back(h);
+        he.push_back(elem);
+        size_t m = hh.size() - 1;
+        while (m > 1 && hh[m / 2] < h) {  // fixUp: parent < child -> swap
+            hh[m] = hh[m / 2];
+            he[m] = he[m / 2];
+            m /= 2;
+        }
+        hh[m] = h;
+        he[m] = elem;
+    }
+    int64_t pq_dequeue() {  // returns the removed element
+        const int64_t res = he[1];
+        const int64_t h = hh.back(), e = he.back();
+        hh.pop_back();
+        he.pop_back();
+        const int64_t n = size();
+        if (n == 0) return res;
+        int64_t kk = 1;
+        while (n >= 2 * kk) {  // fixDown: larger child (left on ties); stop when parent >= child
+            int64_t j = 2 * kk;
+            if (j < n && hh[j] < hh[j + 1]) ++j;
+            if (h >= hh[j]) break;
+            hh[kk] = hh[j];
+            he[kk] = he[j];
+            kk = j;
+        }
+        hh[kk] = h;
+        he[kk] = e;
+        return res;
+    }
+    // RandomValues.sample for one element whose scrambled hash is h (Sampler.scala:394-409)
+    void sample(int64_t elem, int64_t h) {
+        if (size() < k) {
+            if (!contains(elem)) {
+                if (size() + 1 > (int64_t)(mask + 1) / 2 - 1) set_reserve(2 * size() + 2);
+                pq_add(elem, h);
+                set_add(elem);
+                if (h > max_hash) max_hash = h;
+            }
+        } else if (h < max_hash && !contains(elem)) {
+            set_remove(pq_dequeue());
+            pq_add(elem, h);
+            set_add(elem);
+            max_hash = hh[1];
+        }
+    }
+    void reset(int64_t kk) {
+        k = kk;
+        hh.assign(1, 0);
+        he.assign(1, 0);
+        max_hash = INT64_MIN;
+        slots.clear();
+        mask = 0;
+        set_reserve(std::min<int64_t>(kk, 1 << 16));
+    }
+};
+
 struct DistinctState {
     int32_t k = 0;
     int kw = 8;
@@ -250,6 +424,17 @@ struct DistinctState {
     int64_t* h_pinned = nullptr;  // host scalars
     std::vector<int64_t> samp_host;
     KernelTimer* timer = nullptr;
+    // RSV_DISTINCT_ORDERED: exact host replica of RandomValues + chunk buffers
+    bool ordered = false;
+    HostValues rep;
+    int64_t seen = 0;               // elements sampled so far (chunk sizing)
+    uint32_t* cand_i = nullptr;     // [cand_cap] chunk-relative index of each candidate
+    uint32_t* perm = nullptr;       // [cand_cap] candidate slots in arrival order
+    uint32_t* sorted_i = nullptr;   // [cand_cap] radix-sort key output
+    int64_t ord_cap = 0;            // capacity of the three buffers above and of the pinned copies
+    int64_t* ph = nullptr;          // pinned: hashes, keys (as KeyT), perm of one chunk
+    void* pk = nullptr;
+    uint32_t* pp = nullptr;
 };
 
 void distinct_set_timer(DistinctState* d, KernelTimer* t) { d->timer = t; }
@@ -334,9 +519,11 @@ static hipError_t ensure_caps(DistinctState* d, int64_t cand_need, int64_t merge
     return hipSuccess;
 }
 
-DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t r0, int64_t r1,
+DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t r0, int64_t r1, bool ordered,
                                int* status) {
     DistinctState* d = new DistinctState();
+    d->ordered = ordered;
+    if (ordered) d->rep.reset(k);
     d->k = k;
     d->kw = key_width;
     d->hash_kind = hash_kind;
@@ -375,9 +562,12 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
 void distinct_destroy(DistinctState* d) {
     if (!d) return;
     void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->counter, d->mh0, d->mh1, d->mk0,
-                  d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp};
+                  d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp, d->cand_i, d->perm, d->sorted_i};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
     pool_host_free(d->h_pinned);
+    pool_host_free(d->ph);
+    pool_host_free(d->pk);
+    pool_host_free(d->pp);
     delete d;
 }
 
@@ -576,8 +766,161 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
 #undef DTRY
 }
 
+template <typename KeyT>
+static hipError_t launch_filter_idx(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
+                                    int64_t tinc, hipStream_t st) {
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n), 1), 256 * 8);
+    KeyT* ck = (KeyT*)d->cand_k;
+#define RSV_FILTER_IDX(H)                                                                                 \
+    hipLaunchKernelGGL((k3_filter_idx<KeyT, H>), dim3(grid), dim3(kBlock), 0, st, keys, hashes, n, d->r0, \
+                       d->r1, tinc, d->cand_h, ck, d->cand_i, d->counter, d->ord_cap)
+    switch (d->hash_kind) {
+    case kHashJavaLong: RSV_FILTER_IDX(kHashJavaLong); break;
+    case kHashJavaInt: RSV_FILTER_IDX(kHashJavaInt); break;
+    case kHashPrecomputed: RSV_FILTER_IDX(kHashPrecomputed); break;
+    default: RSV_FILTER_IDX(kHashIdentity);
+    }
+#undef RSV_FILTER_IDX
+    return hipGetLastError();
+}
+
+// ordered-mode buffers: device candidate index / permutation / sort output and pinned host copies
+static hipError_t ensure_ordered(DistinctState* d, int64_t cap, hipStream_t st) {
+    if (cap <= d->ord_cap) return hipSuccess;
+    hipError_t e;
+    if ((e = grow((void**)&d->cand_i, 0, (size_t)cap * 4, false, st))) return e;
+    if ((e = grow((void**)&d->perm, 0, (size_t)cap * 4, false, st))) return e;
+    if ((e = grow((void**)&d->sorted_i, 0, (size_t)cap * 4, false, st))) return e;
+    pool_host_free(d->ph);
+    pool_host_free(d->pk);
+    pool_host_free(d->pp);
+    d->ph = nullptr;
+    d->pk = nullptr;
+    d->pp = nullptr;
+    if ((e = pool_host_alloc((void**)&d->ph, (size_t)cap * 8, hipHostMallocDefault))) return e;
+    if ((e = pool_host_alloc(&d->pk, (size_t)cap * d->kw, hipHostMallocDefault))) return e;
+    if ((e = pool_host_alloc((void**)&d->pp, (size_t)cap * 4, hipHostMallocDefault))) return e;
+    size_t tb = 0;
+    if ((e = rocprim::radix_sort_pairs(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                       rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (size_t)cap)))
+        return e;
+    if (tb > d->temp_bytes) {
+        if ((e = grow(&d->temp, 0, tb, false, st))) return e;
+        d->temp_bytes = tb;
+    }
+    d->ord_cap = cap;
+    return hipSuccess;
+}
+
+// The replica's set -> the device set arrays (ascending (h, key), as the SET mode keeps them), so
+// result / export / merge read the same place in both modes.
+template <typename KeyT>
+static hipError_t upload_replica(DistinctState* d, hipStream_t st) {
+    std::vector<HostValues::Ent> es;
+    for (int64_t i = 1; i <= d->rep.size(); ++i) es.push_back(HostValues::Ent{d->rep.he[(size_t)i], d->rep.hh[(size_t)i]});
+    std::sort(es.begin(), es.end(), [](const HostValues::Ent& a, const HostValues::Ent& b) {
+        return a.h != b.h ? a.h < b.h : a.elem < b.elem;
+    });
+    const int64_t m = (int64_t)es.size();
+    hipError_t e = ensure_caps(d, 0, m, st);
+    if (e != hipSuccess || m == 0) {
+        d->m = 0;
+        return e;
+    }
+    std::vector<int64_t> hh((size_t)m);
+    std::vector<KeyT> kk((size_t)m);
+    for (int64_t i = 0; i < m; ++i) {
+        hh[(size_t)i] = es[(size_t)i].h;
+        kk[(size_t)i] = (KeyT)es[(size_t)i].elem;
+    }
+    if ((e = hipMemcpyAsync(d->set_h, hh.data(), (size_t)m * 8, hipMemcpyHostToDevice, st))) return e;
+    if ((e = hipMemcpyAsync(d->set_k, kk.data(), (size_t)m * sizeof(KeyT), hipMemcpyHostToDevice, st))) return e;
+    if ((e = hipStreamSynchronize(st))) return e;  // the host vectors go out of scope
+    d->m = m;
+    d->max_h = d->rep.max_hash;
+    return hipSuccess;
+}
+
+// RSV_DISTINCT_ORDERED: the batch in chunks.  For each chunk the GPU keeps the elements the
+// reference could insert -- all of them while the heap is not full, else h < maxHash (a superset:
+// maxHash only falls within the chunk) -- with their positions; a radix sort by position restores
+// arrival order and the host replica replays them.  Elements the filter drops are exactly ones the
+// reference rejects at `elemHash < maxHash` (Sampler.scala:403), so the replica's state equals the
+// reference's after every chunk.  Chunks double with the stream (expected survivors ~k each).
+template <typename KeyT>
+static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
+                               hipStream_t st) {
+#define OTRY(x)                                                                               \
+    do {                                                                                      \
+        hipError_t _e = (x);                                                                  \
+        if (_e != hipSuccess) {                                                               \
+            set_error(std::string("distinct (ordered): " #x ": ") + hipGetErrorString(_e));   \
+            return _e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;            \
+        }                                                                                     \
+    } while (0)
+    HostValues& rep = d->rep;
+    const int64_t k = d->k;
+    const int64_t cap = std::min<int64_t>(d->cand_limit, std::max<int64_t>(4096, 2 * std::min<int64_t>(n, d->cand_limit)));
+    OTRY(ensure_caps(d, cap, 0, st));
+    OTRY(ensure_ordered(d, d->cand_cap, st));
+    const int64_t ocap = d->ord_cap;
+    int64_t pos = 0;
+    int64_t m_next = 0;  // chunk length after an overflow retry
+    while (pos < n) {
+        const bool full = rep.size() == k;
+        if (full && rep.max_hash == INT64_MIN) break;  // nothing is < Long.MinValue
+        const int64_t tinc = full ? rep.max_hash - 1 : INT64_MAX;
+        int64_t m;
+        if (m_next) {
+            m = m_next;
+        } else if (!full) {
+            m = std::max<int64_t>(1024, 2 * (k - rep.size()) + 1024);  // all survive: bounded by the buffer
+        } else {
+            m = std::max<int64_t>(d->seen, 65536);
+        }
+        m = std::min(std::min(m, n - pos), std::min<int64_t>(full ? ((int64_t)1 << 31) : ocap, (int64_t)1 << 31));
+        OTRY(hipMemsetAsync(d->counter, 0, 8, st));
+        if (d->timer) d->timer->mark(st);
+        OTRY(launch_filter_idx<KeyT>(d, keys + pos, hashes ? hashes + pos : nullptr, m, tinc, st));
+        if (d->timer) d->timer->mark(st);
+        OTRY(hipMemcpyAsync(d->h_pinned + 2, d->counter, 8, hipMemcpyDeviceToHost, st));
+        OTRY(hipStreamSynchronize(st));
+        const int64_t c = d->h_pinned[2];
+        if (c > ocap) {  // repeats of members (or a degenerate hash) overflowed the buffer: shorter chunk
+            m_next = std::max<int64_t>(1, (int64_t)((double)m * ocap / (double)c / 2));
+            continue;
+        }
+        m_next = 0;
+        if (c > 0) {
+            unsigned bits = 1;
+            while (bits < 32 && ((uint64_t)1 << bits) < (uint64_t)m) ++bits;
+            size_t tb = d->temp_bytes;
+            OTRY(rocprim::radix_sort_pairs(d->temp, tb, d->cand_i, d->sorted_i, rocprim::counting_iterator<uint32_t>(0),
+                                           d->perm, (size_t)c, 0, bits, st));
+            OTRY(hipMemcpyAsync(d->pp, d->perm, (size_t)c * 4, hipMemcpyDeviceToHost, st));
+            OTRY(hipMemcpyAsync(d->ph, d->cand_h, (size_t)c * 8, hipMemcpyDeviceToHost, st));
+            OTRY(hipMemcpyAsync(d->pk, d->cand_k, (size_t)c * sizeof(KeyT), hipMemcpyDeviceToHost, st));
+            OTRY(hipStreamSynchronize(st));
+            const KeyT* pk = (const KeyT*)d->pk;
+            for (int64_t t = 0; t < c; ++t) {
+                const uint32_t q = d->pp[t];
+                rep.sample((int64_t)pk[q], d->ph[q]);
+            }
+        }
+        pos += m;
+        d->seen += m;
+    }
+    d->seen += n - pos;  // the rest was rejected wholesale (maxHash == Long.MinValue)
+    OTRY(upload_replica<KeyT>(d, st));
+    return RSV_OK;
+#undef OTRY
+}
+
 int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* hashes, int64_t n,
                            hipStream_t st) {
+    if (d->ordered)
+        return d->kw == 8 ? ordered_sample_impl<int64_t>(d, (const int64_t*)keys, hashes, n, st)
+                          : ordered_sample_impl<int32_t>(d, (const int32_t*)keys, hashes, n, st);
     return d->kw == 8 ? sample_impl<int64_t>(d, (const int64_t*)keys, hashes, n, st)
                       : sample_impl<int32_t>(d, (const int32_t*)keys, hashes, n, st);
 }
@@ -603,6 +946,24 @@ int distinct_merge(DistinctState* d, const void* keys_dev, const int64_t* hash_d
             return RSV_E_DEVICE;
         }
         off += c;
+    }
+    if (d->ordered && n > 0) {
+        // a merged (multi-GPU) set has no single arrival order: rebuild the replica from the
+        // bottom-k union, inserting in ascending (h, key) order
+        std::vector<int64_t> hh((size_t)d->m), kk((size_t)d->m);
+        std::vector<int32_t> k4(d->kw == 4 ? (size_t)d->m : 0);
+        hipError_t e = hipMemcpyAsync(hh.data(), d->set_h, (size_t)d->m * 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d->kw == 8 ? (void*)kk.data() : (void*)k4.data(), d->set_k, (size_t)d->m * d->kw,
+                               hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            set_error(std::string("distinct_merge: ") + hipGetErrorString(e));
+            return RSV_E_DEVICE;
+        }
+        d->rep.reset(d->k);
+        for (int64_t i = 0; i < d->m; ++i) d->rep.sample(d->kw == 8 ? kk[(size_t)i] : (int64_t)k4[(size_t)i], hh[(size_t)i]);
+        d->max_h = d->rep.max_hash;
     }
     return RSV_OK;
 }

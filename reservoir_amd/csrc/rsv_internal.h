@@ -119,7 +119,8 @@ hipError_t launch_merge_packed(const int64_t* rows, int32_t parts, int64_t strid
 
 // ---- distinct (bottom-k over the scrambled hash) --------------------------------------------
 struct DistinctState;  // defined in rsv_distinct.hip
-DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t r0, int64_t r1,
+// ordered: RSV_DISTINCT_ORDERED semantics (exact sequential replay; see rsv_distinct.hip)
+DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t r0, int64_t r1, bool ordered,
                                int* status);
 void distinct_set_timer(DistinctState* d, KernelTimer* t);
 void distinct_destroy(DistinctState* d);

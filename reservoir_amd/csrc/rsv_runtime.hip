@@ -449,6 +449,8 @@ rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out) {
         return fail(RSV_E_ILLEGAL_ARGUMENT, "unknown engine");
     if (cfg->hash_kind < RSV_HASH_DEFAULT || cfg->hash_kind > RSV_HASH_PRECOMPUTED)
         return fail(RSV_E_ILLEGAL_ARGUMENT, "unknown hash kind");
+    if (cfg->distinct_order < RSV_DISTINCT_AUTO || cfg->distinct_order > RSV_DISTINCT_ORDERED)
+        return fail(RSV_E_ILLEGAL_ARGUMENT, "unknown distinct order");
 
     rsv_sampler* s = new rsv_sampler();
     s->cfg = *cfg;
@@ -490,7 +492,13 @@ rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out) {
         const int64_t r0 = r.next_long(), r1 = r.next_long();
         s->hash_kind = resolve_hash_kind(cfg->hash_kind, s->kw);
         int st = RSV_OK;
-        s->distinct = distinct_create((int32_t)s->k, s->kw, s->hash_kind, r0, r1, &st);
+        bool ordered;
+        switch (cfg->distinct_order) {
+        case RSV_DISTINCT_SET: ordered = false; break;
+        case RSV_DISTINCT_ORDERED: ordered = true; break;
+        default: ordered = s->hash_kind == kHashJavaLong || s->hash_kind == kHashPrecomputed;  // may collide
+        }
+        s->distinct = distinct_create((int32_t)s->k, s->kw, s->hash_kind, r0, r1, ordered, &st);
         if (!s->distinct) {
             std::string msg = g_last_error;
             return bail((rsv_status)st, msg);

@@ -23,6 +23,9 @@ Extensions (keyword-only, defaulted so reference-style calls are unchanged):
     seed      RNG seed (default: fresh entropy, like ``new Random()`` at Sampler.scala:199)
     stream_id Philox stream of a "philox_r" sampler
     device    HIP device ordinal (default: current device)
+    order     distinct only: "auto" (default), "set" or "ordered" -- how hash ties are resolved
+              (include/reservoir_hip.h rsv_distinct_order): "ordered" reproduces the reference's
+              sequential heap for any hash, "set" is the order-independent bottom-k by (hash, key)
 """
 from __future__ import annotations
 
@@ -44,6 +47,7 @@ def identity(x):
 
 _KEY = {"long": (8, np.int64), "int": (4, np.int32)}
 _ENGINE = {"philox_r": N.ENGINE_PHILOX_R, "java_l": N.ENGINE_JAVA_L}
+_ORDER = {"auto": N.DISTINCT_AUTO, "set": N.DISTINCT_SET, "ordered": N.DISTINCT_ORDERED}
 
 
 def _fresh_seed() -> int:
@@ -79,11 +83,13 @@ class GpuSampler:
     def __init__(self, kind: int, max_sample_size: int, map_fn: Callable, *, reusable: bool,
                  pre_allocate: bool = False, hash_fn=None, hash_kind: int = N.HASH_DEFAULT,
                  key_type: str = "long", engine: str = "philox_r", seed: int | None = None,
-                 stream_id: int = 0, device: int | None = None):
+                 stream_id: int = 0, device: int | None = None, order: str = "auto"):
         if key_type not in _KEY:
             raise IllegalArgumentException(f"key_type must be one of {sorted(_KEY)}")
         if engine not in _ENGINE:
             raise IllegalArgumentException(f"engine must be one of {sorted(_ENGINE)}")
+        if order not in _ORDER:
+            raise IllegalArgumentException(f"order must be one of {sorted(_ORDER)}")
         self._L = N.load()
         self._map = map_fn
         self._hash_fn = hash_fn
@@ -99,6 +105,7 @@ class GpuSampler:
         cfg.pre_allocate = 1 if pre_allocate else 0
         cfg.engine = _ENGINE[engine]
         cfg.hash_kind = hash_kind
+        cfg.distinct_order = _ORDER[order]
         cfg.device = -1 if device is None else int(device)
         cfg.seed = (_fresh_seed() if seed is None else int(seed)) & (2**64 - 1)
         cfg.stream_id = int(stream_id) & (2**64 - 1)

@@ -2,8 +2,10 @@
 
 Parity contract P3: with an injective hash the GPU set equals the oracle's RandomValues set
 bit-exactly (compared as sets; the reference's order is HashSet order).  With a colliding hash
-(the default Long.hashCode) every element whose scrambled hash is below the final maximum is
-kept by both; only the tie bucket at the maximum is order-dependent (parity unpinned there).
+(the default Long.hashCode) the default order "auto" -> RSV_DISTINCT_ORDERED replays the reference's
+heap, so the set is bit-exact too, tie bucket at the maximum included (against the oracle's
+scala-PriorityQueue restatement; the library source itself is not in the image).  order="set"
+keeps the order-independent bottom-k by (hash, key): everything below the maximum agrees.
 """
 import json
 import os
@@ -26,13 +28,7 @@ def test_golden_distinct(cuda, oracle, case):
     d.sample_all(np.array(case["values"], dtype=np.int64))
     got = d.result().tolist()
     want = case["result_sorted_by_hash"]
-    if case["hash_kind"] == oracle.HASH_JAVA_LONG:
-        # only the part strictly below the max is order-free
-        hs = dict(zip(case["result_sorted_by_hash"], case["hashes"]))
-        M = max(case["hashes"])
-        assert {v for v in want if hs[v] < M} <= set(got) and len(got) == len(want)
-    else:
-        assert got == want  # GPU order: ascending scrambled hash, as the oracle sorts
+    assert got == want  # GPU order: ascending (scrambled hash, key), as the oracle sorts
 
 
 @pytest.mark.parametrize("k", [1, 10, 1000, 65_536])
@@ -71,6 +67,7 @@ def test_int_default_hash_and_per_element(cuda, oracle):
 
 
 def test_default_long_hash_below_max(cuda, oracle):
+    """order="set": the bottom-k by (hash, key) keeps everything below the reference's maximum."""
     from reservoir_amd import Sampler
 
     rng = np.random.default_rng(1)
@@ -79,12 +76,120 @@ def test_default_long_hash_below_max(cuda, oracle):
     ref = oracle.Distinct(500, 4, oracle.HASH_JAVA_LONG)
     ref.sample_all(vals)
     wk, wh = ref.result()
-    d = Sampler.distinct(500, seed=4)()  # default hash = Long.hashCode (Sampler.scala:75)
+    d = Sampler.distinct(500, seed=4, order="set")()  # default hash = Long.hashCode (Sampler.scala:75)
     d.sample_all(vals)
     got = set(d.result().tolist())
     M = wh.max()
     assert len(got) == 500
     assert {int(x) for x, h in zip(wk, wh) if h < M} <= got
+
+
+def _colliding(rng, n, buckets):
+    """Long keys whose Long.hashCode (hi ^ lo) takes only `buckets` values: every hash bucket holds
+    many distinct elements, so the reference's boundary bucket is always tied."""
+    hi = rng.integers(0, 2**31, size=n, dtype=np.int64)
+    lo = (hi ^ rng.integers(0, buckets, size=n, dtype=np.int64)) & 0xFFFFFFFF
+    return (hi << 32) | lo
+
+
+@pytest.mark.parametrize("k,n,buckets", [(1, 10_000, 50), (20, 50_000, 200), (500, 400_000, 3000),
+                                         (4096, 2_000_000, 20_000), (3000, 30_000, 100_000)])
+def test_default_long_hash_ordered_exact(cuda, oracle, k, n, buckets):
+    """Default hash (Long.hashCode, colliding): bit-exact set vs the sequential reference, ties included."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    rng = np.random.default_rng(k + buckets)
+    vals = _colliding(rng, n, buckets)
+    vals = np.concatenate([vals, vals[: n // 3]])  # repeats of earlier elements
+    ref = oracle.Distinct(k, 8, oracle.HASH_JAVA_LONG)
+    ref.sample_all(vals)
+    wk, wh = ref.result()
+    assert (wh == wh.max()).sum() >= 1
+    d = Sampler.distinct(k, seed=8)()  # order "auto" -> ordered for Long.hashCode
+    d.sample_all(torch.from_numpy(vals).to(cuda))
+    assert d.result().tolist() == wk.tolist()
+    s = Sampler.distinct(k, seed=8, order="set")()
+    s.sample_all(torch.from_numpy(vals).to(cuda))
+    got = s.result()
+    assert got.size == wk.size
+
+
+def test_ordered_batching_invariance(cuda, oracle):
+    """sample == sampleAll == any chunking, host or device memory, in the ordered mode."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    rng = np.random.default_rng(12)
+    vals = np.concatenate([_colliding(rng, 300_000, 2000)] * 2)
+    ref = oracle.Distinct(300, 21, oracle.HASH_JAVA_LONG)
+    ref.sample_all(vals)
+    want = ref.result()[0].tolist()
+    cuts = np.r_[0, np.sort(rng.choice(np.arange(1, vals.size), 15, replace=False)), vals.size]
+    dd = Sampler.distinct(300, seed=21)()
+    dh = Sampler.distinct(300, seed=21)()
+    de = Sampler.distinct(300, seed=21)()
+    kd = torch.from_numpy(vals).to(cuda)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        dd.sample_all(kd[a:b])
+        dh.sample_all(vals[a:b])
+    for x in vals[:5000]:
+        de.sample(int(x))
+    de.sample_all(vals[5000:])
+    assert dd.result().tolist() == want
+    assert dh.result().tolist() == want
+    assert de.result().tolist() == want
+
+
+def test_ordered_forced_on_injective_and_int(cuda, oracle):
+    """order="ordered" with injective hashes equals the bottom-k (and the oracle)."""
+    from reservoir_amd import Sampler
+
+    rng = np.random.default_rng(3)
+    vals = rng.integers(-2**63, 2**63 - 1, size=500_000, dtype=np.int64)
+    vals = np.concatenate([vals, vals[:100_000]])
+    ref = oracle.Distinct(1000, 5, oracle.HASH_IDENTITY)
+    ref.sample_all(vals)
+    d = Sampler.distinct(1000, seed=5, order="ordered")(hash="identity")
+    d.sample_all(vals)
+    assert d.result().tolist() == ref.result()[0].tolist()
+    xs = rng.integers(-2**31, 2**31 - 1, size=100_000).astype(np.int32)
+    ref = oracle.Distinct(77, 6, oracle.HASH_JAVA_INT)
+    ref.sample_all(xs.astype(np.int64))
+    d = Sampler.distinct(77, seed=6, key_type="int", order="ordered")()
+    d.sample_all(xs)
+    assert d.result().astype(np.int64).tolist() == ref.result()[0].tolist()
+
+
+def test_ordered_reusable_and_merge(cuda, oracle):
+    """Reusable ordered sampler: result() between batches is non-destructive; the multi-GPU merge
+    of ordered shards is the bottom-k by (hash, key) of the union, like order="set"."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    rng = np.random.default_rng(9)
+    vals = _colliding(rng, 200_000, 5000)
+    ref = oracle.Distinct(256, 2, oracle.HASH_JAVA_LONG)
+    d = Sampler.distinct(256, seed=2, reusable=True)()
+    for part in np.array_split(vals, 4):
+        d.sample_all(part)
+        ref.sample_all(part)
+        assert d.result().tolist() == ref.result()[0].tolist()
+    parts = []
+    for chunk in np.array_split(vals, 3):
+        e = Sampler.distinct(256, seed=2)()
+        e.sample_all(torch.from_numpy(chunk).to(cuda))
+        parts.append(e.export_state(cuda))
+    outs = []
+    for order in ("ordered", "set"):
+        m = Sampler.distinct(256, seed=2, order=order)()
+        m.merge_state(torch.zeros((3, 256), dtype=torch.int64, device=cuda), torch.stack([p[1] for p in parts]),
+                      torch.stack([p[2] for p in parts]), [p[3] for p in parts], vals.size)
+        outs.append(m.result().tolist())
+    assert outs[0] == outs[1] and len(outs[0]) == 256
 
 
 def test_precomputed_hash(cuda, oracle):
