@@ -37,10 +37,11 @@ __device__ __forceinline__ uint32_t candidate_mask16(const u32x4& w, uint64_t i0
     // T = ceil(dense_lim / (i0+1)): the fp32 estimate is within a few units; correct it exactly
     const float Tf = __fdividef((float)dense_lim, (float)(i0 + 1));
     if (Tf > 300.0f) return 0xFFFFu;  // T > 256: every byte qualifies
-    uint64_t T = (uint64_t)Tf;
-    while (T * (i0 + 1) < dense_lim) ++T;
-    while (T > 0 && (T - 1) * (i0 + 1) >= dense_lim) --T;
-    return lt_mask16(w, T > 256 ? 256u : (uint32_t)T);
+    // Tf <= 300: its error is far below one unit, so one step each way makes T exact
+    uint32_t T = (uint32_t)Tf;
+    if ((uint64_t)T * (i0 + 1) < dense_lim) ++T;
+    if (T > 0 && (uint64_t)(T - 1) * (i0 + 1) >= dense_lim) --T;
+    return lt_mask16(w, T > 256u ? 256u : T);
 }
 
 // Evaluate queue entry q[pos] (level 1) and report a hit (j < k) to `hit(j, i)`.

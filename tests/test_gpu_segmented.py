@@ -27,6 +27,24 @@ def test_ragged_parity(cuda, oracle, k):
     assert np.array_equal(out.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("k", [2, 7, 64])
+def test_long_streams_sparse_region(cuda, oracle, k):
+    """Streams far longer than 256k: the dense head and the sparse tail (zero level-0 bytes only)."""
+    import torch
+
+    from reservoir_amd import batch
+
+    rng = np.random.default_rng(100 + k)
+    lens = np.r_[rng.integers(0, 300_000, size=12), 256 * k - 1, 256 * k, 256 * k + 17, 1_000_003]
+    offs = np.r_[0, np.cumsum(lens)].astype(np.int64)
+    keys = oracle.splitmix_keys(3 * k, int(offs[-1]))
+    want, wcnt = oracle.algo_r_segmented(5, 2**40 + 3, k, keys, offs)
+    out, cnt = batch.sample_segmented(torch.from_numpy(keys).to(cuda), torch.from_numpy(offs).to(cuda), k,
+                                      seed=5, stream_base=2**40 + 3)
+    assert np.array_equal(cnt.cpu().numpy(), wcnt)
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
 def test_int32_keys(cuda, oracle):
     import torch
 
