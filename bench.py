@@ -146,46 +146,49 @@ def main() -> None:
     L = _native.load()
     prof = [0.0, 0]  # K1 milliseconds, launches (timed steps)
 
-    def step(timed: bool):
+    def step():
         # a fresh Sampler per step (Sampler.apply): creation and close are inside the step
         s = Sampler(k, seed=args.seed, stream_id=args.stream_id, device=local)()
         s.set_stream(stream)
-        if timed:
-            _native.check(L.rsv_profile_enable(s.handle, 1))
         s.seek(offset)
         s.sample_all(keys)
         if world > 1:
             D.combine(s, device=dev, total_count=n * world)
         r = s.result()
-        if timed:  # HIP events already complete (result() waited for the stream)
-            ms, cnt = C.c_double(), C.c_int64()
-            _native.check(L.rsv_profile_read(s.handle, C.byref(ms), C.byref(cnt)))
-            prof[0] += ms.value
-            prof[1] += cnt.value
         s.close()
         return r
+
+    def profile_read():
+        ms, cnt = C.c_double(), C.c_int64()
+        _native.check(L.rsv_profile_global_read(C.byref(ms), C.byref(cnt)))
+        return ms.value, cnt.value
 
     # Device warm-up (untimed): under sustained load the K1 launch time falls from ~152 to ~140 us
     # over the first ~30 ms as clocks ramp (rocprofv3 trace); run steps for 0.2 s
     # before the W warmup steps so the timed region sees the steady state.
     t_w = time.perf_counter()
     while time.perf_counter() - t_w < 0.2:
-        step(False)
+        step()
     for _ in range(args.warmup):
-        step(False)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # K1 timing: HIP events around every K1 launch of the timed steps (process-wide list, drained
+    # after the timed region; rsv_profile_global in include/reservoir_hip.h)
+    _native.check(L.rsv_profile_global(1))
     t0 = time.perf_counter()
     res = None
     for _ in range(args.steps):
-        res = step(True)
+        res = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    _native.check(L.rsv_profile_global(0))
+    prof[0], prof[1] = profile_read()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

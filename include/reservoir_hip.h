@@ -145,6 +145,12 @@ rsv_status rsv_synchronize(rsv_sampler* s);
  * rsv_profile_read synchronizes and returns the summed kernel time and the launch count. */
 rsv_status rsv_profile_enable(rsv_sampler* s, int32_t on);
 rsv_status rsv_profile_read(rsv_sampler* s, double* total_ms, int64_t* launches);
+/* Process-wide form (bench.py): while on, the hot-kernel launches of every ELEMENTS handle without
+ * its own timing are bracketed by events kept in one process-wide list, so a timed loop that creates and
+ * closes samplers pays no per-handle enable/read; rsv_profile_global_read synchronizes those events,
+ * returns the totals since the last read and starts a new window. */
+rsv_status rsv_profile_global(int32_t on);
+rsv_status rsv_profile_global_read(double* total_ms, int64_t* launches);
 
 /* ---- Multi-GPU (index-range split of one stream; RSV_ENGINE_PHILOX_R / DISTINCT) ---------- */
 /* Declare that the next sampled element has global index `index` (>= count): the elements in

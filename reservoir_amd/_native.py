@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = (
     "rsv_is_open", "rsv_count", "rsv_set_stream", "rsv_get_stream", "rsv_synchronize", "rsv_seek",
     "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
     "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
-    "rsv_merge_packed",
+    "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read",
 )
 
 
@@ -110,11 +110,13 @@ def load():
     L.rsv_export_draws.argtypes = [u64, u64, u64, i64, vp, vp]
     L.rsv_profile_enable.argtypes = [vp, i32]
     L.rsv_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(i64)]
+    L.rsv_profile_global.argtypes = [i32]
+    L.rsv_profile_global_read.argtypes = [C.POINTER(C.c_double), C.POINTER(i64)]
     for name in ("rsv_config_init", "rsv_create", "rsv_sample", "rsv_sample_batch", "rsv_result",
                  "rsv_result_device", "rsv_set_stream", "rsv_synchronize", "rsv_seek",
                  "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
                  "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
-                 "rsv_merge_packed"):
+                 "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read"):
         getattr(L, name).restype = i32
     if L.rsv_abi_version() != 1:
         raise ImportError("libreservoir_hip.so ABI version mismatch")

@@ -152,9 +152,42 @@ struct rsv_sampler {
     uint32_t pub_gen = 0;
     bool pub_valid = false;
     KernelTimer timer;
+    // device work enqueued on `stream` by this handle, in groups, vs the groups known complete
+    // (a stream synchronize, or the host flag of a publication that was the last group)
+    uint64_t ops = 0, ops_done = 0, pub_ops = 0;
 };
 
 namespace {
+
+// process-wide hot-kernel timer (rsv_profile_global); guarded by g_prof_mu
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+KernelTimer& global_timer() {
+    static auto* t = new KernelTimer();  // leaked on purpose, like the pool
+    return *t;
+}
+
+// a new group of device work on the handle's stream / everything enqueued so far is complete
+inline void touch(rsv_sampler* s) { ++s->ops; }
+inline hipError_t sync_stream(rsv_sampler* s) {
+    hipError_t e = hipStreamSynchronize(s->stream);
+    if (e == hipSuccess) s->ops_done = s->ops;
+    return e;
+}
+
+// record a timing mark for the handle's hot kernel: its own timer, else the process-wide one
+void prof_mark(rsv_sampler* s, hipStream_t st) {
+    if (s->timer.on) {
+        s->timer.mark(st);
+        return;
+    }
+    if (!g_prof_on) return;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    KernelTimer& t = global_timer();
+    t.on = true;
+    t.device = s->device;
+    t.mark(st);
+}
 
 constexpr int32_t kMaxSize = 2147483647 - 2;  // Sampler.scala:71 (hotspot VM array limit)
 constexpr int64_t kStageKeys = 1 << 20;
@@ -186,7 +219,7 @@ rsv_status check_open(const rsv_sampler* s) {  // SingleUse.checkOpen, Sampler.s
 rsv_status ensure_events(rsv_sampler* s, int64_t n) {
     if (n <= s->ev_cap) return RSV_OK;
     int64_t cap = std::max<int64_t>(n, 2 * s->ev_cap);
-    if (s->ev_pos_d || s->ev_slot_d) RSV_HIP_TRY(hipStreamSynchronize(s->stream));  // before reuse elsewhere
+    if (s->ev_pos_d || s->ev_slot_d) RSV_HIP_TRY(sync_stream(s));  // before reuse elsewhere
     pool_device_free(s->ev_pos_d);
     pool_device_free(s->ev_slot_d);
     s->ev_pos_d = nullptr;
@@ -202,6 +235,7 @@ rsv_status ensure_events(rsv_sampler* s, int64_t n) {
 // handle's current stream before its first use (creation itself enqueues no device work)
 rsv_status ensure_slots(rsv_sampler* s) {
     if (s->slots_init || s->cfg.kind != RSV_KIND_ELEMENTS) return RSV_OK;
+    touch(s);
     RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream));
     s->slots_init = s->win_zero = true;
     s->pub_valid = false;
@@ -278,6 +312,7 @@ rsv_status resolve_batch(rsv_sampler* s, const void* keys, int64_t base, int64_t
             const int64_t m = std::min<int64_t>(base + n, (int64_t)s->k);
             RSV_HIP_TRY(launch_resolve_publish(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx,
                                                fresh, m, s->result_dev, s->result_flag_dev, gen, s->stream));
+            s->pub_ops = s->ops;  // the last work of this group
             s->pub_gen = gen;
             s->pub_valid = true;
             return RSV_OK;
@@ -291,6 +326,7 @@ rsv_status resolve_batch(rsv_sampler* s, const void* keys, int64_t base, int64_t
 // one batch of n keys already in device memory, at global indices [count, count+n)
 rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t* hashes, int64_t n) {
     if (n <= 0) return RSV_OK;
+    touch(s);
     const int64_t base = s->count;
     bool fresh = false;
     if (s->cfg.kind == RSV_KIND_ELEMENTS) {
@@ -313,18 +349,18 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
             if (rsv_status st = ensure_events(s, ne)) return st;
             RSV_HIP_TRY(hipMemcpyAsync(s->ev_pos_d, s->ev_pos_h.data(), ne * 8, hipMemcpyHostToDevice, s->stream));
             RSV_HIP_TRY(hipMemcpyAsync(s->ev_slot_d, s->ev_slot_h.data(), ne * 4, hipMemcpyHostToDevice, s->stream));
-            s->timer.mark(s->stream);
+            prof_mark(s, s->stream);
             RSV_HIP_TRY(launch_replay_events(s->ev_pos_d, s->ev_slot_d, ne, s->k, s->batch_win, s->stream));
-            s->timer.mark(s->stream);
+            prof_mark(s, s->stream);
         }
         if (rsv_status st = resolve_batch(s, keys, base, n, fresh)) return st;
-        if (ne) RSV_HIP_TRY(hipStreamSynchronize(s->stream));  // host event vectors are reused
+        if (ne) RSV_HIP_TRY(sync_stream(s));  // host event vectors are reused
     } else {
         const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
         const uint64_t lo = std::max<uint64_t>((uint64_t)base, s->k), hi = (uint64_t)(base + n);
-        s->timer.mark(s->stream);
+        prof_mark(s, s->stream);
         RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
-        s->timer.mark(s->stream);
+        prof_mark(s, s->stream);
         if (rsv_status st = resolve_batch(s, keys, base, n, fresh)) return st;
     }
     if (s->cfg.kind == RSV_KIND_ELEMENTS) s->slots_init = s->win_zero = true;
@@ -353,7 +389,7 @@ rsv_status process_host_batch(rsv_sampler* s, const void* keys, const int64_t* h
         if (rsv_status st = process_device_batch(s, s->chunk_d, s->chunk_hash_d, c)) return st;
     }
     // the caller may reuse its buffer after return (ownership stays with the caller)
-    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    RSV_HIP_TRY(sync_stream(s));
     return RSV_OK;
 }
 
@@ -512,7 +548,10 @@ rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out) {
 void rsv_destroy(rsv_sampler* s) {
     if (!s) return;
     DeviceGuard g(s->device);
-    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    // the buffers go back to the pool: nothing this handle enqueued may still touch them.  On a
+    // caller stream whose last group of work was a publication the host has seen, that holds
+    // already (the flag store is the last memory operation of that group).
+    if (s->stream && (s->own_stream || s->ops != s->ops_done)) (void)hipStreamSynchronize(s->stream);
     free_all(s);
     delete s;
 }
@@ -580,7 +619,7 @@ static rsv_status wait_flag(rsv_sampler* s, uint32_t gen) {
         __builtin_ia32_pause();
         if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
     }
-    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    RSV_HIP_TRY(sync_stream(s));
     if (__atomic_load_n(s->result_flag, __ATOMIC_ACQUIRE) == gen) return RSV_OK;
     return fail(RSV_E_DEVICE, "result publish flag not set after stream synchronize");
 }
@@ -605,7 +644,7 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
                 RSV_HIP_TRY(hipMalloc(&tmp, m * s->kw));
                 int rc = distinct_export(s->distinct, tmp, nullptr, s->stream);
                 hipError_t e = hipMemcpyAsync(out, tmp, m * s->kw, hipMemcpyDeviceToHost, s->stream);
-                hipError_t e2 = hipStreamSynchronize(s->stream);
+                hipError_t e2 = sync_stream(s);
                 (void)hipFree(tmp);
                 if (rc) return (rsv_status)rc;
                 RSV_HIP_TRY(e);
@@ -619,6 +658,7 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
         if (m && !out) return fail(RSV_E_NULL_POINTER, "out is NULL");
         src = s->slot_key;
         if (m && device_out) {
+            touch(s);
             RSV_HIP_TRY(hipMemcpyAsync(out, src, m * s->kw, hipMemcpyDeviceToDevice, s->stream));
         } else if (m) {
             if (rsv_status st = ensure_result_buffer(s)) return st;
@@ -626,21 +666,25 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
                 uint32_t gen = s->pub_gen;
                 if (!s->pub_valid) {  // the last batch's resolve did not publish the current slots
                     gen = ++s->result_gen;
+                    touch(s);
                     RSV_HIP_TRY(launch_publish(src, m * s->kw, s->result_dev, s->result_flag_dev, gen, s->stream));
+                    s->pub_ops = s->ops;
                     s->pub_gen = gen;
                     s->pub_valid = true;
                 }
                 if (rsv_status st = wait_flag(s, gen)) return st;
+                if (s->pub_valid && s->pub_ops == s->ops && s->result_gen == gen) s->ops_done = s->ops;
                 memcpy(out, s->result_h, (size_t)m * s->kw);
                 *out_n = m;
                 if (!s->cfg.reusable) s->open = false;
                 return RSV_OK;
             }
             // large reservoirs through a pinned buffer: a pageable D2H costs a staged copy
+            touch(s);
             RSV_HIP_TRY(hipMemcpyAsync(s->result_h, src, m * s->kw, hipMemcpyDeviceToHost, s->stream));
         }
     }
-    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    RSV_HIP_TRY(sync_stream(s));
     if (m && !device_out && s->cfg.kind != RSV_KIND_DISTINCT) memcpy(out, s->result_h, (size_t)m * s->kw);
     *out_n = m;
     if (!s->cfg.reusable) s->open = false;  // SingleUse.close, Sampler.scala:188-191, :345-350
@@ -662,7 +706,8 @@ int64_t rsv_count(const rsv_sampler* s) { return s ? s->count + s->stage_n : 0; 
 rsv_status rsv_set_stream(rsv_sampler* s, void* hip_stream) {
     if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
     DeviceGuard g(s->device);
-    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    if (s->ops != s->ops_done) RSV_HIP_TRY(sync_stream(s));  // a fresh handle: none
+    s->ops_done = s->ops;
     if (s->own_stream) pool_release_stream(s->device, s->stream);
     s->stream = (hipStream_t)hip_stream;
     s->own_stream = false;
@@ -674,7 +719,7 @@ void* rsv_get_stream(const rsv_sampler* s) { return s ? (void*)s->stream : nullp
 rsv_status rsv_synchronize(rsv_sampler* s) {
     if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
     DeviceGuard g(s->device);
-    RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    RSV_HIP_TRY(sync_stream(s));
     return RSV_OK;
 }
 
@@ -690,6 +735,25 @@ rsv_status rsv_profile_read(rsv_sampler* s, double* total_ms, int64_t* launches)
     RSV_HIP_TRY(s->timer.drain());
     *total_ms = s->timer.total_ms;
     *launches = s->timer.launches;
+    return RSV_OK;
+}
+
+rsv_status rsv_profile_global(int32_t on) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_on = on != 0;
+    return RSV_OK;
+}
+
+rsv_status rsv_profile_global_read(double* total_ms, int64_t* launches) {
+    if (!total_ms || !launches) return fail(RSV_E_NULL_POINTER, "NULL argument");
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    KernelTimer& t = global_timer();
+    DeviceGuard g(t.device);
+    RSV_HIP_TRY(t.drain());
+    *total_ms = t.total_ms;
+    *launches = t.launches;
+    t.total_ms = 0;
+    t.launches = 0;
     return RSV_OK;
 }
 
@@ -711,6 +775,7 @@ rsv_status rsv_export_state(rsv_sampler* s, int64_t* idx_dev, void* keys_dev, in
     if (rsv_status st = check_open(s)) return st;
     if (!out_n) return fail(RSV_E_NULL_POINTER, "out_n is NULL");
     DeviceGuard g(s->device);
+    touch(s);
     if (rsv_status st = flush_stage(s)) return st;
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
         if (int rc = distinct_export(s->distinct, keys_dev, hash_dev, s->stream)) return (rsv_status)rc;
@@ -724,7 +789,7 @@ rsv_status rsv_export_state(rsv_sampler* s, int64_t* idx_dev, void* keys_dev, in
     }
     // on the handle's private stream the caller cannot order against it: wait; on a caller
     // stream (rsv_set_stream) the copies are stream-ordered for the caller's next work
-    if (s->own_stream) RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    if (s->own_stream) RSV_HIP_TRY(sync_stream(s));
     return RSV_OK;
 }
 
@@ -734,6 +799,7 @@ rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* k
     if (parts < 0 || part_len < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative parts/part_len");
     if (parts > 0 && !keys_dev) return fail(RSV_E_NULL_POINTER, "keys_dev is NULL");
     DeviceGuard g(s->device);
+    touch(s);
     if (rsv_status st = flush_stage(s)) return st;
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
         if (parts > 0 && (!hash_dev || !part_n_host)) return fail(RSV_E_NULL_POINTER, "hash_dev/part_n is NULL");
@@ -752,7 +818,7 @@ rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* k
         s->pub_valid = false;
     }
     if (total_count > s->count) s->count = total_count;
-    if (s->own_stream) RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    if (s->own_stream) RSV_HIP_TRY(sync_stream(s));
     return RSV_OK;
 }
 
@@ -766,10 +832,11 @@ rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev) {
     if (rsv_status st = check_packed(s)) return st;
     if (!row_dev) return fail(RSV_E_NULL_POINTER, "row_dev is NULL");
     DeviceGuard g(s->device);
+    touch(s);
     if (rsv_status st = flush_stage(s)) return st;
     if (rsv_status st = ensure_slots(s)) return st;
     RSV_HIP_TRY(launch_export_packed(s->slot_idx, s->slot_key, s->kw, s->k, row_dev, s->stream));
-    if (s->own_stream) RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    if (s->own_stream) RSV_HIP_TRY(sync_stream(s));
     return RSV_OK;
 }
 
@@ -780,6 +847,7 @@ rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t par
     if (row_stride < 2 * (int64_t)s->k) return fail(RSV_E_ILLEGAL_ARGUMENT, "row_stride < 2k");
     if (parts > 0 && !rows_dev) return fail(RSV_E_NULL_POINTER, "rows_dev is NULL");
     DeviceGuard g(s->device);
+    touch(s);
     if (rsv_status st = flush_stage(s)) return st;
     if (rsv_status st = ensure_slots(s)) return st;
     if (parts > 0) {
@@ -787,7 +855,7 @@ rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t par
         s->pub_valid = false;
     }
     if (total_count > s->count) s->count = total_count;
-    if (s->own_stream) RSV_HIP_TRY(hipStreamSynchronize(s->stream));
+    if (s->own_stream) RSV_HIP_TRY(sync_stream(s));
     return RSV_OK;
 }
 

@@ -64,6 +64,18 @@ def _validate_shared(max_sample_size: int, map_fn) -> None:
         raise NullPointerException("`map` cannot be `null`")
 
 
+_TORCH = None
+
+
+def _torch():
+    global _TORCH
+    if _TORCH is None:
+        import torch
+
+        _TORCH = torch
+    return _TORCH
+
+
 def _is_torch_cuda(x) -> bool:
     t = type(x)
     return t.__module__.startswith("torch") and t.__name__ == "Tensor" and getattr(x, "is_cuda", False)
@@ -176,8 +188,7 @@ class GpuSampler:
         if not self._L.rsv_is_open(self._h):
             raise IllegalStateException("use of sampler after calling `result()`")
         if _is_torch_cuda(elements) and self._map is identity and not self._precomputed:
-            import torch
-
+            torch = _torch()
             t = elements if elements.is_contiguous() else elements.contiguous()
             cur = _current_raw_stream(torch, t)
             if cur != self._stream:
