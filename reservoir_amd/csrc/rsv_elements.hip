@@ -166,16 +166,22 @@ __global__ __launch_bounds__(kBlock) void k2_segmented(const KeyT* __restrict__ 
         const uint64_t n_groups = ((uint64_t)len + 15) >> 4;
         auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&tab[j], (unsigned long long)i); };
         uint32_t qn = 0;
-        for (uint64_t gb = k >> 4; gb < n_groups; gb += 64) {
-            const uint64_t g = gb + lane;
-            const uint64_t i0 = g << 4;
-            const u32x4 w = level0(dk, g);
-            uint32_t mask = 0;
-            if (g < n_groups) {
-                mask = candidate_mask16(w, i0, dense_lim);
-                if (mask) mask &= clip_mask16(i0, k, (uint64_t)len);
+        // two level-0 blocks per lane per iteration: two independent Philox chains in flight
+        for (uint64_t gb = k >> 4; gb < n_groups; gb += 128) {
+            const uint64_t ga = gb + lane, gc = gb + 64 + lane;
+            const u32x4 wa = level0(dk, ga);
+            const u32x4 wc = level0(dk, gc);
+            uint32_t ma = 0, mc = 0;
+            if (ga < n_groups) {
+                ma = candidate_mask16(wa, ga << 4, dense_lim);
+                if (ma) ma &= clip_mask16(ga << 4, k, (uint64_t)len);
             }
-            enqueue_block(dk, w, i0, mask, q, qn, lane, k, hit);
+            if (gc < n_groups) {
+                mc = candidate_mask16(wc, gc << 4, dense_lim);
+                if (mc) mc &= clip_mask16(gc << 4, k, (uint64_t)len);
+            }
+            enqueue_block(dk, wa, ga << 4, ma, q, qn, lane, k, hit);
+            enqueue_block(dk, wc, gc << 4, mc, q, qn, lane, k, hit);
         }
         drain_queue(dk, q, qn, lane, k, hit);
         __builtin_amdgcn_wave_barrier();
