@@ -22,4 +22,4 @@ if [ -n "$PMC" ]; then
   python tools/pmc_summary.py k1_last_writer 1000000000 gpurun_out/pmc_k1.json \
     gpurun_out/pmc_FETCH_SIZE/pmc_counter_collection.csv gpurun_out/pmc_WRITE_SIZE/pmc_counter_collection.csv
 fi
-find gpurun_out/prof gpurun_out/pmc_* -name "*.csv" 2>/dev/null | head -20
+find gpurun_out/prof -name "*.csv" 2>/dev/null || true
