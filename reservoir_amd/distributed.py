@@ -26,6 +26,16 @@ def shard_range(n_total: int, rank: int, world: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < rem else 0)
 
 
+def shard_streams(offsets, rank: int, world: int):
+    """Independent streams (segmented sampling): this rank's contiguous slice of
+    streams as (first_stream, local offsets rebased to 0, element range [lo, hi)).  No collective:
+    rank r samples its streams with ``stream_base = first_stream`` and the outputs concatenate."""
+    n_streams = len(offsets) - 1
+    s0, s1 = shard_range(n_streams, rank, world)
+    lo, hi = int(offsets[s0]), int(offsets[s1])
+    return s0, offsets[s0:s1 + 1] - lo, (lo, hi)
+
+
 def sample_shard(sampler, keys_local, global_offset: int) -> None:
     """Sample this rank's shard of one stream (keys at [global_offset, +len))."""
     if not sampler.is_distinct:

@@ -78,3 +78,28 @@ def test_status_strings(native):
     L = native.load()
     assert L.rsv_status_string(native.E_ILLEGAL_STATE) == b"illegal state"
     assert L.rsv_abi_version() == 1
+
+
+def test_create_rejects_unknown_distinct_order_without_a_device(native):
+    L = native.load()
+    cfg = native.RsvConfig()
+    L.rsv_config_init(C.byref(cfg))
+    assert cfg.distinct_order == native.DISTINCT_AUTO
+    cfg.kind = native.KIND_DISTINCT
+    cfg.max_sample_size = 10
+    cfg.distinct_order = 7
+    h = C.c_void_p()
+    assert L.rsv_create(C.byref(cfg), C.byref(h)) == native.E_ILLEGAL_ARGUMENT
+    assert not h.value
+    assert "distinct order" in L.rsv_last_error().decode()
+
+
+def test_process_wide_profiler_without_launches(native):
+    """rsv_profile_global on/off and a read with no timed launch: zero totals, no device needed."""
+    L = native.load()
+    assert L.rsv_profile_global(1) == native.OK
+    assert L.rsv_profile_global(0) == native.OK
+    ms, n = C.c_double(-1), C.c_int64(-1)
+    assert L.rsv_profile_global_read(C.byref(ms), C.byref(n)) == native.OK
+    assert (ms.value, n.value) == (0.0, 0)
+    assert L.rsv_profile_global_read(None, None) == native.E_NULL_POINTER

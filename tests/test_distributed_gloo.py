@@ -172,3 +172,24 @@ def test_shard_range_partitions():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+def test_shard_streams_partitions(oracle):
+    """Segmented shards: concatenating the per-rank outputs (stream_base = first stream) equals one
+    launch over every stream (checked on the oracle's segmented Algorithm R)."""
+    from reservoir_amd.distributed import shard_streams
+
+    rng = np.random.default_rng(2)
+    lens = rng.integers(0, 700, size=101)
+    offs = np.r_[0, np.cumsum(lens)].astype(np.int64)
+    keys = oracle.splitmix_keys(4, int(offs[-1]))
+    want, wcnt = oracle.algo_r_segmented(9, 50, 16, keys, offs)
+    for world in (1, 2, 3, 8):
+        outs, cnts = [], []
+        for r in range(world):
+            s0, local, (lo, hi) = shard_streams(offs, r, world)
+            o, c = oracle.algo_r_segmented(9, 50 + s0, 16, keys[lo:hi], local)
+            outs.append(o.reshape(-1, 16))
+            cnts.append(c)
+        assert np.array_equal(np.concatenate(outs).reshape(-1), want.reshape(-1))
+        assert np.array_equal(np.concatenate(cnts), wcnt)
