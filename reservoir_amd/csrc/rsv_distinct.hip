@@ -635,7 +635,16 @@ static hipError_t launch_sample(DistinctState* d, const KeyT* keys, const int64_
 // (h, key).  Returns the distinct count of the union in *n_distinct.
 template <typename KeyT>
 static hipError_t merge_into_set(DistinctState* d, const int64_t* src_h, const KeyT* src_k, int64_t c,
-                                 int64_t* n_distinct, hipStream_t st) {
+                                 int64_t* n_distinct, hipStream_t st, int64_t h_max = INT64_MAX) {
+    // every hash in the merge is <= h_max (the filter threshold; the set lies below it too): the
+    // keys share their top bits, so the radix passes stop at the highest bit that varies
+    // (rocPRIM sorts signed keys as h ^ sign bit = h - INT64_MIN: those are all < 2^hbits)
+    unsigned hbits = 64;
+    if (h_max != INT64_MAX && (d->m == 0 || d->m == d->k)) {  // else the set's maximum is unknown here
+        const int64_t top = d->m == d->k ? std::max(h_max, d->max_h) : h_max;
+        const uint64_t span = (uint64_t)top - (uint64_t)INT64_MIN;
+        hbits = span ? 64u - (unsigned)__builtin_clzll(span) : 1u;
+    }
     const int64_t total = d->m + c;
     if (total == 0) {
         *n_distinct = 0;
@@ -656,7 +665,7 @@ static hipError_t merge_into_set(DistinctState* d, const int64_t* src_h, const K
     size_t tb = d->temp_bytes;
     if (d->hash_kind == kHashIdentity || d->hash_kind == kHashJavaInt) {
         // injective hash: equal h <=> equal element, so one sort by h orders (h, key)
-        if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->mh0, d->mh1, mk0, mk1, (size_t)total, 0, 64, st)))
+        if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->mh0, d->mh1, mk0, mk1, (size_t)total, 0, hbits, st)))
             return e;
         std::swap(d->mh0, d->mh1);
         std::swap(d->mk0, d->mk1);
@@ -668,7 +677,7 @@ static hipError_t merge_into_set(DistinctState* d, const int64_t* src_h, const K
                                            8 * (unsigned)sizeof(KeyT), st)))
             return e;
         tb = d->temp_bytes;
-        if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->mh1, d->mh0, mk1, mk0, (size_t)total, 0, 64, st)))
+        if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->mh1, d->mh0, mk1, mk0, (size_t)total, 0, hbits, st)))
             return e;
     }
     hipLaunchKernelGGL(dedup_flags<KeyT>, dim3(grid_1d(total)), dim3(kBlock), 0, st, d->mh0, mk0, total,
@@ -750,7 +759,7 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
             continue;
         }
         int64_t nd = 0;
-        DTRY(merge_into_set<KeyT>(d, d->cand_h, (const KeyT*)d->cand_k, c, &nd, st));
+        DTRY(merge_into_set<KeyT>(d, d->cand_h, (const KeyT*)d->cand_k, c, &nd, st, tinc));
         // exact once every batch element below the new k-th hash was a candidate
         if (tinc >= t_allowed || (d->m == d->k && d->max_h <= tinc)) return RSV_OK;
         // too tight: widen (the partial merge is harmless: bottom-k(bottom-k(S u C1) u C2) equals
