@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <mutex>
 #include <cmath>
@@ -161,7 +162,7 @@ namespace {
 
 // process-wide hot-kernel timer (rsv_profile_global); guarded by g_prof_mu
 std::mutex g_prof_mu;
-bool g_prof_on = false;
+std::atomic<bool> g_prof_on{false};
 KernelTimer& global_timer() {
     static auto* t = new KernelTimer();  // leaked on purpose, like the pool
     return *t;

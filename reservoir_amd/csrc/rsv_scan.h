@@ -153,7 +153,8 @@ __device__ __forceinline__ void drain_blocks(const uint32_t* q, uint32_t qn, uin
     drain_queue(dk, cq, cqn, lane, k, hit);
 }
 
-// K1 main loop: grid-stride over level-0 blocks (16 indices each), U blocks per lane per
+// K1 main loop, per-iteration pushes (the product launches k1_body_bits below; this form stays as
+// the A/B reference of tools/micro_k1.hip): grid-stride over level-0 blocks (16 indices each), U blocks per lane per
 // iteration; wave-uniform so the queue can run full-wave level-1 evaluations.  Hits (k ln(n/k) of
 // them) go straight to global atomicMax on the k-slot winner table: ~14k atomics per 1e9 indices
 // at k = 1024.  `q` = this wave's block queue (>= 63 + 64 U entries), `cq` its candidate queue
