@@ -9,8 +9,9 @@
  *
  * Conventions
  *   - plain C: no C++ or torch types; opaque handle; every call returns rsv_status.
- *   - keys are primitive fixed-width values (Int -> key_width 4, Long -> key_width 8) that the
- *     host extracted with the sampler's `map` (S:115-116: map may be called more than k times).
+ *   - keys are primitive fixed-width values (Int -> key_width 4, Long -> key_width 8; for the
+ *     element sampler also fixed-width byte keys of 16..256 bytes, e.g. UUIDs) that the host
+ *     extracted with the sampler's `map` (S:115-116: map may be called more than k times).
  *   - "device" pointers are HIP device pointers on the handle's device; "host" pointers are
  *     ordinary (pageable or pinned) memory.  The caller owns every buffer it passes in.
  *   - one handle is single-threaded (S:18-19); distinct handles are independent.
@@ -84,7 +85,7 @@ typedef struct rsv_config {
     uint32_t struct_size;     /* = sizeof(rsv_config) */
     int32_t  kind;            /* rsv_kind */
     int32_t  max_sample_size; /* k: S:130 maxSampleSize / S:173 */
-    int32_t  key_width;       /* 4 (Int) or 8 (Long) */
+    int32_t  key_width;       /* 4 (Int) or 8 (Long); ELEMENTS also fixed-width byte keys: a multiple of 8 up to 256 */
     int32_t  reusable;        /* S:130/S:173 reusable: result() may be called repeatedly (S:353-381, S:430-433) */
     int32_t  pre_allocate;    /* S:130 preAllocate: accepted; device slots are always preallocated */
     int32_t  engine;          /* rsv_engine (ELEMENTS only) */
@@ -170,10 +171,11 @@ rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* k
 
 /* Packed form of the two calls above for ELEMENTS samplers, the one-collective combine of
  * reservoir_amd/distributed.py: row_dev[0..k) = global index per slot (-1 = empty),
- * row_dev[k..2k) = the slot's key widened to int64 (sign-extended for 4-byte keys).  One kernel,
- * no host wait on a caller stream. */
+ * row_dev[k..2k) = the slot's key widened to int64 (sign-extended for 4-byte keys); for wide keys
+ * (key_width > 8) the k keys follow as key_width/8 int64 words each.  One kernel, no host wait on
+ * a caller stream. */
 rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev);
-/* Merge `parts` packed rows (row p at rows_dev + p*row_stride, row_stride >= 2k), e.g. the output
+/* Merge `parts` packed rows (row p at rows_dev + p*row_stride, row_stride >= the row length), e.g. the output
  * of an all-gather of every rank's rsv_export_packed row: per slot the largest global index wins. */
 rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t parts, int64_t row_stride,
                             int64_t total_count);

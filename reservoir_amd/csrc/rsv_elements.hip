@@ -250,6 +250,95 @@ __global__ __launch_bounds__(kBlock) void merge_packed_kernel(const int64_t* __r
     slot_key[j] = key;
 }
 
+// ---- fixed-width byte keys (key_width a multiple of 8 above 8: UUIDs, composite keys) ----------
+// The element sampler never looks inside a key, so wide keys only change the copies: each slot's
+// key is `words` 32-bit words, moved word by word.  Same slot logic as resolve_kernel /
+// resolve_publish_kernel (one kernel; `dst` non-null = publish, launched as one workgroup).
+__global__ __launch_bounds__(1024) void resolve_wide_kernel(const uint32_t* __restrict__ keys, int64_t base,
+                                                            int64_t n, uint32_t k, uint32_t words,
+                                                            unsigned long long* __restrict__ win,
+                                                            uint32_t* __restrict__ slot_key,
+                                                            int64_t* __restrict__ slot_idx, int fresh, int64_t m,
+                                                            uint32_t* dst, uint32_t* flag, uint32_t gen) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < k; j += stride) {
+        const unsigned long long wi = win[j];
+        const uint32_t* src = nullptr;
+        if (wi) {
+            src = keys + (size_t)((int64_t)wi - base) * words;
+            if (slot_idx) slot_idx[j] = (int64_t)wi;
+            win[j] = 0;
+        } else if ((int64_t)j >= base && (int64_t)j < base + n) {
+            src = keys + (size_t)(j - base) * words;
+            if (slot_idx) slot_idx[j] = j;
+        } else if (fresh && slot_idx) {
+            slot_idx[j] = -1;
+        }
+        uint32_t* o = slot_key + (size_t)j * words;
+        const bool out = dst && (int64_t)j < m;
+        for (uint32_t q = 0; q < words; ++q) {
+            const uint32_t v = src ? src[q] : (fresh ? 0u : o[q]);
+            if (src || fresh) o[q] = v;
+            if (out) dst[(size_t)j * words + q] = v;
+        }
+    }
+    if (dst) publish_flag(flag, gen);
+}
+
+__global__ __launch_bounds__(kBlock) void merge_slots_wide_kernel(const int64_t* __restrict__ idx_parts,
+                                                                  const uint32_t* __restrict__ key_parts,
+                                                                  int32_t parts, int64_t part_len, uint32_t k,
+                                                                  uint32_t words, int64_t* __restrict__ slot_idx,
+                                                                  uint32_t* __restrict__ slot_key) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    int64_t best = slot_idx[j];
+    int32_t from = -1;
+    for (int32_t p = 0; p < parts; ++p) {
+        const int64_t idx = idx_parts[(int64_t)p * part_len + j];
+        if (idx > best) {
+            best = idx;
+            from = p;
+        }
+    }
+    if (from < 0) return;
+    slot_idx[j] = best;
+    const uint32_t* src = key_parts + ((size_t)from * part_len + j) * words;
+    for (uint32_t q = 0; q < words; ++q) slot_key[(size_t)j * words + q] = src[q];
+}
+
+// packed rows of wide keys: [slot_idx(k) | k keys of `words` 32-bit words]
+__global__ __launch_bounds__(kBlock) void export_packed_wide_kernel(const int64_t* __restrict__ slot_idx,
+                                                                    const uint32_t* __restrict__ slot_key, uint32_t k,
+                                                                    uint32_t words, int64_t* __restrict__ row) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    row[j] = slot_idx[j];
+    uint32_t* o = (uint32_t*)(row + k) + (size_t)j * words;
+    for (uint32_t q = 0; q < words; ++q) o[q] = slot_key[(size_t)j * words + q];
+}
+
+__global__ __launch_bounds__(kBlock) void merge_packed_wide_kernel(const int64_t* __restrict__ rows, int32_t parts,
+                                                                   int64_t stride, uint32_t k, uint32_t words,
+                                                                   int64_t* __restrict__ slot_idx,
+                                                                   uint32_t* __restrict__ slot_key) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    int64_t best = slot_idx[j];
+    int32_t from = -1;
+    for (int32_t p = 0; p < parts; ++p) {
+        const int64_t idx = rows[(int64_t)p * stride + j];
+        if (idx > best) {
+            best = idx;
+            from = p;
+        }
+    }
+    if (from < 0) return;
+    slot_idx[j] = best;
+    const uint32_t* src = (const uint32_t*)(rows + (int64_t)from * stride + k) + (size_t)j * words;
+    for (uint32_t q = 0; q < words; ++q) slot_key[(size_t)j * words + q] = src[q];
+}
+
 inline DrawKey make_key(const DrawParams& dp) {
     return DrawKey{(uint32_t)dp.seed, (uint32_t)(dp.seed >> 32), (uint32_t)dp.stream,
                    (uint32_t)(dp.stream >> 32)};
@@ -284,6 +373,12 @@ hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t
                           unsigned long long* batch_win, void* slot_key, int64_t* slot_idx, bool fresh,
                           hipStream_t st) {
     const unsigned grid = (unsigned)((k + kBlock - 1) / kBlock);
+    if (key_width > 8) {
+        hipLaunchKernelGGL(resolve_wide_kernel, dim3(std::min<unsigned>(grid, 256 * 64)), dim3(kBlock), 0, st,
+                           (const uint32_t*)keys, base, n, k, (uint32_t)key_width / 4, batch_win, (uint32_t*)slot_key,
+                           slot_idx, (int)fresh, (int64_t)0, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u);
+        return hipGetLastError();
+    }
     if (key_width == 8)
         hipLaunchKernelGGL(resolve_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, st,
                            (const int64_t*)keys, base, n, k, batch_win, (int64_t*)slot_key, slot_idx, (int)fresh);
@@ -302,8 +397,10 @@ __global__ __launch_bounds__(kBlock) void init_slots_kernel(uint8_t* slot_key, i
         slot_idx[j] = -1;
         if (key_width == 8)
             ((int64_t*)slot_key)[j] = 0;
-        else
+        else if (key_width == 4)
             ((int32_t*)slot_key)[j] = 0;
+        else
+            for (int q = 0; q < key_width / 4; ++q) ((uint32_t*)slot_key)[(size_t)j * (key_width / 4) + q] = 0;
     }
 }
 
@@ -339,6 +436,12 @@ hipError_t launch_resolve_publish(const void* keys, int key_width, int64_t base,
                                   unsigned long long* batch_win, void* slot_key, int64_t* slot_idx, bool fresh,
                                   int64_t m, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st) {
     const unsigned threads = std::min<unsigned>(1024, std::max<unsigned>(64, (k + 63) / 64 * 64));
+    if (key_width > 8) {
+        hipLaunchKernelGGL(resolve_wide_kernel, dim3(1), dim3(threads), 0, st, (const uint32_t*)keys, base, n, k,
+                           (uint32_t)key_width / 4, batch_win, (uint32_t*)slot_key, slot_idx, (int)fresh, m,
+                           (uint32_t*)dst_host_dev, flag_dev, gen);
+        return hipGetLastError();
+    }
     if (key_width == 8)
         hipLaunchKernelGGL(resolve_publish_kernel<int64_t>, dim3(1), dim3(threads), 0, st, (const int64_t*)keys, base,
                            n, k, batch_win, (int64_t*)slot_key, slot_idx, (int)fresh, m, (int64_t*)dst_host_dev,
@@ -395,6 +498,12 @@ hipError_t launch_merge_slots(const int64_t* idx_parts, const void* key_parts, i
                               int32_t parts, int64_t part_len, uint32_t k, int64_t* slot_idx,
                               void* slot_key, hipStream_t st) {
     const unsigned grid = (unsigned)((k + kBlock - 1) / kBlock);
+    if (key_width > 8) {
+        hipLaunchKernelGGL(merge_slots_wide_kernel, dim3(grid), dim3(kBlock), 0, st, idx_parts,
+                           (const uint32_t*)key_parts, parts, part_len, k, (uint32_t)key_width / 4, slot_idx,
+                           (uint32_t*)slot_key);
+        return hipGetLastError();
+    }
     if (key_width == 8)
         hipLaunchKernelGGL(merge_slots_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, st, idx_parts,
                            (const int64_t*)key_parts, parts, part_len, k, slot_idx, (int64_t*)slot_key);
@@ -407,6 +516,11 @@ hipError_t launch_merge_slots(const int64_t* idx_parts, const void* key_parts, i
 hipError_t launch_export_packed(const int64_t* slot_idx, const void* slot_key, int key_width, uint32_t k,
                                 int64_t* row, hipStream_t st) {
     const unsigned grid = (unsigned)((k + kBlock - 1) / kBlock);
+    if (key_width > 8) {
+        hipLaunchKernelGGL(export_packed_wide_kernel, dim3(grid), dim3(kBlock), 0, st, slot_idx,
+                           (const uint32_t*)slot_key, k, (uint32_t)key_width / 4, row);
+        return hipGetLastError();
+    }
     if (key_width == 8)
         hipLaunchKernelGGL(export_packed_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, st, slot_idx,
                            (const int64_t*)slot_key, k, row);
@@ -419,6 +533,11 @@ hipError_t launch_export_packed(const int64_t* slot_idx, const void* slot_key, i
 hipError_t launch_merge_packed(const int64_t* rows, int32_t parts, int64_t stride, uint32_t k, int64_t* slot_idx,
                                void* slot_key, int key_width, hipStream_t st) {
     const unsigned grid = (unsigned)((k + kBlock - 1) / kBlock);
+    if (key_width > 8) {
+        hipLaunchKernelGGL(merge_packed_wide_kernel, dim3(grid), dim3(kBlock), 0, st, rows, parts, stride, k,
+                           (uint32_t)key_width / 4, slot_idx, (uint32_t*)slot_key);
+        return hipGetLastError();
+    }
     if (key_width == 8)
         hipLaunchKernelGGL(merge_packed_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, st, rows, parts, stride, k,
                            slot_idx, (int64_t*)slot_key);

@@ -478,8 +478,10 @@ rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out) {
     // validateSharedParams, Sampler.scala:79-83
     if (cfg->max_sample_size > kMaxSize) return fail(RSV_E_ILLEGAL_ARGUMENT, "maxSampleSize exceeds VM limit");
     if (cfg->max_sample_size <= 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "maxSampleSize must be positive");
-    if (cfg->key_width != 4 && cfg->key_width != 8)
-        return fail(RSV_E_ILLEGAL_ARGUMENT, "key_width must be 4 or 8");
+    const bool wide = cfg->key_width > 8 && cfg->key_width <= 256 && cfg->key_width % 8 == 0;
+    if (cfg->key_width != 4 && cfg->key_width != 8 && !(wide && cfg->kind == RSV_KIND_ELEMENTS))
+        return fail(RSV_E_ILLEGAL_ARGUMENT,
+                    "key_width must be 4 or 8 (ELEMENTS also: a multiple of 8 up to 256 bytes)");
     if (cfg->kind != RSV_KIND_ELEMENTS && cfg->kind != RSV_KIND_DISTINCT)
         return fail(RSV_E_ILLEGAL_ARGUMENT, "unknown sampler kind");
     if (cfg->kind == RSV_KIND_ELEMENTS && cfg->engine != RSV_ENGINE_PHILOX_R && cfg->engine != RSV_ENGINE_JAVA_L)
@@ -590,7 +592,8 @@ rsv_status rsv_sample(rsv_sampler* s, const void* key, const int64_t* hash) {
     }
     const int b = s->stage_cur;
     if (s->kw == 8) memcpy(s->stage_h[b] + s->stage_n * 8, key, 8);
-    else memcpy(s->stage_h[b] + s->stage_n * 4, key, 4);
+    else if (s->kw == 4) memcpy(s->stage_h[b] + s->stage_n * 4, key, 4);
+    else memcpy(s->stage_h[b] + s->stage_n * s->kw, key, (size_t)s->kw);
     if (pre) s->stage_hash_h[b][s->stage_n] = *hash;
     ++s->stage_n;
     return RSV_OK;
@@ -845,7 +848,8 @@ rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t par
                             int64_t total_count) {
     if (rsv_status st = check_packed(s)) return st;
     if (parts < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative parts");
-    if (row_stride < 2 * (int64_t)s->k) return fail(RSV_E_ILLEGAL_ARGUMENT, "row_stride < 2k");
+    const int64_t row_min = (int64_t)s->k * (1 + (s->kw > 8 ? s->kw / 8 : 1));  // [idx(k) | keys]
+    if (row_stride < row_min) return fail(RSV_E_ILLEGAL_ARGUMENT, "row_stride shorter than a packed row");
     if (parts > 0 && !rows_dev) return fail(RSV_E_NULL_POINTER, "rows_dev is NULL");
     DeviceGuard g(s->device);
     touch(s);

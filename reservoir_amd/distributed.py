@@ -80,13 +80,15 @@ def _combine_elements(sampler, world, group, device, total_count) -> None:
     """Element sampler: one kernel packs ``[idx(k) | keys(k)]`` (+ the count when the global
     length is unknown), one all-gather, one merge kernel over the gathered rows in place."""
     k = sampler.max_sample_size
-    width = 2 * k + (0 if total_count is not None else 1)
+    kw = getattr(sampler, "key_width", 8)
+    body = k * (1 + (kw // 8 if kw > 8 else 1))  # [idx(k) | keys: one int64 each, or kw/8 words]
+    width = body + (0 if total_count is not None else 1)
     row = torch.empty(width, dtype=torch.int64, device=device)
     sampler.export_packed(row)
     if total_count is None:
-        row[2 * k] = sampler.count
+        row[body] = sampler.count
     flat = torch.empty(world * width, dtype=torch.int64, device=device)
     dist.all_gather_into_tensor(flat, row, group=group)
     rows = flat.view(world, width)
-    total = int(rows[:, 2 * k].max().item()) if total_count is None else int(total_count)
+    total = int(rows[:, body].max().item()) if total_count is None else int(total_count)
     sampler.merge_packed(rows, total)

@@ -17,7 +17,10 @@ called more than ``maxSampleSize`` times, Sampler.scala:115-116); the extracted 
 to the GPU in batches.  Keys already resident in HBM (a torch CUDA tensor) are sampled in place.
 
 Extensions (keyword-only, defaulted so reference-style calls are unchanged):
-    key_type  "long" (B = Long, 8-byte keys, default) or "int" (B = Int, 4-byte keys)
+    key_type  "long" (B = Long, 8-byte keys, default), "int" (B = Int, 4-byte keys), or "bytesN"
+              (element samplers: fixed-width byte keys, N a multiple of 8 in 16..256, e.g.
+              "bytes16" for UUIDs; numpy arrays of shape (n, N) uint8 or dtype "VN", torch
+              CUDA uint8 tensors of shape (n, N))
     engine    "philox_r" (default: data-parallel Algorithm R) or "java_l" (the reference's own
               Algorithm L over java.util.Random(seed): bit-identical results to the reference)
     seed      RNG seed (default: fresh entropy, like ``new Random()`` at Sampler.scala:199)
@@ -46,6 +49,15 @@ def identity(x):
 
 
 _KEY = {"long": (8, np.int64), "int": (4, np.int32)}
+
+
+def _wide_width(key_type) -> int:
+    """Width of a "bytesN" key type (N a multiple of 8 in 16..256), else 0."""
+    if isinstance(key_type, str) and key_type.startswith("bytes") and key_type[5:].isdigit():
+        w = int(key_type[5:])
+        if 16 <= w <= 256 and w % 8 == 0:
+            return w
+    return 0
 _ENGINE = {"philox_r": N.ENGINE_PHILOX_R, "java_l": N.ENGINE_JAVA_L}
 _ORDER = {"auto": N.DISTINCT_AUTO, "set": N.DISTINCT_SET, "ordered": N.DISTINCT_ORDERED}
 
@@ -96,8 +108,8 @@ class GpuSampler:
                  pre_allocate: bool = False, hash_fn=None, hash_kind: int = N.HASH_DEFAULT,
                  key_type: str = "long", engine: str = "philox_r", seed: int | None = None,
                  stream_id: int = 0, device: int | None = None, order: str = "auto"):
-        if key_type not in _KEY:
-            raise IllegalArgumentException(f"key_type must be one of {sorted(_KEY)}")
+        if key_type not in _KEY and not _wide_width(key_type):
+            raise IllegalArgumentException(f"key_type must be one of {sorted(_KEY)} or 'bytesN'")
         if engine not in _ENGINE:
             raise IllegalArgumentException(f"engine must be one of {sorted(_ENGINE)}")
         if order not in _ORDER:
@@ -105,7 +117,11 @@ class GpuSampler:
         self._L = N.load()
         self._map = map_fn
         self._hash_fn = hash_fn
-        self._width, self._dtype = _KEY[key_type]
+        if key_type in _KEY:
+            self._width, self._dtype = _KEY[key_type]
+        else:
+            self._width = _wide_width(key_type)
+            self._dtype = np.dtype(f"V{self._width}")
         self._kind = kind
         self._k = max_sample_size
         cfg = N.RsvConfig()
@@ -179,7 +195,10 @@ class GpuSampler:
         if not self._L.rsv_is_open(self._h):
             raise IllegalStateException("use of sampler after calling `result()`")
         key, hv = self._key_hash(element)
-        kbuf = self._dtype(key).tobytes() if not isinstance(key, (bytes, bytearray)) else key
+        if self._width > 8:
+            kbuf = self._key_bytes(key)
+        else:
+            kbuf = self._dtype(key).tobytes() if not isinstance(key, (bytes, bytearray)) else key
         N.check(self._L.rsv_sample(self._h, C.c_char_p(kbuf),
                                    C.byref(hv) if hv is not None else None))
 
@@ -196,12 +215,20 @@ class GpuSampler:
                 # and torch must not hand the block to another tensor while this handle's stream
                 # still reads it (the caller may drop `elements` as soon as we return)
                 t.record_stream(torch.cuda.ExternalStream(self._stream, device=t.device))
-            if t.element_size() != self._width:
-                raise IllegalArgumentException("device tensor dtype does not match key_type")
-            N.check(self._L.rsv_sample_batch(self._h, C.c_void_p(t.data_ptr()), t.numel(),
+            if self._width <= 8:
+                if t.element_size() != self._width:
+                    raise IllegalArgumentException("device tensor dtype does not match key_type")
+                n_keys = t.numel()
+            else:  # fixed-width byte keys: any dtype, rows of exactly key_width bytes
+                if t.dim() < 2 or t.shape[-1] * t.element_size() != self._width:
+                    raise IllegalArgumentException("device tensor rows must hold key_width bytes")
+                n_keys = t.numel() * t.element_size() // self._width
+            N.check(self._L.rsv_sample_batch(self._h, C.c_void_p(t.data_ptr()), n_keys,
                                              N.MEM_DEVICE, None))
             return
-        if isinstance(elements, np.ndarray) and self._map is identity:
+        if self._width > 8:
+            keys = self._wide_keys(elements)
+        elif isinstance(elements, np.ndarray) and self._map is identity:
             keys = np.ascontiguousarray(elements, dtype=self._dtype)
         else:
             keys = np.fromiter((self._map(x) for x in elements), dtype=self._dtype)
@@ -216,6 +243,24 @@ class GpuSampler:
 
     sampleAll = sample_all
 
+    def _wide_keys(self, elements) -> np.ndarray:
+        """Host batch of fixed-width byte keys as a contiguous array of dtype VN."""
+        if isinstance(elements, np.ndarray) and self._map is identity:
+            a = np.ascontiguousarray(elements)
+        else:
+            a = np.array([self._key_bytes(self._map(x)) for x in elements], dtype=np.uint8).reshape(-1, self._width)
+        if a.dtype != self._dtype:
+            if a.dtype != np.uint8 or a.ndim != 2 or a.shape[1] != self._width:
+                raise IllegalArgumentException(f"byte keys must be uint8 rows of {self._width} bytes")
+            a = np.ascontiguousarray(a).view(self._dtype).reshape(-1)
+        return a
+
+    def _key_bytes(self, key) -> bytes:
+        b = bytes(key) if not isinstance(key, (bytes, bytearray)) else bytes(key)
+        if len(b) != self._width:
+            raise IllegalArgumentException(f"key is {len(b)} bytes, key_width is {self._width}")
+        return b
+
     def result(self) -> np.ndarray:
         """Sampler.result (Sampler.scala:59-60). Slot order for element samplers."""
         if not self._L.rsv_is_open(self._h):
@@ -223,6 +268,8 @@ class GpuSampler:
         out = np.empty(self._k, dtype=self._dtype)
         n = C.c_int64(0)
         N.check(self._L.rsv_result(self._h, out.ctypes.data_as(C.c_void_p), self._k, C.byref(n)))
+        if self._width > 8:  # fixed-width byte keys: (n, key_width) uint8 rows, slot order
+            return out[: n.value].view(np.uint8).reshape(-1, self._width).copy()
         return out if n.value == self._k else out[: n.value].copy()
 
     def result_device(self, out_tensor) -> int:
@@ -242,6 +289,10 @@ class GpuSampler:
         return self._k
 
     @property
+    def key_width(self) -> int:
+        return self._width
+
+    @property
     def key_dtype(self):
         return self._dtype
 
@@ -253,9 +304,11 @@ class GpuSampler:
         """Partial state as device tensors (idx[k], keys[k], hashes[k], n)."""
         import torch
 
-        tdt = torch.int64 if self._width == 8 else torch.int32
         idx = torch.full((self._k,), -1, dtype=torch.int64, device=device)
-        keys = torch.zeros(self._k, dtype=tdt, device=device)
+        if self._width > 8:
+            keys = torch.zeros((self._k, self._width), dtype=torch.uint8, device=device)
+        else:
+            keys = torch.zeros(self._k, dtype=torch.int64 if self._width == 8 else torch.int32, device=device)
         hashes = torch.zeros(self._k, dtype=torch.int64, device=device)
         n = C.c_int64(0)
         N.check(self._L.rsv_export_state(self._h, C.c_void_p(idx.data_ptr()),
