@@ -114,6 +114,16 @@ void       rsv_destroy(rsv_sampler* s);
  * is read only for RSV_HASH_PRECOMPUTED (may be NULL otherwise). */
 rsv_status rsv_sample(rsv_sampler* s, const void* key, const int64_t* hash);
 
+/* Zero-copy pinned batches (the north-star JVM path: keys extracted straight into pinned memory,
+ * e.g. a Panama MemorySegment over the returned pointer).  rsv_stage_acquire returns the free tail
+ * of the handle's current pinned staging buffer -- room for *capacity keys (and hashes, for
+ * RSV_HASH_PRECOMPUTED, else *hashes_out = NULL) -- and rsv_stage_commit(n) appends the first n
+ * keys written there, exactly as n rsv_sample calls would.  A full buffer is flushed to the GPU
+ * asynchronously and the next acquire returns the other buffer (double buffering).  The pointers
+ * are valid until the next call on the handle. */
+rsv_status rsv_stage_acquire(rsv_sampler* s, void** keys_out, int64_t** hashes_out, int64_t* capacity);
+rsv_status rsv_stage_commit(rsv_sampler* s, int64_t n);
+
 /* Sampler.sampleAll(elements) (S:49-50, S:289-316): appends n keys at global indices
  * [count, count+n).  mem says where `keys` (and `hashes`) live.  Identical results to n calls of
  * rsv_sample, for any split into batches (SamplerTest.scala:117-142). */

@@ -28,7 +28,8 @@ EXPORTED_SYMBOLS = (
     "rsv_is_open", "rsv_count", "rsv_set_stream", "rsv_get_stream", "rsv_synchronize", "rsv_seek",
     "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
     "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
-    "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read",
+    "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read", "rsv_stage_acquire",
+    "rsv_stage_commit",
 )
 
 
@@ -112,11 +113,14 @@ def load():
     L.rsv_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(i64)]
     L.rsv_profile_global.argtypes = [i32]
     L.rsv_profile_global_read.argtypes = [C.POINTER(C.c_double), C.POINTER(i64)]
+    L.rsv_stage_acquire.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(i64)]
+    L.rsv_stage_commit.argtypes = [vp, i64]
     for name in ("rsv_config_init", "rsv_create", "rsv_sample", "rsv_sample_batch", "rsv_result",
                  "rsv_result_device", "rsv_set_stream", "rsv_synchronize", "rsv_seek",
                  "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
                  "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
-                 "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read"):
+                 "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read", "rsv_stage_acquire",
+                 "rsv_stage_commit"):
         getattr(L, name).restype = i32
     if L.rsv_abi_version() != 1:
         raise ImportError("libreservoir_hip.so ABI version mismatch")

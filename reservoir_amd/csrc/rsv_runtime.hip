@@ -599,6 +599,32 @@ rsv_status rsv_sample(rsv_sampler* s, const void* key, const int64_t* hash) {
     return RSV_OK;
 }
 
+rsv_status rsv_stage_acquire(rsv_sampler* s, void** keys_out, int64_t** hashes_out, int64_t* capacity) {
+    if (!s || !s->open) return check_open(s);
+    if (!keys_out || !capacity) return fail(RSV_E_NULL_POINTER, "keys_out/capacity is NULL");
+    const bool pre = s->hash_kind == kHashPrecomputed && s->cfg.kind == RSV_KIND_DISTINCT;
+    if (s->stage_n == 0 || s->stage_n == s->stage_cap) {
+        if (rsv_status st = stage_slow(s, pre)) return st;
+    }
+    const int b = s->stage_cur;
+    *keys_out = s->stage_h[b] + s->stage_n * s->kw;
+    if (hashes_out) *hashes_out = pre ? s->stage_hash_h[b] + s->stage_n : nullptr;
+    *capacity = s->stage_cap - s->stage_n;
+    return RSV_OK;
+}
+
+rsv_status rsv_stage_commit(rsv_sampler* s, int64_t n) {
+    if (!s || !s->open) return check_open(s);
+    if (n < 0 || n > s->stage_cap - s->stage_n)
+        return fail(RSV_E_ILLEGAL_ARGUMENT, "commit exceeds the acquired staging capacity");
+    s->stage_n += n;
+    if (s->stage_n == s->stage_cap && n > 0) {  // full: start its flush now, overlapping the next fill
+        DeviceGuard g(s->device);
+        if (rsv_status st = flush_stage(s)) return st;
+    }
+    return RSV_OK;
+}
+
 rsv_status rsv_sample_batch(rsv_sampler* s, const void* keys, int64_t n, int32_t mem, const int64_t* hashes) {
     if (rsv_status st = check_open(s)) return st;
     if (n < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative batch size");
