@@ -68,6 +68,9 @@ struct Options {
     uint64_t seed = 0;       // default: fresh entropy, like `new Random()` (Sampler.scala:199)
     uint64_t stream_id = 0;  // Philox stream of an Engine::PhiloxR sampler
     int device = -1;         // HIP device ordinal, -1 = current
+    // Sampler.distinct tie semantics (rsv_distinct_order): Auto = the reference's sequential heap
+    // for colliding hashes (Long#hashCode), order-independent bottom-k for injective ones
+    rsv_distinct_order distinct_order = RSV_DISTINCT_AUTO;
 };
 
 // trait Sampler[A, B] (Sampler.scala:26-68)
@@ -178,6 +181,7 @@ private:
         cfg.engine = (int32_t)opts.engine;
         cfg.hash_kind = hash_kind;
         cfg.device = opts.device;
+        cfg.distinct_order = (int32_t)opts.distinct_order;
         if (opts.has_seed) {
             cfg.seed = opts.seed;
         } else {
