@@ -108,6 +108,36 @@ def load_traffic(n: int):
     return None
 
 
+def secondary(dev, with_cpu: bool) -> list:
+    """The other hot-path configs of BASELINE.json (not the headline `value`): C3 segmented,
+    C4 distinct (one GPU's share; identity hash, and Long.hashCode in set and ordered order), C2 on
+    the reference's Algorithm L (engine java_l).  Same measurement code as tools/bench_paths.py;
+    a failure here is reported in the entry, never fails the headline line."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_paths as P
+
+    out = []
+    jobs = [("C3", lambda: P.c3(dev)), ("C4 identity", lambda: P.c4(dev, "identity")),
+            ("C4 default/set", lambda: P.c4(dev, "default", "set")),
+            ("C4 default/ordered", lambda: P.c4(dev, "default")), ("C2 java_l", lambda: P.c2l(dev))]
+    for name, fn in jobs:
+        try:
+            r = fn()
+        except Exception as ex:  # noqa: BLE001 -- reported, not raised
+            r = {"config": name, "error": f"{type(ex).__name__}: {ex}"}
+        out.append({kk: (round(v, 6) if isinstance(v, float) else v) for kk, v in r.items()})
+        torch.cuda.empty_cache()
+    if with_cpu:
+        from oracle import oracle as O
+
+        keys = O.splitmix_keys(0xD15C, 10_000_000)
+        t = O.lib().or_time_distinct(65536, 7, O.HASH_IDENTITY, keys, keys.size)
+        out.append({"config": "CPU baseline: Sampler.distinct per element (RandomValues restated, "
+                              "Sampler.scala:394-409), k=65536, identity hash, 1e7 keys, 1 core",
+                    "Gelem_s": round(keys.size / t / 1e9, 4), "kind": "port", "cores": 1})
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -118,6 +148,8 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=0xC0FFEE)
     ap.add_argument("--stream-id", type=int, default=0x5A5A)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the other hot-path configs (C3 segmented, C4 distinct, C2 on java_l)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -239,6 +271,10 @@ def main() -> None:
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(k, n, args.seed)
+        if world == 1 and not args.no_secondary:
+            del keys
+            torch.cuda.empty_cache()
+            line["secondary"] = secondary(dev, with_cpu=not args.no_cpu_baseline)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
