@@ -9,6 +9,9 @@ all_gather + merge kernel inside the step.
 Prints ONE JSON line on rank 0 (contract in the task statement), including
   roofline      -- K1's average launch time, measured with HIP events on the sampler's stream
   cpu_baseline  -- the oracle's C restatement of the reference (Algorithm L) on one host core
+  secondary     -- (N = 1) the other configs of BASELINE.json, measured after the headline:
+                   C3 segmented, C4 distinct (identity; Long.hashCode in set and ordered order),
+                   C2 on engine java_l, and the CPU distinct baseline (tools/bench_paths.py)
 """
 from __future__ import annotations
 
