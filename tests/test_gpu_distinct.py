@@ -116,6 +116,21 @@ def test_default_long_hash_ordered_exact(cuda, oracle, k, n, buckets):
     assert got.size == wk.size
 
 
+def test_ordered_heavy_repeats(cuda, oracle):
+    """Streams of repeats of set members: most survive the maxHash filter (they are below it), so
+    the chunks shrink to the candidate buffer; the replica still matches the reference."""
+    from reservoir_amd import Sampler
+
+    rng = np.random.default_rng(31)
+    base = _colliding(rng, 600, 40)
+    vals = np.concatenate([base] + [rng.permutation(base) for _ in range(300)])
+    ref = oracle.Distinct(50, 13, oracle.HASH_JAVA_LONG)
+    ref.sample_all(vals)
+    d = Sampler.distinct(50, seed=13)()
+    d.sample_all(vals)
+    assert d.result().tolist() == ref.result()[0].tolist()
+
+
 def test_ordered_batching_invariance(cuda, oracle):
     """sample == sampleAll == any chunking, host or device memory, in the ordered mode."""
     import torch
