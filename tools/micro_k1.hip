@@ -180,6 +180,11 @@ int main(int argc, char** argv) {
             return 0;
         };
         if (run_once(k1_var<2>, 8192, ref)) return 1;
+        if (argv[1][0] == 'g') {  // grid sweep of the product body
+            for (int g : {1536, 2048, 2560, 3072, 3584, 4096, 5120, 6144, 8192, 12288})
+                time_v(k1_var_bits<2>, "k1 bit-mask push", g, 2);
+            return 0;
+        }
         for (int grid : {2048, 4096, 8192, 16384}) {
             time_v(k1_var<2>, "k1 per-iteration push", grid / 2, 2);
             time_v(k1_var_bits<1>, "k1 bit-mask push", grid, 1);
