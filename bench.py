@@ -144,8 +144,8 @@ def secondary(dev, with_cpu: bool) -> list:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--keys-per-gpu", dest="n", type=int, default=1_000_000_000)
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--seed", type=int, default=0xC0FFEE)
