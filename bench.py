@@ -201,8 +201,18 @@ def main() -> None:
     # Device warm-up (untimed): under sustained load the K1 launch time falls from ~152 to ~140 us
     # over the first ~30 ms as clocks ramp (rocprofv3 trace); run steps for 0.2 s
     # before the W warmup steps so the timed region sees the steady state.
+    # Every step holds a collective at N>1, so all ranks must run the same number of steps: the
+    # count comes from one timed step, agreed as the max over ranks.
     t_w = time.perf_counter()
-    while time.perf_counter() - t_w < 0.2:
+    step()
+    torch.cuda.synchronize()
+    n_ramp = max(1, int(0.2 / max(time.perf_counter() - t_w, 1e-4)))
+    if world > 1:
+        t = torch.tensor([min(n_ramp, 10_000)], dtype=torch.int64,
+                         device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n_ramp = int(t.item())
+    for _ in range(min(n_ramp, 10_000)):
         step()
     for _ in range(args.warmup):
         step()

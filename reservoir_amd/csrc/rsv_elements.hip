@@ -250,6 +250,36 @@ __global__ __launch_bounds__(kBlock) void merge_packed_kernel(const int64_t* __r
     slot_key[j] = key;
 }
 
+// merge of packed rows + publication in one dispatch (k <= 8192, Int/Long keys): the multi-GPU
+// combine's last step before result(), as resolve_publish_kernel is for a batch
+template <typename KeyT>
+__global__ __launch_bounds__(1024) void merge_packed_publish_kernel(const int64_t* __restrict__ rows, int32_t parts,
+                                                                    int64_t stride, uint32_t k,
+                                                                    int64_t* __restrict__ slot_idx,
+                                                                    KeyT* __restrict__ slot_key, int64_t m, KeyT* dst,
+                                                                    uint32_t* flag, uint32_t gen) {
+    for (uint32_t j = threadIdx.x; j < k; j += blockDim.x) {
+        int64_t best = slot_idx[j];
+        KeyT key = slot_key[j];
+        bool moved = false;
+        for (int32_t p = 0; p < parts; ++p) {
+            const int64_t* r = rows + (int64_t)p * stride;
+            const int64_t idx = r[j];
+            if (idx > best) {
+                best = idx;
+                key = (KeyT)r[k + j];
+                moved = true;
+            }
+        }
+        if (moved) {
+            slot_idx[j] = best;
+            slot_key[j] = key;
+        }
+        if ((int64_t)j < m) dst[j] = key;
+    }
+    publish_flag(flag, gen);
+}
+
 // ---- fixed-width byte keys (key_width a multiple of 8 above 8: UUIDs, composite keys) ----------
 // The element sampler never looks inside a key, so wide keys only change the copies: each slot's
 // key is `words` 32-bit words, moved word by word.  Same slot logic as resolve_kernel /
@@ -544,6 +574,19 @@ hipError_t launch_merge_packed(const int64_t* rows, int32_t parts, int64_t strid
     else
         hipLaunchKernelGGL(merge_packed_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, st, rows, parts, stride, k,
                            slot_idx, (int32_t*)slot_key);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_packed_publish(const int64_t* rows, int32_t parts, int64_t stride, uint32_t k,
+                                       int64_t* slot_idx, void* slot_key, int key_width, int64_t m, void* dst_host_dev,
+                                       uint32_t* flag_dev, uint32_t gen, hipStream_t st) {
+    const unsigned threads = std::min<unsigned>(1024, std::max<unsigned>(64, (k + 63) / 64 * 64));
+    if (key_width == 8)
+        hipLaunchKernelGGL(merge_packed_publish_kernel<int64_t>, dim3(1), dim3(threads), 0, st, rows, parts, stride, k,
+                           slot_idx, (int64_t*)slot_key, m, (int64_t*)dst_host_dev, flag_dev, gen);
+    else
+        hipLaunchKernelGGL(merge_packed_publish_kernel<int32_t>, dim3(1), dim3(threads), 0, st, rows, parts, stride, k,
+                           slot_idx, (int32_t*)slot_key, m, (int32_t*)dst_host_dev, flag_dev, gen);
     return hipGetLastError();
 }
 

@@ -117,6 +117,11 @@ hipError_t launch_export_packed(const int64_t* slot_idx, const void* slot_key, i
 hipError_t launch_merge_packed(const int64_t* rows, int32_t parts, int64_t stride, uint32_t k, int64_t* slot_idx,
                                void* slot_key, int key_width, hipStream_t st);
 
+// merge of packed rows + publication of the first m keys (k <= 8192, key_width 4 / 8)
+hipError_t launch_merge_packed_publish(const int64_t* rows, int32_t parts, int64_t stride, uint32_t k,
+                                       int64_t* slot_idx, void* slot_key, int key_width, int64_t m, void* dst_host_dev,
+                                       uint32_t* flag_dev, uint32_t gen, hipStream_t st);
+
 // ---- distinct (bottom-k over the scrambled hash) --------------------------------------------
 struct DistinctState;  // defined in rsv_distinct.hip
 // ordered: RSV_DISTINCT_ORDERED semantics (exact sequential replay; see rsv_distinct.hip)

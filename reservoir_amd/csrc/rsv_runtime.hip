@@ -881,11 +881,28 @@ rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t par
     touch(s);
     if (rsv_status st = flush_stage(s)) return st;
     if (rsv_status st = ensure_slots(s)) return st;
-    if (parts > 0) {
-        RSV_HIP_TRY(launch_merge_packed(rows_dev, parts, row_stride, s->k, s->slot_idx, s->slot_key, s->kw, s->stream));
-        s->pub_valid = false;
-    }
     if (total_count > s->count) s->count = total_count;
+    if (parts > 0) {
+        bool fused = false;
+        if (s->k <= kFusedPublishMaxK && s->kw <= 8) {  // merge + publish in one dispatch
+            if (rsv_status st = ensure_result_buffer(s)) return st;
+            if (s->result_publish) {
+                const uint32_t gen = ++s->result_gen;
+                const int64_t m = std::min<int64_t>(s->count, (int64_t)s->k);
+                RSV_HIP_TRY(launch_merge_packed_publish(rows_dev, parts, row_stride, s->k, s->slot_idx, s->slot_key,
+                                                        s->kw, m, s->result_dev, s->result_flag_dev, gen, s->stream));
+                s->pub_gen = gen;
+                s->pub_valid = true;
+                s->pub_ops = s->ops;
+                fused = true;
+            }
+        }
+        if (!fused) {
+            RSV_HIP_TRY(launch_merge_packed(rows_dev, parts, row_stride, s->k, s->slot_idx, s->slot_key, s->kw,
+                                            s->stream));
+            s->pub_valid = false;
+        }
+    }
     if (s->own_stream) RSV_HIP_TRY(sync_stream(s));
     return RSV_OK;
 }
