@@ -150,6 +150,8 @@ def main() -> None:
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--seed", type=int, default=0xC0FFEE)
     ap.add_argument("--stream-id", type=int, default=0x5A5A)
+    ap.add_argument("--time-every", type=int, default=4,
+                    help="HIP events around every N-th K1 launch of the timed steps (1 = every launch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the other hot-path configs (C3 segmented, C4 distinct, C2 on java_l)")
@@ -220,9 +222,10 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # K1 timing: HIP events around every K1 launch of the timed steps (process-wide list, drained
-    # after the timed region; rsv_profile_global in include/reservoir_hip.h)
-    _native.check(L.rsv_profile_global(1))
+    # K1 timing: HIP events around every N-th K1 launch of the timed steps (process-wide list,
+    # drained after the timed region; rsv_profile_global in include/reservoir_hip.h).  Each event
+    # pair adds ~5 us of marker packets to its step, so by default one step in four carries them.
+    _native.check(L.rsv_profile_global(max(1, args.time_every)))
     t0 = time.perf_counter()
     res = None
     for _ in range(args.steps):
@@ -276,6 +279,7 @@ def main() -> None:
                 "traffic": load_traffic(n),
                 "kernel": "k1_last_writer",
                 "launch_avg_us": round(k1_s * 1e6, 2),
+                "launches_timed": prof[1],
                 "note": "achieved charges 8 B per element (SURVEY.md 8(d)); K1 reads no key "
                         "(draws depend only on the index), so it is bound by Philox integer "
                         "VALU work, not HBM -- see the valu_roofline object and DESIGN.md",

@@ -159,7 +159,9 @@ rsv_status rsv_profile_read(rsv_sampler* s, double* total_ms, int64_t* launches)
 /* Process-wide form (bench.py): while on, the hot-kernel launches of every ELEMENTS handle without
  * its own timing are bracketed by events kept in one process-wide list, so a timed loop that creates and
  * closes samplers pays no per-handle enable/read; rsv_profile_global_read synchronizes those events,
- * returns the totals since the last read and starts a new window. */
+ * returns the totals since the last read and starts a new window.  `on` = 0 turns it off; N > 0
+ * times every N-th launch from now on (1 = every launch; a larger N keeps the event packets off
+ * most launches of a tight loop while the average stays a live measurement). */
 rsv_status rsv_profile_global(int32_t on);
 rsv_status rsv_profile_global_read(double* total_ms, int64_t* launches);
 

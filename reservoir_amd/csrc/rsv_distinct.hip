@@ -577,6 +577,7 @@ void distinct_destroy(DistinctState* d) {
 }
 
 int64_t distinct_size(const DistinctState* d) { return d->m; }
+const void* distinct_keys_dev(const DistinctState* d) { return d->set_k; }
 
 template <typename KeyT>
 static hipError_t launch_filter(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,

@@ -133,6 +133,7 @@ void distinct_destroy(DistinctState* d);
 int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* hashes, int64_t n,
                            hipStream_t st);
 int64_t distinct_size(const DistinctState* d);
+const void* distinct_keys_dev(const DistinctState* d);  // the current set's keys (m of them)
 // copies the set (ascending hash) to device buffers; either may be null
 int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStream_t st);
 // merge external (key, hash) entries (device) into the set

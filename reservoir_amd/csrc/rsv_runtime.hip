@@ -176,18 +176,35 @@ inline hipError_t sync_stream(rsv_sampler* s) {
     return e;
 }
 
-// record a timing mark for the handle's hot kernel: its own timer, else the process-wide one
-void prof_mark(rsv_sampler* s, hipStream_t st) {
+// Timing marks around the handle's hot kernel: its own timer (every launch), else the process-wide
+// one, which times every g_prof_every-th launch (rsv_profile_global).  prof_begin's return value
+// goes to the matching prof_end.
+std::atomic<int64_t> g_prof_every{1};
+int64_t g_prof_seq = 0;  // guarded by g_prof_mu
+
+bool prof_begin(rsv_sampler* s, hipStream_t st) {
     if (s->timer.on) {
         s->timer.mark(st);
-        return;
+        return true;
     }
-    if (!g_prof_on) return;
+    if (!g_prof_on) return false;
     std::lock_guard<std::mutex> lk(g_prof_mu);
+    if (g_prof_seq++ % g_prof_every != 0) return false;
     KernelTimer& t = global_timer();
     t.on = true;
     t.device = s->device;
     t.mark(st);
+    return true;
+}
+
+void prof_end(rsv_sampler* s, hipStream_t st, bool marked) {
+    if (!marked) return;
+    if (s->timer.on) {
+        s->timer.mark(st);
+        return;
+    }
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    global_timer().mark(st);
 }
 
 constexpr int32_t kMaxSize = 2147483647 - 2;  // Sampler.scala:71 (hotspot VM array limit)
@@ -350,18 +367,18 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
             if (rsv_status st = ensure_events(s, ne)) return st;
             RSV_HIP_TRY(hipMemcpyAsync(s->ev_pos_d, s->ev_pos_h.data(), ne * 8, hipMemcpyHostToDevice, s->stream));
             RSV_HIP_TRY(hipMemcpyAsync(s->ev_slot_d, s->ev_slot_h.data(), ne * 4, hipMemcpyHostToDevice, s->stream));
-            prof_mark(s, s->stream);
+            const bool pm = prof_begin(s, s->stream);
             RSV_HIP_TRY(launch_replay_events(s->ev_pos_d, s->ev_slot_d, ne, s->k, s->batch_win, s->stream));
-            prof_mark(s, s->stream);
+            prof_end(s, s->stream, pm);
         }
         if (rsv_status st = resolve_batch(s, keys, base, n, fresh)) return st;
         if (ne) RSV_HIP_TRY(sync_stream(s));  // host event vectors are reused
     } else {
         const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
         const uint64_t lo = std::max<uint64_t>((uint64_t)base, s->k), hi = (uint64_t)(base + n);
-        prof_mark(s, s->stream);
+        const bool pm = prof_begin(s, s->stream);
         RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
-        prof_mark(s, s->stream);
+        prof_end(s, s->stream, pm);
         if (rsv_status st = resolve_batch(s, keys, base, n, fresh)) return st;
     }
     if (s->cfg.kind == RSV_KIND_ELEMENTS) s->slots_init = s->win_zero = true;
@@ -669,16 +686,20 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
             if (device_out) {
                 if (int rc = distinct_export(s->distinct, out, nullptr, s->stream)) return (rsv_status)rc;
             } else {
-                // stage through the chunk buffer-free path: export to device scratch then copy
-                void* tmp = nullptr;
-                RSV_HIP_TRY(hipMalloc(&tmp, m * s->kw));
-                int rc = distinct_export(s->distinct, tmp, nullptr, s->stream);
-                hipError_t e = hipMemcpyAsync(out, tmp, m * s->kw, hipMemcpyDeviceToHost, s->stream);
-                hipError_t e2 = sync_stream(s);
-                (void)hipFree(tmp);
-                if (rc) return (rsv_status)rc;
-                RSV_HIP_TRY(e);
-                RSV_HIP_TRY(e2);
+                if (rsv_status st = ensure_result_buffer(s)) return st;
+                const void* set_k = distinct_keys_dev(s->distinct);
+                touch(s);
+                if (s->result_publish) {  // the set straight into coherent host memory + flag spin
+                    const uint32_t gen = ++s->result_gen;
+                    RSV_HIP_TRY(launch_publish(set_k, m * s->kw, s->result_dev, s->result_flag_dev, gen, s->stream));
+                    s->pub_valid = false;  // the element publication state is not this one
+                    if (rsv_status st = wait_flag(s, gen)) return st;
+                    s->ops_done = s->ops;
+                } else {
+                    RSV_HIP_TRY(hipMemcpyAsync(s->result_h, set_k, m * s->kw, hipMemcpyDeviceToHost, s->stream));
+                    RSV_HIP_TRY(sync_stream(s));
+                }
+                memcpy(out, s->result_h, (size_t)m * s->kw);
             }
         }
         src = nullptr;
@@ -769,7 +790,12 @@ rsv_status rsv_profile_read(rsv_sampler* s, double* total_ms, int64_t* launches)
 }
 
 rsv_status rsv_profile_global(int32_t on) {
+    if (on < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "rsv_profile_global: negative sampling stride");
     std::lock_guard<std::mutex> lk(g_prof_mu);
+    if (on) {
+        g_prof_every = on;
+        g_prof_seq = 0;
+    }
     g_prof_on = on != 0;
     return RSV_OK;
 }

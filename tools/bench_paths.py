@@ -145,6 +145,8 @@ def main():
         print(json.dumps(c4(dev, "default", "set")), flush=True)
         print(json.dumps(c4(dev, "default")), flush=True)  # auto -> ordered (exact ties)
         torch.cuda.empty_cache()
+    if "c4i" in todo:  # identity hash only (for traces)
+        print(json.dumps(c4(dev, "identity")), flush=True)
     if "c2l" in todo:
         print(json.dumps(c2l(dev)), flush=True)
 
