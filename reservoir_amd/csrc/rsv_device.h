@@ -141,4 +141,16 @@ __host__ __device__ __forceinline__ int64_t hash_of(KeyT key) {
     }
 }
 
+// End of a one-workgroup host publication: every wave waits for its own stores, the workgroup
+// barrier orders them before lane 0, and lane 0 alone runs the system-scope release (L2 write-back)
+// and stores the flag.  (A __threadfence_system() in every wave cost ~4 us more per publication.)
+__device__ __forceinline__ void publish_flag(uint32_t* flag, uint32_t gen) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(flag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 }  // namespace rsv

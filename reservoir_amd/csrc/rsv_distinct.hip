@@ -19,6 +19,8 @@
 #include <rocprim/iterator/counting_iterator.hpp>
 
 #include <algorithm>
+#include <chrono>
+#include <limits>
 #include <vector>
 
 #include "../../include/reservoir_hip.h"
@@ -275,7 +277,320 @@ __global__ __launch_bounds__(kBlock) void compact_first_k(const int64_t* __restr
         out_k[pos[p]] = key[p];
         if ((int64_t)pos[p] == k - 1) out_count[1] = h[p];  // the new maximum (set full)
     }
-    if (p == n - 1) out_count[0] = (int64_t)pos[p] + (int64_t)flags[p];
+    if (p == n - 1) {
+        const int64_t nd = (int64_t)pos[p] + (int64_t)flags[p];
+        out_count[0] = nd;
+        if (nd <= k) out_count[1] = h[p];  // the set's largest hash (its duplicates share it)
+    }
+}
+
+// ---- bucketed merge (set mode, typical k) ------------------------------------------------------
+// set + candidates -> buckets by h (the scrambled hash is uniform; bucket b covers the b-th of B
+// equal parts of the span, B = 2^lb >= total / 128, so buckets hold ~64-128 entries) -> one wave
+// per bucket sorts by (h, key) in registers (bitonic network over cross-lane shuffles, no LDS, no
+// barriers) and drops duplicates -> each bucket's distinct entries land at their global rank; the
+// first k are the new set.  Three dispatches sized from counts read on the device: no host round
+// trip between the filter and the merge, no radix-sort passes.  A bucket above kBucketCap entries
+// (a degenerate precomputed hash) sets the overflow word and the host reruns the merge on the
+// radix-sort path.
+//   ctl: [0] filter candidate counter  [1] overflow  [2] distinct count  [3] largest kept h
+//        [4] publication ticket  [5..7] unused
+//        then (uint32, from ctl + 8) bucket_count[b] at b * 32 (one 128-B line each: the scatter's
+//        atomics on neighbouring counters would serialise on a shared line), bucket_distinct[b] at
+//        bmax * 32 + b.  bucket_sort re-zeroes the counts it consumed, so only ctl[0..1] are cleared
+//        per pass (and the counts after an overflow).
+constexpr uint32_t kBucketCap = 256;  // 4 entries per lane of the sorting wave
+constexpr uint32_t kBucketAvgLog = 7;
+constexpr uint32_t kCountStride = 32;
+constexpr int kCtlWords = 8;
+
+__device__ __forceinline__ uint32_t* bucket_count(int64_t* ctl) { return (uint32_t*)(ctl + kCtlWords); }
+__device__ __forceinline__ uint32_t* bucket_distinct(int64_t* ctl, int32_t log_bmax) {
+    return (uint32_t*)(ctl + kCtlWords) + ((size_t)kCountStride << log_bmax);
+}
+
+__device__ __forceinline__ uint32_t bucket_log(int64_t total, int32_t log_bmax) {
+    uint32_t lb = 0;
+    while ((int32_t)lb < log_bmax && ((int64_t)1 << (lb + kBucketAvgLog)) < total) ++lb;
+    return lb;
+}
+
+// Bucket of u = h - INT64_MIN in [0, span]: floor(u * B / (span + 1)) as umulhi(u, q * B) with
+// q = floor((2^64 - 1) / (span + 1)) (host), monotone in u; a span below B buckets directly.
+struct BucketMap {
+    uint64_t mult;  // 0: b = u
+    uint32_t last;
+    __device__ __forceinline__ BucketMap(uint64_t q, uint32_t lb) {
+        last = (1u << lb) - 1u;
+        mult = (lb == 0) ? 0ull : ((q >> (64 - lb)) ? 0ull : q << lb);
+        if (lb == 0) last = 0;
+    }
+    __device__ __forceinline__ uint32_t operator()(int64_t h) const {
+        const uint64_t u = (uint64_t)h ^ 0x8000000000000000ull;
+        const uint64_t b = mult ? __umul64hi(u, mult) : (last ? u : 0ull);
+        return (uint32_t)(b < last ? b : last);  // an entry above the span sorts after every bucket
+    }
+};
+
+template <typename KeyT>
+__device__ __forceinline__ bool ent_less(int64_t ha, KeyT ka, int64_t hb, KeyT kb) {
+    return ha < hb || (ha == hb && ka < kb);
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void bucket_scatter(const int64_t* __restrict__ set_h,
+                                                         const KeyT* __restrict__ set_k, int64_t m,
+                                                         const int64_t* __restrict__ cand_h,
+                                                         const KeyT* __restrict__ cand_k, int64_t cand_cap,
+                                                         int64_t* __restrict__ ctl, uint64_t q,
+                                                         int32_t log_bmax, int64_t* __restrict__ bh,
+                                                         KeyT* __restrict__ bk) {
+    const int64_t c = ctl[0];
+    if (c > cand_cap) return;  // the filter overflowed its buffer: the host tightens and reruns
+    const int64_t total = m + c;
+    const BucketMap map(q, bucket_log(total, log_bmax));
+    uint32_t* bcnt = bucket_count(ctl);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        int64_t h;
+        KeyT key;
+        if (i < m) {
+            h = set_h[i];
+            key = set_k[i];
+        } else {
+            h = cand_h[i - m];
+            key = cand_k[i - m];
+        }
+        const uint32_t b = map(h);
+        const uint32_t p = atomicAdd(&bcnt[(size_t)b * kCountStride], 1u);
+        if (p < kBucketCap) {
+            bh[(size_t)b * kBucketCap + p] = h;
+            bk[(size_t)b * kBucketCap + p] = key;
+        } else {
+            ctl[1] = 1;
+        }
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T shfl_xor_any(T v, int mask) {
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t x = (uint64_t)v;
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, mask);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), mask);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)__shfl_xor((int)v, mask);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T shfl_any(T v, int src) {
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t x = (uint64_t)v;
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)x, src);
+        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(x >> 32), src);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)__shfl((int)v, src);
+    }
+}
+
+// One wave per bucket: entry i = r * 64 + lane lives in register slot r of `lane` (R slots).
+// Bitonic network: strides >= 64 swap between a lane's own slots, smaller ones exchange with lane
+// ^ stride; then the first of each run of equal entries is kept and written back compacted;
+// bucket_distinct[b] = their number.
+template <typename KeyT, int R>
+__device__ __forceinline__ void wave_sort_bucket(int64_t* gh, KeyT* gk, uint32_t n, uint32_t* out_cnt) {
+    const uint32_t lane = threadIdx.x & 63;
+    constexpr uint32_t N = 64u * R;
+    int64_t h[R];
+    KeyT k[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = r * 64u + lane;
+        if (i < n) {
+            h[r] = gh[i];
+            k[r] = gk[i];
+        } else {
+            h[r] = INT64_MAX;
+            k[r] = std::numeric_limits<KeyT>::max();
+        }
+    }
+#pragma unroll
+    for (uint32_t size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 64) {
+                const uint32_t rs = stride / 64;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if ((r & rs) == 0) {
+                        const uint32_t i = r * 64u + lane;
+                        const bool up = (i & size) == 0;
+                        const int r2 = r + rs;
+                        if (ent_less<KeyT>(h[r2], k[r2], h[r], k[r]) == up) {
+                            const int64_t th = h[r];
+                            const KeyT tk = k[r];
+                            h[r] = h[r2];
+                            k[r] = k[r2];
+                            h[r2] = th;
+                            k[r2] = tk;
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t i = r * 64u + lane;
+                    const int64_t oh = shfl_xor_any(h[r], (int)stride);
+                    const KeyT ok = shfl_xor_any(k[r], (int)stride);
+                    const bool lower = (lane & stride) == 0;
+                    const bool up = (i & size) == 0;
+                    // the lower lane keeps the smaller entry in an ascending run, the larger otherwise
+                    const bool other_less = ent_less<KeyT>(oh, ok, h[r], k[r]);
+                    const bool mine_less = ent_less<KeyT>(h[r], k[r], oh, ok);
+                    const bool take = (lower == up) ? other_less : mine_less;
+                    if (take) {
+                        h[r] = oh;
+                        k[r] = ok;
+                    }
+                }
+            }
+        }
+    }
+    // distinct: entry i differs from entry i - 1
+    uint32_t base = 0;
+    int64_t prev_h_last = 0;
+    KeyT prev_k_last = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = r * 64u + lane;
+        int64_t ph = shfl_any(h[r], (int)((lane + 63) & 63));
+        KeyT pk = shfl_any(k[r], (int)((lane + 63) & 63));
+        if (lane == 0) {
+            ph = prev_h_last;
+            pk = prev_k_last;
+        }
+        const bool first = i < n && (i == 0 || ph != h[r] || pk != k[r]);
+        const unsigned long long bal = __ballot(first);
+        if (first) {
+            const uint32_t o = base + (uint32_t)__popcll(bal & lanemask_lt());
+            gh[o] = h[r];
+            gk[o] = k[r];
+        }
+        base += (uint32_t)__popcll(bal);
+        prev_h_last = shfl_any(h[r], 63);
+        prev_k_last = shfl_any(k[r], 63);
+    }
+    if (lane == 0) *out_cnt = base;
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void bucket_sort(int64_t m, int64_t cand_cap, int64_t* __restrict__ ctl,
+                                                      int32_t log_bmax, int64_t* __restrict__ bh,
+                                                      KeyT* __restrict__ bk) {
+    const int64_t c = ctl[0];
+    if (c > cand_cap || ctl[1]) return;
+    const uint32_t lb = bucket_log(m + c, log_bmax);
+    const uint32_t b = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (b >= (1u << lb)) return;
+    uint32_t* bcnt = bucket_count(ctl) + (size_t)b * kCountStride;
+    uint32_t* bdist = bucket_distinct(ctl, log_bmax) + b;
+    const uint32_t n = *bcnt;
+    int64_t* gh = bh + (size_t)b * kBucketCap;
+    KeyT* gk = bk + (size_t)b * kBucketCap;
+    if (n == 0) {
+        if ((threadIdx.x & 63) == 0) *bdist = 0;
+        return;
+    }
+    if (n <= 64)
+        wave_sort_bucket<KeyT, 1>(gh, gk, n, bdist);
+    else if (n <= 128)
+        wave_sort_bucket<KeyT, 2>(gh, gk, n, bdist);
+    else
+        wave_sort_bucket<KeyT, 4>(gh, gk, n, bdist);
+    if ((threadIdx.x & 63) == 0) *bcnt = 0;  // consumed (n was read before the sort's loads); re-armed
+}
+
+// each bucket's distinct entries to their global rank (ranks < k) in the set arrays.  A workgroup
+// covers kEmitBuckets consecutive buckets: their rank base is the sum of the distinct counts before
+// them (one strided pass over bucket_distinct per workgroup), then one wave per 4 buckets copies.
+constexpr uint32_t kEmitBuckets = 16;
+
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void bucket_emit(int64_t m, int64_t cand_cap, int64_t* __restrict__ ctl,
+                                                      int32_t log_bmax, const int64_t* __restrict__ bh,
+                                                      const KeyT* __restrict__ bk, int64_t k,
+                                                      int64_t* __restrict__ set_h, KeyT* __restrict__ set_k) {
+    __shared__ uint64_t s_pre[kBlock / 64], s_tot[kBlock / 64];
+    __shared__ uint64_t s_base[kEmitBuckets + 1];
+    const int64_t c = ctl[0];
+    if (c > cand_cap || ctl[1]) return;
+    const uint32_t lb = bucket_log(m + c, log_bmax);
+    const uint32_t B = 1u << lb;
+    const uint32_t b0 = blockIdx.x * kEmitBuckets;
+    if (b0 >= B) return;
+    const uint32_t* bdist = bucket_distinct(ctl, log_bmax);
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint64_t pre = 0, tot = 0;
+    for (uint32_t i = t; i < B; i += kBlock) {
+        const uint64_t v = bdist[i];
+        tot += v;
+        if (i < b0) pre += v;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        pre += shfl_xor_any(pre, off);
+        tot += shfl_xor_any(tot, off);
+    }
+    if (lane == 0) {
+        s_pre[w] = pre;
+        s_tot[w] = tot;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint64_t p = 0, q = 0;
+        for (int i = 0; i < kBlock / 64; ++i) {
+            p += s_pre[i];
+            q += s_tot[i];
+        }
+        const uint32_t nb = std::min<uint32_t>(kEmitBuckets, B - b0);
+        for (uint32_t i = 0; i < nb; ++i) {
+            s_base[i] = p;
+            p += bdist[b0 + i];
+        }
+        s_base[kEmitBuckets] = q;
+        if (b0 == 0) ctl[2] = (int64_t)q;
+    }
+    __syncthreads();
+    tot = s_base[kEmitBuckets];
+    const uint64_t mk = std::min<uint64_t>(tot, (uint64_t)k);
+    for (uint32_t j = 0; j < kEmitBuckets / (kBlock / 64); ++j) {
+        const uint32_t bi = w * (kEmitBuckets / (kBlock / 64)) + j;
+        const uint32_t b = b0 + bi;
+        if (b >= B) break;
+        const uint64_t base = s_base[bi];
+        if (base >= (uint64_t)k) break;  // later buckets rank higher still
+        const uint32_t cnt = bdist[b];
+        const int64_t* gh = bh + (size_t)b * kBucketCap;
+        const KeyT* gk = bk + (size_t)b * kBucketCap;
+        for (uint32_t r = lane; r < cnt; r += 64) {
+            const uint64_t rank = base + r;
+            if (rank < (uint64_t)k) {
+                set_h[rank] = gh[r];
+                set_k[rank] = gk[r];
+                if (rank + 1 == mk) ctl[3] = gh[r];
+            }
+        }
+    }
+}
+
+// ctl[0..3] -> coherent host memory + flag (one wave; the host spins instead of a stream sync)
+__global__ __launch_bounds__(64) void ctl_publish(const int64_t* __restrict__ ctl, int64_t* dst, uint32_t* flag,
+                                                  uint32_t gen) {
+    if (threadIdx.x < 4) dst[threadIdx.x] = ctl[threadIdx.x];
+    publish_flag(flag, gen);
 }
 
 inline unsigned grid_1d(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -410,6 +725,7 @@ struct DistinctState {
     int64_t r0 = 0, r1 = 0;
     int64_t m = 0;                // current set size
     int64_t max_h = INT64_MIN;    // valid when m == k
+    int64_t set_top = INT64_MIN;  // the set's largest hash, valid when m > 0
     int64_t* set_h = nullptr;     // [set_cap <= k], ascending (h, key)
     void* set_k = nullptr;
     int64_t set_cap = 0;
@@ -423,6 +739,14 @@ struct DistinctState {
     void *mk0 = nullptr, *mk1 = nullptr;
     uint32_t *flags = nullptr, *pos = nullptr;
     int64_t* d_count = nullptr;
+    // bucketed merge (bucket_scatter/sort/emit); log_bmax < 0: radix-sort merge only
+    int32_t log_bmax = -1;
+    int64_t* ctl = nullptr;       // control block (see bucket_scatter); `counter` points at ctl[0]
+    int64_t* hc = nullptr;        // coherent host: ctl[0..3] copies + flag at hc[8]
+    int64_t* hc_dev = nullptr;
+    uint32_t hc_gen = 0;
+    int64_t* bh = nullptr;        // [bmax * kBucketCap] bucket entries
+    void* bk = nullptr;
     void* temp = nullptr;
     size_t temp_bytes = 0;
     int64_t* samp = nullptr;      // [2 * kSample]
@@ -539,7 +863,24 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
     auto A = [&](void** p, size_t bytes) {
         if (e == hipSuccess) e = pool_device_alloc(p, bytes ? bytes : 16);
     };
-    A((void**)&d->counter, 16);
+    // bucketed merge for typical k: bmax buckets of kBucketCap entries, mean occupancy <= 128 at
+    // the largest merge (k + cand_limit entries)
+    int32_t log_bmax = 0;
+    while (((int64_t)1 << (log_bmax + kBucketAvgLog)) < (int64_t)k + d->cand_limit) ++log_bmax;
+    const double bucket_bytes = (double)((int64_t)1 << log_bmax) * kBucketCap * (8 + key_width);
+    const bool bucketed = !ordered && bucket_bytes <= 256.0 * 1024 * 1024;
+    const size_t ctl_bytes = kCtlWords * 8 + (bucketed ? ((size_t)(kCountStride + 1) * 4 << log_bmax) : 0);
+    A((void**)&d->ctl, ctl_bytes);
+    if (e == hipSuccess) e = hipMemset(d->ctl, 0, ctl_bytes);  // once: bucket_sort keeps the counts zeroed
+    d->counter = (unsigned long long*)d->ctl;
+    if (e == hipSuccess) e = pool_host_alloc((void**)&d->hc, 128, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&d->hc_dev, d->hc, 0);
+    if (e == hipSuccess) ((uint32_t*)(d->hc + 8))[0] = 0;
+    if (bucketed) {
+        A((void**)&d->bh, ((size_t)1 << log_bmax) * kBucketCap * 8);
+        A(&d->bk, ((size_t)1 << log_bmax) * kBucketCap * key_width);
+        if (e == hipSuccess) d->log_bmax = log_bmax;
+    }
     A((void**)&d->d_count, 16);
     A((void**)&d->samp, 2 * kSample * 8);
     if (e == hipSuccess) {
@@ -566,10 +907,11 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
 
 void distinct_destroy(DistinctState* d) {
     if (!d) return;
-    void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->counter, d->mh0, d->mh1, d->mk0,
+    void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->ctl, d->bh, d->bk, d->mh0, d->mh1, d->mk0,
                   d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp, d->cand_i, d->perm, d->sorted_i};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
     pool_host_free(d->h_pinned);
+    pool_host_free(d->hc);
     pool_host_free(d->ph);
     pool_host_free(d->pk);
     pool_host_free(d->pp);
@@ -578,6 +920,11 @@ void distinct_destroy(DistinctState* d) {
 
 int64_t distinct_size(const DistinctState* d) { return d->m; }
 const void* distinct_keys_dev(const DistinctState* d) { return d->set_k; }
+
+int distinct_publish(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st) {
+    RSV_HIP_TRY(launch_publish_multi(d->set_k, d->m * d->kw, dst_host_dev, flag_dev, gen, (uint32_t*)(d->ctl + 4), st));
+    return RSV_OK;
+}
 
 template <typename KeyT>
 static hipError_t launch_filter(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
@@ -632,6 +979,60 @@ static hipError_t launch_sample(DistinctState* d, const KeyT* keys, const int64_
     return rocprim::radix_sort_keys(d->temp, tb, d->samp, d->samp + kSample, (size_t)ns, 0, 64, st);
 }
 
+// span bits of every hash in a merge whose entries are all <= top (rocPRIM and the buckets both
+// work on h - INT64_MIN)
+static unsigned span_bits(int64_t top) {
+    const uint64_t span = (uint64_t)top - (uint64_t)INT64_MIN;
+    return span ? 64u - (unsigned)__builtin_clzll(span) : 1u;
+}
+
+// ctl[0..3] to the host: published by one wave into coherent memory and spun on (a stream
+// synchronize costs ~15-20 us more); falls back to a blocking synchronize after ~2 ms
+static hipError_t read_ctl(DistinctState* d, int64_t* out, hipStream_t st) {
+    const uint32_t gen = ++d->hc_gen;
+    uint32_t* flag = (uint32_t*)(d->hc + 8);
+    hipLaunchKernelGGL(ctl_publish, dim3(1), dim3(64), 0, st, (const int64_t*)d->ctl, d->hc_dev,
+                       (uint32_t*)(d->hc_dev + 8), gen);
+    if (hipError_t e = hipGetLastError()) return e;
+    const auto t0 = std::chrono::steady_clock::now();
+    bool seen = false;
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == gen) {
+            seen = true;
+            break;
+        }
+        __builtin_ia32_pause();
+        if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+    }
+    if (!seen) {
+        if (hipError_t e = hipStreamSynchronize(st)) return e;
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != gen) return hipErrorUnknown;
+    }
+    for (int i = 0; i < 4; ++i) out[i] = __atomic_load_n(d->hc + i, __ATOMIC_RELAXED);
+    return hipSuccess;
+}
+
+// the filter's candidates (count read on the device) + the current set -> new set, on the
+// bucketed path; results land in ctl[1..3] (overflow, distinct count, largest kept h)
+template <typename KeyT>
+static hipError_t launch_bucket_merge(DistinctState* d, int64_t tinc, hipStream_t st) {
+    const int64_t top = d->m ? std::max(tinc, d->set_top) : tinc;
+    const uint64_t span = (uint64_t)top - (uint64_t)INT64_MIN;
+    const uint64_t q = span == UINT64_MAX ? 1ull : UINT64_MAX / (span + 1);
+    const unsigned waves = 1u << d->log_bmax;  // one per bucket
+    const unsigned wgrid = (waves + kBlock / 64 - 1) / (kBlock / 64);
+    const unsigned sgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(d->m + d->cand_cap), 1), 1024);
+    KeyT* bk = (KeyT*)d->bk;
+    hipLaunchKernelGGL(bucket_scatter<KeyT>, dim3(sgrid), dim3(kBlock), 0, st, d->set_h, (const KeyT*)d->set_k, d->m,
+                       d->cand_h, (const KeyT*)d->cand_k, d->cand_cap, d->ctl, q, d->log_bmax, d->bh, bk);
+    hipLaunchKernelGGL(bucket_sort<KeyT>, dim3(wgrid), dim3(kBlock), 0, st, d->m, d->cand_cap, d->ctl, d->log_bmax,
+                       d->bh, bk);
+    const unsigned egrid = (waves + kEmitBuckets - 1) / kEmitBuckets;
+    hipLaunchKernelGGL(bucket_emit<KeyT>, dim3(egrid), dim3(kBlock), 0, st, d->m, d->cand_cap, d->ctl, d->log_bmax,
+                       (const int64_t*)d->bh, (const KeyT*)bk, (int64_t)d->k, d->set_h, (KeyT*)d->set_k);
+    return hipGetLastError();
+}
+
 // Merge `c` entries at (src_h, src_k) with the current set; new set = first k distinct by
 // (h, key).  Returns the distinct count of the union in *n_distinct.
 template <typename KeyT>
@@ -643,8 +1044,7 @@ static hipError_t merge_into_set(DistinctState* d, const int64_t* src_h, const K
     unsigned hbits = 64;
     if (h_max != INT64_MAX && (d->m == 0 || d->m == d->k)) {  // else the set's maximum is unknown here
         const int64_t top = d->m == d->k ? std::max(h_max, d->max_h) : h_max;
-        const uint64_t span = (uint64_t)top - (uint64_t)INT64_MIN;
-        hbits = span ? 64u - (unsigned)__builtin_clzll(span) : 1u;
+        hbits = span_bits(top);
     }
     const int64_t total = d->m + c;
     if (total == 0) {
@@ -695,6 +1095,7 @@ static hipError_t merge_into_set(DistinctState* d, const int64_t* src_h, const K
     if ((e = hipStreamSynchronize(st))) return e;
     *n_distinct = d->h_pinned[0];
     d->m = std::min<int64_t>(*n_distinct, d->k);
+    if (d->m) d->set_top = d->h_pinned[1];
     if (d->m == d->k) d->max_h = d->h_pinned[1];
     return hipSuccess;
 }
@@ -739,13 +1140,15 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
         tinc = f >= 1.0L ? t_allowed : (int64_t)((long double)INT64_MIN + f * 18446744073709551616.0L);
     }
     for (int attempt = 0; attempt < 128; ++attempt) {
-        DTRY(hipMemsetAsync(d->counter, 0, 8, st));
+        // the merge needs the set arrays at their full size (set_h/set_k are written by rank)
+        const bool bucketed = d->log_bmax >= 0 && d->set_cap >= d->k;
+        DTRY(hipMemsetAsync(d->ctl, 0, 16, st));  // candidate counter, overflow
         if (d->timer) d->timer->mark(st);
         DTRY(launch_filter<KeyT>(d, keys, hashes, n, tinc, st));
         if (d->timer) d->timer->mark(st);
-        DTRY(hipMemcpyAsync(d->h_pinned + 2, d->counter, 8, hipMemcpyDeviceToHost, st));
-        DTRY(hipStreamSynchronize(st));
-        const int64_t c = d->h_pinned[2];
+        if (bucketed) DTRY(launch_bucket_merge<KeyT>(d, tinc, st));
+        DTRY(read_ctl(d, d->h_pinned + 4, st));
+        const int64_t c = d->h_pinned[4];
         if (c > d->cand_cap) {  // threshold too loose for the candidate buffer: tighten
             if (ns == 0) {
                 if (int rc = take_sample()) return rc;
@@ -760,7 +1163,16 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
             continue;
         }
         int64_t nd = 0;
-        DTRY(merge_into_set<KeyT>(d, d->cand_h, (const KeyT*)d->cand_k, c, &nd, st, tinc));
+        if (bucketed && d->h_pinned[5] == 0) {  // merged on the device already
+            nd = d->h_pinned[6];
+            d->m = std::min<int64_t>(nd, d->k);
+            if (d->m) d->set_top = d->h_pinned[7];
+            if (d->m == d->k) d->max_h = d->set_top;
+        } else {
+            if (bucketed)  // bucket overflow: the scatter's counts were not consumed
+                DTRY(hipMemsetAsync(d->ctl + kCtlWords, 0, (size_t)kCountStride * 4 << d->log_bmax, st));
+            DTRY(merge_into_set<KeyT>(d, d->cand_h, (const KeyT*)d->cand_k, c, &nd, st, tinc));
+        }
         // exact once every batch element below the new k-th hash was a candidate
         if (tinc >= t_allowed || (d->m == d->k && d->max_h <= tinc)) return RSV_OK;
         // too tight: widen (the partial merge is harmless: bottom-k(bottom-k(S u C1) u C2) equals
@@ -854,6 +1266,7 @@ static hipError_t upload_replica(DistinctState* d, hipStream_t st) {
     if ((e = hipStreamSynchronize(st))) return e;  // the host vectors go out of scope
     d->m = m;
     d->max_h = d->rep.max_hash;
+    d->set_top = hh[(size_t)m - 1];
     return hipSuccess;
 }
 

@@ -36,18 +36,6 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
     k1_body_bits<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
 }
 
-// End of a one-workgroup host publication: every wave waits for its own stores, the workgroup
-// barrier orders them before lane 0, and lane 0 alone runs the system-scope release (L2 write-back)
-// and stores the flag.  (A __threadfence_system() in every wave cost ~4 us more per publication.)
-__device__ __forceinline__ void publish_flag(uint32_t* flag, uint32_t gen) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence_system();
-        __hip_atomic_store(flag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
 // Per slot j: the batch's last writer (win[j], then cleared), else the fill of j < k from this
 // batch, else -- first batch of a handle whose slots were never initialised (`fresh`) -- empty.
 template <typename KeyT>
@@ -453,6 +441,39 @@ __global__ __launch_bounds__(1024) void publish_kernel(const uint32_t* __restric
         ((uint4*)dst)[i] = ((const uint4*)src)[i];
     for (int64_t i = (vecs << 2) + threadIdx.x; i < words; i += blockDim.x) dst[i] = src[i];
     publish_flag(flag, gen);
+}
+
+// Publication of a large buffer (a distinct set: up to 512 KB at k = 65536) by several workgroups:
+// one workgroup's posted PCIe writes run at ~20 GB/s.  Each workgroup releases its stores at system
+// scope and takes a ticket; the last one stores the flag (and re-arms the ticket).
+__global__ __launch_bounds__(1024) void publish_multi_kernel(const uint32_t* __restrict__ src, uint32_t* dst,
+                                                            int64_t words, uint32_t* flag, uint32_t gen,
+                                                            uint32_t* ticket) {
+    const int64_t vecs = words >> 2;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = t0; i < vecs; i += stride) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    for (int64_t i = (vecs << 2) + t0; i < words; i += stride) dst[i] = src[i];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        const uint32_t prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence_system();
+            __hip_atomic_store(flag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+hipError_t launch_publish_multi(const void* src, int64_t bytes, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen,
+                                uint32_t* ticket_dev, hipStream_t st) {
+    const int64_t per = 32 * 1024;  // bytes per workgroup
+    const unsigned grid = (unsigned)std::min<int64_t>(32, std::max<int64_t>(1, (bytes + per - 1) / per));
+    hipLaunchKernelGGL(publish_multi_kernel, dim3(grid), dim3(1024), 0, st, (const uint32_t*)src,
+                       (uint32_t*)dst_host_dev, bytes / 4, flag_dev, gen, ticket_dev);
+    return hipGetLastError();
 }
 
 hipError_t launch_publish(const void* src, int64_t bytes, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen,

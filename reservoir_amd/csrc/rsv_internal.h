@@ -89,6 +89,9 @@ hipError_t launch_init_slots(void* slot_key, int key_width, int64_t* slot_idx, u
                              hipStream_t st);
 hipError_t launch_publish(const void* src, int64_t bytes, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen,
                           hipStream_t st);
+// the same from up to 32 workgroups (large buffers); ticket_dev: a zeroed device word, re-armed
+hipError_t launch_publish_multi(const void* src, int64_t bytes, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen,
+                                uint32_t* ticket_dev, hipStream_t st);
 hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,
                           unsigned long long* batch_win, void* slot_key, int64_t* slot_idx, bool fresh,
                           hipStream_t st);
@@ -134,6 +137,8 @@ int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* ha
                            hipStream_t st);
 int64_t distinct_size(const DistinctState* d);
 const void* distinct_keys_dev(const DistinctState* d);  // the current set's keys (m of them)
+// the set's m keys into coherent host memory (device-mapped pointer) + flag = gen
+int distinct_publish(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st);
 // copies the set (ascending hash) to device buffers; either may be null
 int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStream_t st);
 // merge external (key, hash) entries (device) into the set

@@ -691,7 +691,8 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
                 touch(s);
                 if (s->result_publish) {  // the set straight into coherent host memory + flag spin
                     const uint32_t gen = ++s->result_gen;
-                    RSV_HIP_TRY(launch_publish(set_k, m * s->kw, s->result_dev, s->result_flag_dev, gen, s->stream));
+                    if (int rc = distinct_publish(s->distinct, s->result_dev, s->result_flag_dev, gen, s->stream))
+                        return (rsv_status)rc;
                     s->pub_valid = false;  // the element publication state is not this one
                     if (rsv_status st = wait_flag(s, gen)) return st;
                     s->ops_done = s->ops;
