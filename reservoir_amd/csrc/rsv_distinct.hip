@@ -1113,8 +1113,11 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
     } while (0)
     if (n <= 0) return RSV_OK;
     const bool full = d->m == d->k;
-    if (full && d->max_h == INT64_MIN) return RSV_OK;  // nothing can be smaller than the max
-    const int64_t t_allowed = full ? d->max_h - 1 : INT64_MAX;  // Sampler.scala:403 (strict <)
+    // Set mode keeps the bottom-k by (h, key): an element tied with the current maximum hash can
+    // still displace the set's largest key, so the bound is inclusive.  (The reference's strict
+    // `h < maxHash`, Sampler.scala:403, makes the tie bucket depend on arrival order; that is
+    // RSV_DISTINCT_ORDERED's job.  With an injective hash both agree: no two elements tie.)
+    const int64_t t_allowed = full ? d->max_h : INT64_MAX;
     int64_t q = 0, ns = 0;
     auto take_sample = [&]() -> int {
         ns = std::min<int64_t>(n, kSample);
@@ -1140,6 +1143,17 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
         tinc = f >= 1.0L ? t_allowed : (int64_t)((long double)INT64_MIN + f * 18446744073709551616.0L);
     }
     for (int attempt = 0; attempt < 128; ++attempt) {
+        if (attempt == 8 && n > d->cand_limit / 2) {
+            // A hash with few distinct values near the boundary (e.g. a constant precomputed hash)
+            // defeats the threshold search: no threshold keeps between k and cand_cap candidates.
+            // Take the batch in slices whose every element fits the candidate buffer (each slice
+            // merges in one pass); what the attempts above merged is a subset of the batch.
+            const int64_t step = d->cand_limit / 2;
+            for (int64_t off = 0; off < n; off += step)
+                if (int rc = sample_impl<KeyT>(d, keys + off, hashes ? hashes + off : nullptr, std::min(step, n - off), st))
+                    return rc;
+            return RSV_OK;
+        }
         // the merge needs the set arrays at their full size (set_h/set_k are written by rank)
         const bool bucketed = d->log_bmax >= 0 && d->set_cap >= d->k;
         DTRY(hipMemsetAsync(d->ctl, 0, 16, st));  // candidate counter, overflow

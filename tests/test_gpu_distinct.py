@@ -219,6 +219,31 @@ def test_precomputed_hash(cuda, oracle):
     assert sorted(d.result().tolist()) == want
 
 
+@pytest.mark.parametrize("key_type", ["long", "int"])
+@pytest.mark.parametrize("n_hashes", [1, 3, 40, 5000])
+def test_set_mode_few_hash_values(cuda, oracle, key_type, n_hashes):
+    """A precomputed hash with few values: thousands of distinct elements share each scrambled
+    hash, so no threshold separates k candidates (the batch is then taken in slices that keep every
+    element) and the device merge's buckets overflow (> 256 entries; merged on the radix-sort path
+    instead); with 5000 values the buckets hold.  Either way the set is the bottom-k by
+    (scrambled hash, key) over the distinct elements, in several batches."""
+    from reservoir_amd import Sampler
+
+    rng = np.random.default_rng(n_hashes)
+    hi = 2**31 - 1 if key_type == "int" else 2**62
+    xs = rng.integers(-hi, hi, size=60_000, dtype=np.int64)
+    xs = np.concatenate([xs, xs[:20_000]])
+    k = 700
+    d = Sampler.distinct(k, seed=11, key_type=key_type, order="set")(hash=lambda x: (x * 0x9E3779B1) % n_hashes)
+    for part in np.array_split(xs, 3):
+        d.sample_all(part)
+    got = d.result().tolist()
+    r = oracle.Distinct(k, 11, oracle.HASH_IDENTITY)
+    r0, r1 = r.r0, r.r1
+    ent = sorted({(oracle.scramble(r0, r1, (int(x) * 0x9E3779B1) % n_hashes), int(x)) for x in xs.tolist()})
+    assert got == [x for _, x in ent[:k]]
+
+
 def test_distinct_lifecycle_and_duplicates(cuda):
     from reservoir_amd import IllegalStateException, Sampler
 
