@@ -244,6 +244,23 @@ def test_set_mode_few_hash_values(cuda, oracle, key_type, n_hashes):
     assert got == [x for _, x in ent[:k]]
 
 
+def test_ordered_constant_hash(cuda):
+    """hash = constant: the reference's heap fills with the first k distinct elements and then
+    rejects everything (h < maxHash never holds, Sampler.scala:403), in every batching."""
+    from reservoir_amd import Sampler
+
+    rng = np.random.default_rng(9)
+    xs = rng.integers(-2**40, 2**40, size=30_000, dtype=np.int64)
+    xs = np.concatenate([xs[:50], xs])  # repeats inside the fill phase
+    k = 1000
+    want = sorted(list(dict.fromkeys(xs.tolist()))[:k])
+    for parts in (1, 7):
+        d = Sampler.distinct(k, seed=3)(hash=lambda x: 12345)  # precomputed -> ordered by default
+        for part in np.array_split(xs, parts):
+            d.sample_all(part)
+        assert sorted(d.result().tolist()) == want
+
+
 def test_distinct_lifecycle_and_duplicates(cuda):
     from reservoir_amd import IllegalStateException, Sampler
 
