@@ -25,6 +25,7 @@
 
 #include "../../include/reservoir_hip.h"
 #include "rsv_device.h"
+#include "rsv_host_values.h"
 #include "rsv_internal.h"
 
 namespace rsv {
@@ -596,127 +597,6 @@ __global__ __launch_bounds__(64) void ctl_publish(const int64_t* __restrict__ ct
 inline unsigned grid_1d(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 }  // namespace
-
-// Exact host replica of the reference's RandomValues state (Sampler.scala:389-409): a 1-indexed
-// binary max-heap on the hash with scala 2.13 mutable.PriorityQueue's fixUp / fixDown tie behaviour
-// (addOne: sift up while parent < child; dequeue: last to the root, sift down to the larger child,
-// left on ties, stop when parent >= child), an open-addressing element set, and maxHash.  Used by
-// RSV_DISTINCT_ORDERED, which replays the GPU-filtered survivors of each chunk in arrival order.
-// (Product implementation; the oracle under oracle/ is an independent restatement for the tests.)
-struct HostValues {
-    struct Ent {
-        int64_t elem, h;
-    };
-    struct Slot {  // one cache access per probe: key and occupancy side by side
-        int64_t key;
-        int64_t used;
-    };
-    int64_t k = 0;
-    // heap as two arrays (index 0 unused): the sift loops compare hashes only
-    std::vector<int64_t> hh{0}, he{0};
-    int64_t max_hash = INT64_MIN;  // Sampler.scala:392
-    std::vector<Slot> slots;
-    uint64_t mask = 0;
-
-    int64_t size() const { return (int64_t)hh.size() - 1; }
-    static uint64_t mix(int64_t v) {
-        uint64_t z = (uint64_t)v * 0x9E3779B97F4A7C15ull;
-        return z ^ (z >> 29);
-    }
-    void set_reserve(int64_t n) {
-        uint64_t cap = 16;
-        while (cap < 2 * (uint64_t)n + 2) cap <<= 1;
-        if (cap <= mask + 1 && !slots.empty()) return;
-        std::vector<Slot> old;
-        old.swap(slots);
-        slots.assign(cap, Slot{0, 0});
-        mask = cap - 1;
-        for (const Slot& x : old)
-            if (x.used) set_add(x.key);
-    }
-    bool contains(int64_t v) const {
-        for (uint64_t q = mix(v) & mask;; q = (q + 1) & mask) {
-            if (!slots[q].used) return false;
-            if (slots[q].key == v) return true;
-        }
-    }
-    void set_add(int64_t v) {
-        uint64_t q = mix(v) & mask;
-        while (slots[q].used) q = (q + 1) & mask;
-        slots[q] = Slot{v, 1};
-    }
-    void set_remove(int64_t v) {
-        uint64_t p = mix(v) & mask;
-        while (!slots[p].used || slots[p].key != v) p = (p + 1) & mask;
-        slots[p].used = 0;
-        for (uint64_t q = (p + 1) & mask; slots[q].used; q = (q + 1) & mask) {  // backward-shift deletion
-            const uint64_t home = mix(slots[q].key) & mask;
-            const bool move = p <= q ? (home <= p || home > q) : (home <= p && home > q);
-            if (move) {
-                slots[p] = slots[q];
-                slots[q].used = 0;
-                p = q;
-            }
-        }
-    }
-    void pq_add(int64_t elem, int64_t h) {
-        hh.push_back(h);
-        he.push_back(elem);
-        size_t m = hh.size() - 1;
-        while (m > 1 && hh[m / 2] < h) {  // fixUp: parent < child -> swap
-            hh[m] = hh[m / 2];
-            he[m] = he[m / 2];
-            m /= 2;
-        }
-        hh[m] = h;
-        he[m] = elem;
-    }
-    int64_t pq_dequeue() {  // returns the removed element
-        const int64_t res = he[1];
-        const int64_t h = hh.back(), e = he.back();
-        hh.pop_back();
-        he.pop_back();
-        const int64_t n = size();
-        if (n == 0) return res;
-        int64_t kk = 1;
-        while (n >= 2 * kk) {  // fixDown: larger child (left on ties); stop when parent >= child
-            int64_t j = 2 * kk;
-            if (j < n && hh[j] < hh[j + 1]) ++j;
-            if (h >= hh[j]) break;
-            hh[kk] = hh[j];
-            he[kk] = he[j];
-            kk = j;
-        }
-        hh[kk] = h;
-        he[kk] = e;
-        return res;
-    }
-    // RandomValues.sample for one element whose scrambled hash is h (Sampler.scala:394-409)
-    void sample(int64_t elem, int64_t h) {
-        if (size() < k) {
-            if (!contains(elem)) {
-                if (size() + 1 > (int64_t)(mask + 1) / 2 - 1) set_reserve(2 * size() + 2);
-                pq_add(elem, h);
-                set_add(elem);
-                if (h > max_hash) max_hash = h;
-            }
-        } else if (h < max_hash && !contains(elem)) {
-            set_remove(pq_dequeue());
-            pq_add(elem, h);
-            set_add(elem);
-            max_hash = hh[1];
-        }
-    }
-    void reset(int64_t kk) {
-        k = kk;
-        hh.assign(1, 0);
-        he.assign(1, 0);
-        max_hash = INT64_MIN;
-        slots.clear();
-        mask = 0;
-        set_reserve(std::min<int64_t>(kk, 1 << 16));
-    }
-};
 
 struct DistinctState {
     int32_t k = 0;
@@ -1345,10 +1225,10 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
             OTRY(hipMemcpyAsync(d->pk, d->cand_k, (size_t)c * sizeof(KeyT), hipMemcpyDeviceToHost, st));
             OTRY(hipStreamSynchronize(st));
             const KeyT* pk = (const KeyT*)d->pk;
-            for (int64_t t = 0; t < c; ++t) {
-                const uint32_t q = d->pp[t];
-                rep.sample((int64_t)pk[q], d->ph[q]);
-            }
+            const uint32_t* pp = d->pp;
+            const int64_t* ph = d->ph;
+            rep.sample_run(
+                c, [&](int64_t t) { return (int64_t)pk[pp[t]]; }, [&](int64_t t) { return ph[pp[t]]; });
         }
         pos += m;
         d->seen += m;

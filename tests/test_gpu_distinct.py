@@ -261,6 +261,35 @@ def test_ordered_constant_hash(cuda):
         assert sorted(d.result().tolist()) == want
 
 
+def test_ordered_extreme_keys(cuda, oracle):
+    """Keys at the bottom of the Long range (the host replica's element set marks free slots with
+    Long.MinValue + 1 and tracks that key by a flag): kept once, repeats rejected, like any key.
+    The precomputed hash gives Long.MinValue + 1 the smallest scrambled hash of 1000 values (the
+    lowest few of the stream), so it stays in the set; Long.MinValue gets a hash of its own."""
+    from reservoir_amd import Sampler
+
+    s_key, m_key = -2**63 + 1, -2**63
+    r = oracle.Distinct(5, 4, oracle.HASH_IDENTITY)
+    v0 = min(range(1000), key=lambda v: oracle.scramble(r.r0, r.r1, v))
+    rng = np.random.default_rng(77)
+    xs = rng.integers(10**6, 10**12, size=6000, dtype=np.int64).tolist()
+    for p in (0, 7, 500, 2999, 5999):
+        xs.insert(p, s_key)
+    for p in (3, 1200, 4000):
+        xs.insert(p, m_key)
+    hf = {s_key: v0, m_key: 1000}
+    for k in (1, 5, 64):
+        d = Sampler.distinct(k, seed=4)(hash=lambda x: hf.get(x, x))
+        d.sample_all(xs)
+        ref = oracle.Distinct(k, 4, oracle.HASH_IDENTITY)
+        ref.sample_all([hf.get(x, x) for x in xs])
+        inv = {v: x for x, v in hf.items()}
+        want = sorted(inv.get(v, v) for v in ref.result()[0].tolist())
+        got = d.result().tolist()
+        assert sorted(got) == want and got.count(s_key) == want.count(s_key) <= 1
+        assert k < 64 or (s_key in want and m_key in xs)
+
+
 def test_distinct_lifecycle_and_duplicates(cuda):
     from reservoir_amd import IllegalStateException, Sampler
 
