@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <limits>
 #include <vector>
 
@@ -40,51 +41,86 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
     return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
-// Candidate output: staged per wave in LDS and written 64 at a time, so the global reservation
-// counter sees one atomic per 64 candidates (a single contended word sustains ~88 atomics/us:
-// one atomic per candidate cost 1.5 ms at 132k candidates).
-template <typename KeyT>
+// Candidate output: staged per wave in LDS and written B at a time, so the global reservation
+// counter sees one atomic per B candidates (a single contended word sustains ~88 atomics/us:
+// one atomic per candidate cost 1.5 ms at 132k candidates).  IDX: each candidate also carries its
+// pass-relative index (the ordered mode's arrival order); its chunks run at ~3k candidates per
+// pass, so it stages B = 256 (64: ~35 us of atomics per short chunk).
+template <typename KeyT, bool IDX = false>
 struct CandOut {
-    int64_t* qh;  // LDS: 128 hashes of this wave
-    KeyT* qk;     // LDS: 128 keys
+    static constexpr uint32_t B = IDX ? 256 : 64;  // batch; the LDS queue holds B + 64
+    int64_t* qh;  // LDS: B + 64 hashes of this wave
+    KeyT* qk;     // LDS: B + 64 keys
     uint32_t qn;  // wave-uniform fill
     int64_t* cand_h;
     KeyT* cand_k;
     unsigned long long* counter;
     int64_t cap;
+    uint32_t* qi = nullptr;      // LDS: B + 64 indices (IDX)
+    uint32_t* cand_i = nullptr;  // (IDX)
 
     __device__ __forceinline__ void write64(uint32_t from, uint32_t cnt) {
         const uint32_t lane = threadIdx.x & 63;
         unsigned long long base = 0;
         if (lane == 0) base = atomicAdd(counter, (unsigned long long)cnt);
         base = __shfl(base, 0);
-        if (lane < cnt) {
-            const unsigned long long pos = base + lane;
-            if ((int64_t)pos < cap) {
-                cand_h[pos] = qh[from + lane];
-                cand_k[pos] = qk[from + lane];
+        write_at(base, from, cnt);
+    }
+    __device__ __forceinline__ void write_at(unsigned long long base, uint32_t from, uint32_t cnt) {
+        const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+        for (uint32_t j0 = 0; j0 < B; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            if (j < cnt) {
+                const unsigned long long pos = base + j;
+                if ((int64_t)pos < cap) {
+                    cand_h[pos] = qh[from + j];
+                    cand_k[pos] = qk[from + j];
+                    if constexpr (IDX) cand_i[pos] = qi[from + j];
+                }
             }
         }
     }
-    __device__ __forceinline__ void push(bool c, int64_t h, KeyT key) {
+    __device__ __forceinline__ void push(bool c, int64_t h, KeyT key, uint32_t idx) {
         const unsigned long long bal = __ballot(c);
         if (bal == 0) return;
         if (c) {
             const uint32_t pos = qn + __popcll(bal & lanemask_lt());
             qh[pos] = h;
             qk[pos] = key;
+            if constexpr (IDX) qi[pos] = idx;
         }
         qn += (uint32_t)__popcll(bal);
-        if (qn >= 64) {
-            qn -= 64;
+        if (qn >= B) {
+            qn -= B;
             __builtin_amdgcn_wave_barrier();
-            write64(qn, 64);
+            write64(qn, B);
             __builtin_amdgcn_wave_barrier();
         }
     }
     __device__ __forceinline__ void flush() {
         __builtin_amdgcn_wave_barrier();
         if (qn) write64(0, qn);
+        qn = 0;
+    }
+    // the final flush of every wave of the workgroup under ONE reservation atomic: the counter is
+    // a single contended word (~88 atomics/us), and a pass whose waves each end with a few staged
+    // candidates (the ordered mode's short chunks) was bound by one atomic per wave
+    template <int WAVES>
+    __device__ __forceinline__ void flush_block(uint32_t* s_q, unsigned long long* s_base) {
+        const uint32_t w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) s_q[w] = qn;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+#pragma unroll
+            for (int i = 0; i < WAVES; ++i) tot += s_q[i];
+            *s_base = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+        }
+        __syncthreads();
+        uint32_t pre = 0;
+        for (uint32_t i = 0; i < w; ++i) pre += s_q[i];
+        if (qn) write_at(*s_base + pre, 0, qn);
         qn = 0;
     }
 };
@@ -116,10 +152,10 @@ struct Vec<int32_t> {
 // K3 filter: streaming pass.  The main loop covers whole grid tiles with unguarded loads (U x 16 B
 // per lane issued back to back, so each wave keeps U loads in flight); per-element work is the
 // scrambled hash and one compare, and the rare candidates take one wave-uniform slow path.
-template <typename KeyT, int HASH, int U, bool GUARD>
+template <typename KeyT, int HASH, int U, bool GUARD, typename Out>
 __device__ __forceinline__ void k3_tile(const typename Vec<KeyT>::T* x, int64_t v0, int64_t T, int64_t n_vec,
                                         const KeyT* keys, const int64_t* hashes, int64_t r0, int64_t r1,
-                                        int64_t tinc, CandOut<KeyT>& out) {
+                                        int64_t tinc, Out& out, uint32_t ioff) {
     using V = Vec<KeyT>;
     int64_t h[U][V::N];
     bool c[U][V::N];
@@ -141,34 +177,47 @@ __device__ __forceinline__ void k3_tile(const typename Vec<KeyT>::T* x, int64_t 
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int e = 0; e < V::N; ++e)
-                out.push(c[u][e], h[u][e], V::get(x[u], e));
+                out.push(c[u][e], h[u][e], V::get(x[u], e), ioff + (uint32_t)((v0 + u * T) * V::N + e));
     }
 }
 
-template <typename KeyT, int HASH>
+// IDX (the ordered mode's chunk pass): candidates also carry their index in [0, n < 2^32).
+template <typename KeyT, int HASH, bool IDX = false>
 __global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ keys,
                                                     const int64_t* __restrict__ hashes, int64_t n,
                                                     int64_t r0, int64_t r1, int64_t tinc,
                                                     int64_t* __restrict__ cand_h,
                                                     KeyT* __restrict__ cand_k,
                                                     unsigned long long* __restrict__ counter,
-                                                    int64_t cap) {
+                                                    int64_t cap, uint32_t* __restrict__ cand_i = nullptr) {
     using V = Vec<KeyT>;
     constexpr int U = 8;  // 8 x 16-B loads in flight per lane (tools/micro_k3: 6.0 -> 6.4 TB/s vs 4)
-    __shared__ int64_t sh_h[kBlock / 64][128];
-    __shared__ KeyT sh_k[kBlock / 64][128];
-    CandOut<KeyT> out{sh_h[threadIdx.x >> 6], sh_k[threadIdx.x >> 6], 0u, cand_h, cand_k, counter, cap};
+    constexpr uint32_t Q = CandOut<KeyT, IDX>::B + 64;
+    __shared__ int64_t sh_h[kBlock / 64][Q];
+    __shared__ KeyT sh_k[kBlock / 64][Q];
+    __shared__ uint32_t sh_i[IDX ? kBlock / 64 : 1][IDX ? Q : 1];
+    CandOut<KeyT, IDX> out{sh_h[threadIdx.x >> 6], sh_k[threadIdx.x >> 6], 0u, cand_h, cand_k, counter, cap};
+    if constexpr (IDX) {
+        out.qi = sh_i[threadIdx.x >> 6];
+        out.cand_i = cand_i;
+    }
     const int64_t T = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t n_vec = n / V::N;
-    const typename V::T* kv = reinterpret_cast<const typename V::T*>(keys);
+    // the vector loads start at the first 16-B boundary (a batch may begin anywhere in a tensor);
+    // the <= 3 head elements before it go through the scalar loop at the end
+    const int64_t head = std::min<int64_t>(n, (int64_t)(((16u - ((uintptr_t)keys & 15u)) & 15u) / sizeof(KeyT)));
+    const KeyT* kb = keys + head;
+    const int64_t* hb = HASH == kHashPrecomputed ? hashes + head : hashes;
+    const int64_t nb = n - head;
+    const int64_t n_vec = nb / V::N;
+    const typename V::T* kv = reinterpret_cast<const typename V::T*>(kb);
     const int64_t full = n_vec / (T * U);  // whole tiles: every lane has U vectors
     for (int64_t it = 0; it < full; ++it) {
         const int64_t v0 = it * T * U + tid;
         typename V::T x[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(kv + v0 + u * T);
-        k3_tile<KeyT, HASH, U, false>(x, v0, T, n_vec, keys, hashes, r0, r1, tinc, out);
+        k3_tile<KeyT, HASH, U, false>(x, v0, T, n_vec, kb, hb, r0, r1, tinc, out, (uint32_t)head);
     }
     if (full * T * U < n_vec) {  // the partial last tile, same shape: out-of-range lanes re-load the
         const int64_t v0 = full * T * U + tid;  // last vector (no guarded loads) and are masked out
@@ -178,68 +227,25 @@ __global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ key
             const int64_t v = v0 + u * T;
             x[u] = __builtin_nontemporal_load(kv + (v < n_vec ? v : n_vec - 1));
         }
-        k3_tile<KeyT, HASH, U, true>(x, v0, T, n_vec, keys, hashes, r0, r1, tinc, out);
+        k3_tile<KeyT, HASH, U, true>(x, v0, T, n_vec, kb, hb, r0, r1, tinc, out, (uint32_t)head);
     }
-    // then the n % V::N tail elements
-    for (int64_t idx = n_vec * V::N + tid; idx - tid < n; idx += T) {
+    // then the head and the nb % V::N tail elements
+    for (int64_t idx = tid; idx - tid < head; idx += T) {
+        const bool ok = idx < head;
+        const KeyT key = ok ? keys[idx] : (KeyT)0;
+        const int64_t h = ok ? elem_hash<KeyT, HASH>(keys, hashes, idx, key, r0, r1) : 0;
+        out.push(ok && h <= tinc, h, key, (uint32_t)idx);
+    }
+    for (int64_t idx = head + n_vec * V::N + tid; idx - tid < n; idx += T) {
         const bool ok = idx < n;
         const KeyT key = ok ? keys[idx] : (KeyT)0;
         const int64_t h = ok ? elem_hash<KeyT, HASH>(keys, hashes, idx, key, r0, r1) : 0;
-        out.push(ok && h <= tinc, h, key);
+        out.push(ok && h <= tinc, h, key, (uint32_t)idx);
     }
-    out.flush();
-}
-
-// Ordered-mode filter (RSV_DISTINCT_ORDERED): elements [0, n) of one chunk with h <= tinc, each
-// with its chunk-relative index so the host can replay them in arrival order.  Per-wave LDS staging
-// and one reservation atomic per 64 survivors, as k3_filter; plain grid-stride loads (the ordered
-// path is bound by the host replay, not by this pass).
-template <typename KeyT, int HASH>
-__global__ __launch_bounds__(kBlock) void k3_filter_idx(const KeyT* __restrict__ keys,
-                                                        const int64_t* __restrict__ hashes, int64_t n,
-                                                        int64_t r0, int64_t r1, int64_t tinc,
-                                                        int64_t* __restrict__ cand_h, KeyT* __restrict__ cand_k,
-                                                        uint32_t* __restrict__ cand_i,
-                                                        unsigned long long* __restrict__ counter, int64_t cap) {
-    __shared__ int64_t sh_h[kBlock / 64][128];
-    __shared__ KeyT sh_k[kBlock / 64][128];
-    __shared__ uint32_t sh_i[kBlock / 64][128];
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint32_t qn = 0;
-    auto write64 = [&](uint32_t from, uint32_t cnt) {
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(counter, (unsigned long long)cnt);
-        base = __shfl(base, 0);
-        if (lane < cnt && (int64_t)(base + lane) < cap) {
-            cand_h[base + lane] = sh_h[w][from + lane];
-            cand_k[base + lane] = sh_k[w][from + lane];
-            cand_i[base + lane] = sh_i[w][from + lane];
-        }
-    };
-    const int64_t T = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx - lane < n; idx += T) {
-        const bool ok = idx < n;
-        const KeyT key = ok ? keys[idx] : (KeyT)0;
-        const int64_t h = ok ? elem_hash<KeyT, HASH>(keys, hashes, idx, key, r0, r1) : 0;
-        const bool c = ok && h <= tinc;
-        const unsigned long long bal = __ballot(c);
-        if (bal == 0) continue;
-        if (c) {
-            const uint32_t p = qn + __popcll(bal & lanemask_lt());
-            sh_h[w][p] = h;
-            sh_k[w][p] = key;
-            sh_i[w][p] = (uint32_t)idx;
-        }
-        qn += (uint32_t)__popcll(bal);
-        if (qn >= 64) {
-            qn -= 64;
-            __builtin_amdgcn_wave_barrier();
-            write64(qn, 64);
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
+    __shared__ uint32_t s_q[kBlock / 64];
+    __shared__ unsigned long long s_base;
     __builtin_amdgcn_wave_barrier();
-    if (qn) write64(0, qn);
+    out.template flush_block<kBlock / 64>(s_q, &s_base);
 }
 
 template <typename KeyT, int HASH>
@@ -278,6 +284,9 @@ __global__ __launch_bounds__(kBlock) void compact_first_k(const int64_t* __restr
         out_k[pos[p]] = key[p];
         if ((int64_t)pos[p] == k - 1) out_count[1] = h[p];  // the new maximum (set full)
     }
+    // rank k ties with rank k - 1 on h: the maximum's bucket holds more distinct elements than the
+    // set keeps (entry p - 1 is rank k - 1 or one of its duplicates)
+    if (flags[p] && (int64_t)pos[p] == k && p > 0 && h[p - 1] == h[p]) out_count[2] = 1;
     if (p == n - 1) {
         const int64_t nd = (int64_t)pos[p] + (int64_t)flags[p];
         out_count[0] = nd;
@@ -295,7 +304,7 @@ __global__ __launch_bounds__(kBlock) void compact_first_k(const int64_t* __restr
 // (a degenerate precomputed hash) sets the overflow word and the host reruns the merge on the
 // radix-sort path.
 //   ctl: [0] filter candidate counter  [1] overflow  [2] distinct count  [3] largest kept h
-//        [4] publication ticket  [5..7] unused
+//        [4] publication ticket  [5] tie at the boundary (rank k has rank k - 1's h)  [6..7] unused
 //        then (uint32, from ctl + 8) bucket_count[b] at b * 32 (one 128-B line each: the scatter's
 //        atomics on neighbouring counters would serialise on a shared line), bucket_distinct[b] at
 //        bmax * 32 + b.  bucket_sort re-zeroes the counts it consumed, so only ctl[0..1] are cleared
@@ -346,6 +355,7 @@ __global__ __launch_bounds__(kBlock) void bucket_scatter(const int64_t* __restri
                                                          int64_t* __restrict__ ctl, uint64_t q,
                                                          int32_t log_bmax, int64_t* __restrict__ bh,
                                                          KeyT* __restrict__ bk) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctl[5] = 0;  // bucket_emit sets it
     const int64_t c = ctl[0];
     if (c > cand_cap) return;  // the filter overflowed its buffer: the host tightens and reruns
     const int64_t total = m + c;
@@ -582,15 +592,17 @@ __global__ __launch_bounds__(kBlock) void bucket_emit(int64_t m, int64_t cand_ca
                 set_h[rank] = gh[r];
                 set_k[rank] = gk[r];
                 if (rank + 1 == mk) ctl[3] = gh[r];
+            } else if (rank == (uint64_t)k && r > 0 && gh[r - 1] == gh[r]) {
+                ctl[5] = 1;  // equal h share a bucket (the map is monotone): rank k - 1 is entry r - 1
             }
         }
     }
 }
 
-// ctl[0..3] -> coherent host memory + flag (one wave; the host spins instead of a stream sync)
+// ctl[0..5] -> coherent host memory + flag (one wave; the host spins instead of a stream sync)
 __global__ __launch_bounds__(64) void ctl_publish(const int64_t* __restrict__ ctl, int64_t* dst, uint32_t* flag,
                                                   uint32_t gen) {
-    if (threadIdx.x < 4) dst[threadIdx.x] = ctl[threadIdx.x];
+    if (threadIdx.x < 6) dst[threadIdx.x] = ctl[threadIdx.x];
     publish_flag(flag, gen);
 }
 
@@ -633,15 +645,29 @@ struct DistinctState {
     int64_t* h_pinned = nullptr;  // host scalars
     std::vector<int64_t> samp_host;
     KernelTimer* timer = nullptr;
-    // RSV_DISTINCT_ORDERED: exact host replica of RandomValues + chunk buffers
+    bool last_tie = false;        // merge_into_set: rank k tied with rank k - 1 on h
+    // RSV_DISTINCT_ORDERED (see ordered_sample_impl): the set arrays track the bottom-k by (h, key)
+    // of what the reference could admit; the exact replica of RandomValues runs on the host over a
+    // device log of the admitted candidates, only when the tie bucket makes it necessary
     bool ordered = false;
-    HostValues rep;
+    bool over = false;              // more admitted distinct elements have h <= max_h than k
+    bool exact = true;              // the set arrays hold the reference's set
+    HostValues rep;                 // the replica, current up to the first logged segment
     int64_t seen = 0;               // elements sampled so far (chunk sizing)
-    uint32_t* cand_i = nullptr;     // [cand_cap] chunk-relative index of each candidate
-    uint32_t* perm = nullptr;       // [cand_cap] candidate slots in arrival order
-    uint32_t* sorted_i = nullptr;   // [cand_cap] radix-sort key output
-    int64_t ord_cap = 0;            // capacity of the three buffers above and of the pinned copies
-    int64_t* ph = nullptr;          // pinned: hashes, keys (as KeyT), perm of one chunk
+    int64_t rate_c = 0, rate_m = 0; // the last full-heap chunk: candidates, length,
+    double rate_span = 0;           // and its threshold's distance above Long.MinValue
+    struct Seg {
+        int64_t off, c, m;          // log offset, candidates, chunk length
+    };
+    std::vector<Seg> segs;
+    int64_t* log_h = nullptr;       // [log_cap] candidates of every chunk since the last replay
+    void* log_k = nullptr;
+    uint32_t* log_i = nullptr;      // chunk-relative arrival index
+    int64_t log_n = 0, log_cap = 0, log_limit = 0;
+    uint32_t* perm = nullptr;       // [ord_cap] one segment's candidates in arrival order
+    uint32_t* sorted_i = nullptr;   // [ord_cap] radix-sort key output
+    int64_t ord_cap = 0;            // capacity of the two buffers above and of the pinned copies
+    int64_t* ph = nullptr;          // pinned: hashes, keys (as KeyT), perm of one segment
     void* pk = nullptr;
     uint32_t* pp = nullptr;
 };
@@ -739,6 +765,9 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
     d->r0 = r0;
     d->r1 = r1;
     d->cand_limit = 4 * (int64_t)k + 4096;
+    d->log_limit = std::max<int64_t>(d->cand_limit, std::min<int64_t>(std::max<int64_t>(32 * d->cand_limit, 1 << 22), 1 << 27));
+    if (const char* v = std::getenv("RSV_ORDERED_LOG_LIMIT"))  // test hook: force eager replays
+        d->log_limit = std::max<int64_t>(d->cand_limit, std::atoll(v));
     hipError_t e = hipSuccess;
     auto A = [&](void** p, size_t bytes) {
         if (e == hipSuccess) e = pool_device_alloc(p, bytes ? bytes : 16);
@@ -748,7 +777,7 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
     int32_t log_bmax = 0;
     while (((int64_t)1 << (log_bmax + kBucketAvgLog)) < (int64_t)k + d->cand_limit) ++log_bmax;
     const double bucket_bytes = (double)((int64_t)1 << log_bmax) * kBucketCap * (8 + key_width);
-    const bool bucketed = !ordered && bucket_bytes <= 256.0 * 1024 * 1024;
+    const bool bucketed = bucket_bytes <= 256.0 * 1024 * 1024;
     const size_t ctl_bytes = kCtlWords * 8 + (bucketed ? ((size_t)(kCountStride + 1) * 4 << log_bmax) : 0);
     A((void**)&d->ctl, ctl_bytes);
     if (e == hipSuccess) e = hipMemset(d->ctl, 0, ctl_bytes);  // once: bucket_sort keeps the counts zeroed
@@ -761,7 +790,7 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
         A(&d->bk, ((size_t)1 << log_bmax) * kBucketCap * key_width);
         if (e == hipSuccess) d->log_bmax = log_bmax;
     }
-    A((void**)&d->d_count, 16);
+    A((void**)&d->d_count, 32);
     A((void**)&d->samp, 2 * kSample * 8);
     if (e == hipSuccess) {
         size_t tb = 0;  // the threshold sample's sort
@@ -769,7 +798,7 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
         d->temp_bytes = tb;
     }
     A(&d->temp, d->temp_bytes);
-    if (e == hipSuccess) e = pool_host_alloc((void**)&d->h_pinned, 64, hipHostMallocDefault);
+    if (e == hipSuccess) e = pool_host_alloc((void**)&d->h_pinned, 128, hipHostMallocDefault);
     // Typical k: allocate the whole working set now (nothing is allocated on the sampling path).
     // Huge k (up to Int.MaxValue - 2): grow with what the sampler holds.
     const int64_t full_merge = (int64_t)k + d->cand_limit;
@@ -788,7 +817,8 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
 void distinct_destroy(DistinctState* d) {
     if (!d) return;
     void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->ctl, d->bh, d->bk, d->mh0, d->mh1, d->mk0,
-                  d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp, d->cand_i, d->perm, d->sorted_i};
+                  d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp, d->log_h, d->log_k, d->log_i,
+                  d->perm, d->sorted_i};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
     pool_host_free(d->h_pinned);
     pool_host_free(d->hc);
@@ -866,7 +896,7 @@ static unsigned span_bits(int64_t top) {
     return span ? 64u - (unsigned)__builtin_clzll(span) : 1u;
 }
 
-// ctl[0..3] to the host: published by one wave into coherent memory and spun on (a stream
+// ctl[0..5] to the host: published by one wave into coherent memory and spun on (a stream
 // synchronize costs ~15-20 us more); falls back to a blocking synchronize after ~2 ms
 static hipError_t read_ctl(DistinctState* d, int64_t* out, hipStream_t st) {
     const uint32_t gen = ++d->hc_gen;
@@ -888,27 +918,33 @@ static hipError_t read_ctl(DistinctState* d, int64_t* out, hipStream_t st) {
         if (hipError_t e = hipStreamSynchronize(st)) return e;
         if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != gen) return hipErrorUnknown;
     }
-    for (int i = 0; i < 4; ++i) out[i] = __atomic_load_n(d->hc + i, __ATOMIC_RELAXED);
+    for (int i = 0; i < 6; ++i) out[i] = __atomic_load_n(d->hc + i, __ATOMIC_RELAXED);
     return hipSuccess;
 }
 
 // the filter's candidates (count read on the device) + the current set -> new set, on the
 // bucketed path; results land in ctl[1..3] (overflow, distinct count, largest kept h)
 template <typename KeyT>
-static hipError_t launch_bucket_merge(DistinctState* d, int64_t tinc, hipStream_t st) {
+static hipError_t launch_bucket_merge(DistinctState* d, int64_t tinc, hipStream_t st, const int64_t* cand_h = nullptr,
+                                      const KeyT* cand_k = nullptr, int64_t cand_cap = 0) {
+    if (!cand_h) {  // the set-mode filter's buffer
+        cand_h = d->cand_h;
+        cand_k = (const KeyT*)d->cand_k;
+        cand_cap = d->cand_cap;
+    }
     const int64_t top = d->m ? std::max(tinc, d->set_top) : tinc;
     const uint64_t span = (uint64_t)top - (uint64_t)INT64_MIN;
     const uint64_t q = span == UINT64_MAX ? 1ull : UINT64_MAX / (span + 1);
     const unsigned waves = 1u << d->log_bmax;  // one per bucket
     const unsigned wgrid = (waves + kBlock / 64 - 1) / (kBlock / 64);
-    const unsigned sgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(d->m + d->cand_cap), 1), 1024);
+    const unsigned sgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(d->m + cand_cap), 1), 1024);
     KeyT* bk = (KeyT*)d->bk;
     hipLaunchKernelGGL(bucket_scatter<KeyT>, dim3(sgrid), dim3(kBlock), 0, st, d->set_h, (const KeyT*)d->set_k, d->m,
-                       d->cand_h, (const KeyT*)d->cand_k, d->cand_cap, d->ctl, q, d->log_bmax, d->bh, bk);
-    hipLaunchKernelGGL(bucket_sort<KeyT>, dim3(wgrid), dim3(kBlock), 0, st, d->m, d->cand_cap, d->ctl, d->log_bmax,
+                       cand_h, cand_k, cand_cap, d->ctl, q, d->log_bmax, d->bh, bk);
+    hipLaunchKernelGGL(bucket_sort<KeyT>, dim3(wgrid), dim3(kBlock), 0, st, d->m, cand_cap, d->ctl, d->log_bmax,
                        d->bh, bk);
     const unsigned egrid = (waves + kEmitBuckets - 1) / kEmitBuckets;
-    hipLaunchKernelGGL(bucket_emit<KeyT>, dim3(egrid), dim3(kBlock), 0, st, d->m, d->cand_cap, d->ctl, d->log_bmax,
+    hipLaunchKernelGGL(bucket_emit<KeyT>, dim3(egrid), dim3(kBlock), 0, st, d->m, cand_cap, d->ctl, d->log_bmax,
                        (const int64_t*)d->bh, (const KeyT*)bk, (int64_t)d->k, d->set_h, (KeyT*)d->set_k);
     return hipGetLastError();
 }
@@ -964,6 +1000,7 @@ static hipError_t merge_into_set(DistinctState* d, const int64_t* src_h, const K
     hipLaunchKernelGGL(dedup_flags<KeyT>, dim3(grid_1d(total)), dim3(kBlock), 0, st, d->mh0, mk0, total,
                        d->flags);
     if ((e = hipGetLastError())) return e;
+    if ((e = hipMemsetAsync(d->d_count + 2, 0, 8, st))) return e;
     tb = d->temp_bytes;
     if ((e = rocprim::exclusive_scan(d->temp, tb, d->flags, d->pos, 0u, (size_t)total,
                                      rocprim::plus<uint32_t>(), st)))
@@ -971,9 +1008,10 @@ static hipError_t merge_into_set(DistinctState* d, const int64_t* src_h, const K
     hipLaunchKernelGGL(compact_first_k<KeyT>, dim3(grid_1d(total)), dim3(kBlock), 0, st, d->mh0, mk0,
                        d->flags, d->pos, total, (int64_t)d->k, d->set_h, (KeyT*)d->set_k, d->d_count);
     if ((e = hipGetLastError())) return e;
-    if ((e = hipMemcpyAsync(d->h_pinned, d->d_count, 16, hipMemcpyDeviceToHost, st))) return e;
+    if ((e = hipMemcpyAsync(d->h_pinned, d->d_count, 24, hipMemcpyDeviceToHost, st))) return e;
     if ((e = hipStreamSynchronize(st))) return e;
     *n_distinct = d->h_pinned[0];
+    d->last_tie = d->h_pinned[2] != 0;
     d->m = std::min<int64_t>(*n_distinct, d->k);
     if (d->m) d->set_top = d->h_pinned[1];
     if (d->m == d->k) d->max_h = d->h_pinned[1];
@@ -1090,12 +1128,12 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
 
 template <typename KeyT>
 static hipError_t launch_filter_idx(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
-                                    int64_t tinc, hipStream_t st) {
-    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n), 1), 256 * 8);
-    KeyT* ck = (KeyT*)d->cand_k;
-#define RSV_FILTER_IDX(H)                                                                                 \
-    hipLaunchKernelGGL((k3_filter_idx<KeyT, H>), dim3(grid), dim3(kBlock), 0, st, keys, hashes, n, d->r0, \
-                       d->r1, tinc, d->cand_h, ck, d->cand_i, d->counter, d->ord_cap)
+                                    int64_t tinc, int64_t* out_h, KeyT* out_k, uint32_t* out_i, int64_t cap,
+                                    hipStream_t st) {
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 32 + 1), 1), 256 * 32);
+#define RSV_FILTER_IDX(H)                                                                                       \
+    hipLaunchKernelGGL((k3_filter<KeyT, H, true>), dim3(grid), dim3(kBlock), 0, st, keys, hashes, n, d->r0,     \
+                       d->r1, tinc, out_h, out_k, d->counter, cap, out_i)
     switch (d->hash_kind) {
     case kHashJavaLong: RSV_FILTER_IDX(kHashJavaLong); break;
     case kHashJavaInt: RSV_FILTER_IDX(kHashJavaInt); break;
@@ -1106,11 +1144,11 @@ static hipError_t launch_filter_idx(DistinctState* d, const KeyT* keys, const in
     return hipGetLastError();
 }
 
-// ordered-mode buffers: device candidate index / permutation / sort output and pinned host copies
+// ordered-mode replay buffers: device permutation / sort output and pinned host copies of one
+// logged segment
 static hipError_t ensure_ordered(DistinctState* d, int64_t cap, hipStream_t st) {
     if (cap <= d->ord_cap) return hipSuccess;
     hipError_t e;
-    if ((e = grow((void**)&d->cand_i, 0, (size_t)cap * 4, false, st))) return e;
     if ((e = grow((void**)&d->perm, 0, (size_t)cap * 4, false, st))) return e;
     if ((e = grow((void**)&d->sorted_i, 0, (size_t)cap * 4, false, st))) return e;
     pool_host_free(d->ph);
@@ -1131,6 +1169,21 @@ static hipError_t ensure_ordered(DistinctState* d, int64_t cap, hipStream_t st) 
         d->temp_bytes = tb;
     }
     d->ord_cap = cap;
+    return hipSuccess;
+}
+
+// room for `need` log entries (kept contents).  The first allocation takes ~8 full chunks (at most
+// 256 MB): a growth copies the log and waits for the stream (~100 us each, measured).
+static hipError_t ensure_log(DistinctState* d, int64_t need, hipStream_t st) {
+    if (need <= d->log_cap) return hipSuccess;
+    const int64_t first = std::min<int64_t>(8 * d->cand_limit, (256ll << 20) / (12 + d->kw));
+    const int64_t want = std::max(need, std::min(d->log_limit, d->log_cap ? need : first));
+    const int64_t c = grown(d->log_cap, want, std::max(want, d->log_limit));
+    hipError_t e;
+    if ((e = grow((void**)&d->log_h, (size_t)d->log_n * 8, (size_t)c * 8, true, st))) return e;
+    if ((e = grow(&d->log_k, (size_t)d->log_n * d->kw, (size_t)c * d->kw, true, st))) return e;
+    if ((e = grow((void**)&d->log_i, (size_t)d->log_n * 4, (size_t)c * 4, true, st))) return e;
+    d->log_cap = c;
     return hipSuccess;
 }
 
@@ -1164,12 +1217,53 @@ static hipError_t upload_replica(DistinctState* d, hipStream_t st) {
     return hipSuccess;
 }
 
-// RSV_DISTINCT_ORDERED: the batch in chunks.  For each chunk the GPU keeps the elements the
-// reference could insert -- all of them while the heap is not full, else h < maxHash (a superset:
-// maxHash only falls within the chunk) -- with their positions; a radix sort by position restores
-// arrival order and the host replica replays them.  Elements the filter drops are exactly ones the
-// reference rejects at `elemHash < maxHash` (Sampler.scala:403), so the replica's state equals the
-// reference's after every chunk.  Chunks double with the stream (expected survivors ~k each).
+// Every logged segment, in order, through the host replica: a radix sort by chunk index restores
+// arrival order, the replica runs RandomValues.sample on each candidate (Sampler.scala:394-409).
+template <typename KeyT>
+static hipError_t replay_log(DistinctState* d, hipStream_t st) {
+    hipError_t e;
+    for (const DistinctState::Seg& g : d->segs) {
+        if (g.c == 0) continue;
+        if ((e = ensure_ordered(d, g.c, st))) return e;
+        unsigned bits = 1;
+        while (bits < 32 && ((uint64_t)1 << bits) < (uint64_t)g.m) ++bits;
+        size_t tb = d->temp_bytes;
+        if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->log_i + g.off, d->sorted_i,
+                                           rocprim::counting_iterator<uint32_t>(0), d->perm, (size_t)g.c, 0, bits,
+                                           st)))
+            return e;
+        if ((e = hipMemcpyAsync(d->pp, d->perm, (size_t)g.c * 4, hipMemcpyDeviceToHost, st))) return e;
+        if ((e = hipMemcpyAsync(d->ph, d->log_h + g.off, (size_t)g.c * 8, hipMemcpyDeviceToHost, st))) return e;
+        if ((e = hipMemcpyAsync(d->pk, (const KeyT*)d->log_k + g.off, (size_t)g.c * sizeof(KeyT),
+                                hipMemcpyDeviceToHost, st)))
+            return e;
+        if ((e = hipStreamSynchronize(st))) return e;
+        const KeyT* pk = (const KeyT*)d->pk;
+        const uint32_t* pp = d->pp;
+        const int64_t* ph = d->ph;
+        d->rep.sample_run(
+            g.c, [&](int64_t t) { return (int64_t)pk[pp[t]]; }, [&](int64_t t) { return ph[pp[t]]; });
+    }
+    d->segs.clear();
+    d->log_n = 0;
+    return hipSuccess;
+}
+
+// RSV_DISTINCT_ORDERED: the reference's exact RandomValues (strict `elemHash < maxHash` and the
+// scala PriorityQueue's choice among equal hashes, Sampler.scala:394-409), without replaying the
+// stream on the host unless a tie forces it.
+//
+// Let U be the distinct elements seen so far.  Once the heap is full its maximum M is the k-th
+// smallest hash of U, and the heap holds every element of U with hash < M (an element below M was
+// admitted on arrival -- M only falls -- and is never the maximum that leaves).  So M, and the set
+// itself when U has exactly k elements with hash <= M, follow from set arithmetic: the GPU keeps
+// the bottom-k by (h, key) of the elements the reference could admit (each chunk filtered strictly
+// below the maximum at its start, a superset of the admitted; all of it while the heap fills) and
+// the bucketed merge reports whether rank k ties rank k - 1 on h.  Only when more than k admitted
+// elements have hash <= M (`over`, sticky while M stays) does the set depend on the heap's history;
+// then the logged candidates of every chunk since the last replay go through the host replica in
+// arrival order and the replica's set replaces the device set (`distinct_finalize`, at result /
+// export / merge).  The log is replayed eagerly when it would outgrow log_limit.
 template <typename KeyT>
 static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
                                hipStream_t st) {
@@ -1181,60 +1275,77 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
             return _e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;            \
         }                                                                                     \
     } while (0)
-    HostValues& rep = d->rep;
+    if (n <= 0) return RSV_OK;
     const int64_t k = d->k;
-    const int64_t cap = std::min<int64_t>(d->cand_limit, std::max<int64_t>(4096, 2 * std::min<int64_t>(n, d->cand_limit)));
-    OTRY(ensure_caps(d, cap, 0, st));
-    OTRY(ensure_ordered(d, d->cand_cap, st));
-    const int64_t ocap = d->ord_cap;
+    const int64_t ccap = std::min<int64_t>(d->cand_limit, std::max<int64_t>(4096, 2 * std::min<int64_t>(n, d->cand_limit)));
+    OTRY(ensure_caps(d, 0, std::min<int64_t>(k, ccap + d->m), st));
     int64_t pos = 0;
     int64_t m_next = 0;  // chunk length after an overflow retry
     while (pos < n) {
-        const bool full = rep.size() == k;
-        if (full && rep.max_hash == INT64_MIN) break;  // nothing is < Long.MinValue
-        const int64_t tinc = full ? rep.max_hash - 1 : INT64_MAX;
+        const bool full = d->m == k;
+        if (full && d->max_h == INT64_MIN) break;  // nothing is < Long.MinValue
+        const int64_t tinc = full ? d->max_h - 1 : INT64_MAX;
         int64_t m;
         if (m_next) {
             m = m_next;
         } else if (!full) {
-            m = std::max<int64_t>(1024, 2 * (k - rep.size()) + 1024);  // all survive: bounded by the buffer
+            m = std::max<int64_t>(1024, 2 * (k - d->m) + 1024);  // all survive: bounded by the buffer
+        } else if (d->rate_m > 0 && d->rate_c > 0) {
+            // aim at ~3k candidates (the buffer holds 4k + 4096): the last full chunk's candidate
+            // rate, scaled by how far the threshold fell since (the scrambled hash is uniform)
+            const double span_now = (double)((uint64_t)tinc - (uint64_t)INT64_MIN) + 1.0;
+            const double rate = (double)d->rate_c / (double)d->rate_m * (span_now / d->rate_span);
+            m = (int64_t)std::min<double>(std::max<double>(0.75 * (double)ccap / rate, 65536.0), (double)(1ll << 31));
         } else {
             m = std::max<int64_t>(d->seen, 65536);
         }
-        m = std::min(std::min(m, n - pos), std::min<int64_t>(full ? ((int64_t)1 << 31) : ocap, (int64_t)1 << 31));
-        OTRY(hipMemsetAsync(d->counter, 0, 8, st));
+        m = std::min(std::min(m, n - pos), std::min<int64_t>(full ? ((int64_t)1 << 31) : ccap, (int64_t)1 << 31));
+        if (d->log_n + ccap > d->log_limit && !d->segs.empty()) OTRY(replay_log<KeyT>(d, st));
+        OTRY(ensure_log(d, d->log_n + ccap, st));
+        int64_t* lh = d->log_h + d->log_n;
+        KeyT* lk = (KeyT*)d->log_k + d->log_n;
+        const bool bucketed = d->log_bmax >= 0 && d->set_cap >= k;
+        OTRY(hipMemsetAsync(d->ctl, 0, 16, st));  // candidate counter, overflow
         if (d->timer) d->timer->mark(st);
-        OTRY(launch_filter_idx<KeyT>(d, keys + pos, hashes ? hashes + pos : nullptr, m, tinc, st));
+        OTRY(launch_filter_idx<KeyT>(d, keys + pos, hashes ? hashes + pos : nullptr, m, tinc, lh, lk,
+                                     d->log_i + d->log_n, ccap, st));
         if (d->timer) d->timer->mark(st);
-        OTRY(hipMemcpyAsync(d->h_pinned + 2, d->counter, 8, hipMemcpyDeviceToHost, st));
-        OTRY(hipStreamSynchronize(st));
-        const int64_t c = d->h_pinned[2];
-        if (c > ocap) {  // repeats of members (or a degenerate hash) overflowed the buffer: shorter chunk
-            m_next = std::max<int64_t>(1, (int64_t)((double)m * ocap / (double)c / 2));
+        if (bucketed) OTRY(launch_bucket_merge<KeyT>(d, tinc, st, lh, lk, ccap));
+        int64_t* hp = d->h_pinned + 4;
+        OTRY(read_ctl(d, hp, st));
+        const int64_t c = hp[0];
+        if (c > ccap) {  // repeats of members (or a degenerate hash) overflowed the buffer: shorter chunk
+            m_next = std::max<int64_t>(1, (int64_t)((double)m * ccap / (double)c / 2));
             continue;
         }
         m_next = 0;
-        if (c > 0) {
-            unsigned bits = 1;
-            while (bits < 32 && ((uint64_t)1 << bits) < (uint64_t)m) ++bits;
-            size_t tb = d->temp_bytes;
-            OTRY(rocprim::radix_sort_pairs(d->temp, tb, d->cand_i, d->sorted_i, rocprim::counting_iterator<uint32_t>(0),
-                                           d->perm, (size_t)c, 0, bits, st));
-            OTRY(hipMemcpyAsync(d->pp, d->perm, (size_t)c * 4, hipMemcpyDeviceToHost, st));
-            OTRY(hipMemcpyAsync(d->ph, d->cand_h, (size_t)c * 8, hipMemcpyDeviceToHost, st));
-            OTRY(hipMemcpyAsync(d->pk, d->cand_k, (size_t)c * sizeof(KeyT), hipMemcpyDeviceToHost, st));
-            OTRY(hipStreamSynchronize(st));
-            const KeyT* pk = (const KeyT*)d->pk;
-            const uint32_t* pp = d->pp;
-            const int64_t* ph = d->ph;
-            rep.sample_run(
-                c, [&](int64_t t) { return (int64_t)pk[pp[t]]; }, [&](int64_t t) { return ph[pp[t]]; });
+        const int64_t old_max = d->max_h;
+        bool tie;
+        if (bucketed && hp[1] == 0) {  // merged on the device already
+            d->m = std::min<int64_t>(hp[2], k);
+            if (d->m) d->set_top = hp[3];
+            if (d->m == k) d->max_h = d->set_top;
+            tie = hp[5] != 0;
+        } else {
+            if (bucketed)  // bucket overflow: the scatter's counts were not consumed
+                OTRY(hipMemsetAsync(d->ctl + kCtlWords, 0, (size_t)kCountStride * 4 << d->log_bmax, st));
+            int64_t nd = 0;
+            OTRY(merge_into_set<KeyT>(d, lh, lk, c, &nd, st, tinc));
+            tie = d->last_tie;
         }
+        if (d->m == k) d->over = tie || (full && d->over && d->max_h == old_max);
+        if (full) {  // candidate rate at this threshold (chunk sizing)
+            d->rate_c = c;
+            d->rate_m = m;
+            d->rate_span = (double)((uint64_t)tinc - (uint64_t)INT64_MIN) + 1.0;
+        }
+        d->segs.push_back(DistinctState::Seg{d->log_n, c, m});
+        d->log_n += c;
         pos += m;
         d->seen += m;
     }
     d->seen += n - pos;  // the rest was rejected wholesale (maxHash == Long.MinValue)
-    OTRY(upload_replica<KeyT>(d, st));
+    d->exact = d->m < k || !d->over;
     return RSV_OK;
 #undef OTRY
 }
@@ -1248,6 +1359,18 @@ int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* ha
                       : sample_impl<int32_t>(d, (const int32_t*)keys, hashes, n, st);
 }
 
+int distinct_finalize(DistinctState* d, hipStream_t st) {
+    if (!d->ordered || d->exact) return RSV_OK;
+    hipError_t e = d->kw == 8 ? replay_log<int64_t>(d, st) : replay_log<int32_t>(d, st);
+    if (e == hipSuccess) e = d->kw == 8 ? upload_replica<int64_t>(d, st) : upload_replica<int32_t>(d, st);
+    if (e != hipSuccess) {
+        set_error(std::string("distinct (ordered) replay: ") + hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;
+    }
+    d->exact = true;
+    return RSV_OK;
+}
+
 int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStream_t st) {
     if (d->m == 0) return RSV_OK;
     if (keys_dev) RSV_HIP_TRY(hipMemcpyAsync(keys_dev, d->set_k, d->m * d->kw, hipMemcpyDeviceToDevice, st));
@@ -1257,6 +1380,8 @@ int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStre
 
 int distinct_merge(DistinctState* d, const void* keys_dev, const int64_t* hash_dev, int64_t n,
                    hipStream_t st) {
+    if (n > 0)
+        if (int rc = distinct_finalize(d, st)) return rc;
     int64_t off = 0;
     while (off < n) {  // chunks that fit the merge buffer
         const int64_t c = std::min<int64_t>(n - off, d->cand_limit);
@@ -1287,6 +1412,10 @@ int distinct_merge(DistinctState* d, const void* keys_dev, const int64_t* hash_d
         d->rep.reset(d->k);
         for (int64_t i = 0; i < d->m; ++i) d->rep.sample(d->kw == 8 ? kk[(size_t)i] : (int64_t)k4[(size_t)i], hh[(size_t)i]);
         d->max_h = d->rep.max_hash;
+        d->segs.clear();  // the replica starts over from the union: the set arrays are its set
+        d->log_n = 0;
+        d->over = false;
+        d->exact = true;
     }
     return RSV_OK;
 }

@@ -136,6 +136,9 @@ void distinct_destroy(DistinctState* d);
 int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* hashes, int64_t n,
                            hipStream_t st);
 int64_t distinct_size(const DistinctState* d);
+// RSV_DISTINCT_ORDERED: bring the set arrays to the reference's set (host replay of the logged
+// candidates when the tie bucket requires it); a no-op otherwise.  Before size / export / publish.
+int distinct_finalize(DistinctState* d, hipStream_t st);
 const void* distinct_keys_dev(const DistinctState* d);  // the current set's keys (m of them)
 // the set's m keys into coherent host memory (device-mapped pointer) + flag = gen
 int distinct_publish(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st);

@@ -679,6 +679,7 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
     int64_t m;
     const void* src;
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
+        if (int rc = distinct_finalize(s->distinct, s->stream)) return (rsv_status)rc;
         m = distinct_size(s->distinct);
         if (m > cap) return fail(RSV_E_ILLEGAL_ARGUMENT, "result buffer too small");
         if (m && !out) return fail(RSV_E_NULL_POINTER, "out is NULL");
@@ -835,6 +836,7 @@ rsv_status rsv_export_state(rsv_sampler* s, int64_t* idx_dev, void* keys_dev, in
     touch(s);
     if (rsv_status st = flush_stage(s)) return st;
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
+        if (int rc = distinct_finalize(s->distinct, s->stream)) return (rsv_status)rc;
         if (int rc = distinct_export(s->distinct, keys_dev, hash_dev, s->stream)) return (rsv_status)rc;
         *out_n = distinct_size(s->distinct);
     } else {

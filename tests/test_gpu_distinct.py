@@ -207,6 +207,53 @@ def test_ordered_reusable_and_merge(cuda, oracle):
     assert outs[0] == outs[1] and len(outs[0]) == 256
 
 
+@pytest.mark.parametrize("buckets", [200_000, 1_000_000])
+def test_ordered_sparse_collisions_many_seeds(cuda, oracle, buckets):
+    """Long.hashCode with few collisions (~0.1-0.5 elements per hash value): across seeds the
+    boundary bucket is sometimes oversubscribed (the set depends on the heap's tie choice: host
+    replay of the logged candidates) and mostly not (the device bottom-k is the reference's set
+    as is).  Both must match the reference, in one batch and in several with result() between."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    for seed in range(12):
+        rng = np.random.default_rng(1000 + seed)
+        vals = _colliding(rng, 60_000, buckets)
+        vals = np.concatenate([vals, vals[rng.integers(0, vals.size, 20_000)]])
+        ref = oracle.Distinct(64, seed, oracle.HASH_JAVA_LONG)
+        ref.sample_all(vals)
+        d = Sampler.distinct(64, seed=seed)()
+        d.sample_all(torch.from_numpy(vals).to(cuda))
+        assert d.result().tolist() == ref.result()[0].tolist(), seed
+        ref = oracle.Distinct(64, seed, oracle.HASH_JAVA_LONG)
+        r = Sampler.distinct(64, seed=seed, reusable=True)()
+        for part in np.array_split(vals, 5):
+            r.sample_all(part)
+            ref.sample_all(part)
+            assert r.result().tolist() == ref.result()[0].tolist(), seed
+
+
+def test_ordered_eager_log_replay(cuda, oracle, monkeypatch):
+    """A candidate log at its limit is replayed into the host replica before the next chunk
+    (RSV_ORDERED_LOG_LIMIT: test hook, read at creation); the result is unchanged."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    monkeypatch.setenv("RSV_ORDERED_LOG_LIMIT", "1")
+    rng = np.random.default_rng(5)
+    vals = _colliding(rng, 400_000, 4000)
+    ref = oracle.Distinct(300, 17, oracle.HASH_JAVA_LONG)
+    ref.sample_all(vals)
+    want = ref.result()[0].tolist()
+    for parts in (1, 6):
+        d = Sampler.distinct(300, seed=17)()
+        for part in np.array_split(vals, parts):
+            d.sample_all(torch.from_numpy(part).to(cuda))
+        assert d.result().tolist() == want
+
+
 def test_precomputed_hash(cuda, oracle):
     from reservoir_amd import Sampler
 

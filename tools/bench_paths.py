@@ -145,6 +145,8 @@ def main():
         print(json.dumps(c4(dev, "default", "set")), flush=True)
         print(json.dumps(c4(dev, "default")), flush=True)  # auto -> ordered (exact ties)
         torch.cuda.empty_cache()
+    if "c4o" in todo:  # default hash, auto -> ordered only (for traces)
+        print(json.dumps(c4(dev, "default")), flush=True)
     if "c4i" in todo:  # identity hash only (for traces)
         print(json.dumps(c4(dev, "identity")), flush=True)
     if "c2l" in todo:
