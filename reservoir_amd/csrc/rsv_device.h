@@ -55,6 +55,40 @@ __device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_
     return {c0, c1, c2, c3};
 }
 
+// The same function when counter words 1..3 are wave-uniform (c0 per lane): round 0's first output
+// and round 1's first product are then scalar (SALU, hoisted out of any loop over c0), and round
+// 1's xors take one scalar operand each -- 18 v_mad_u64_u32 + 1 v_bitop3 + 2 v_xor per call
+// instead of 19 + 20 (the asm xor3 forces VGPR operands, so the uniform part must stay in C).
+__device__ __forceinline__ u32x4 philox4x32_10_uniform_hi(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                          uint32_t k0, uint32_t k1) {
+    // round 0
+    const uint64_t p1u = (uint64_t)kPhiloxM1 * c2;                  // scalar
+    const uint32_t n0u = (uint32_t)(p1u >> 32) ^ c1 ^ k0;           // scalar
+    const uint64_t p0 = (uint64_t)kPhiloxM0 * c0;                   // vector
+    uint32_t d2 = xor3_key((uint32_t)(p0 >> 32), c3, k1);           // vector (c3 ^ k1 is scalar)
+    const uint32_t d1u = (uint32_t)p1u;                             // scalar
+    uint32_t d3 = (uint32_t)p0;                                     // vector
+    // round 1
+    const uint64_t q0u = (uint64_t)kPhiloxM0 * n0u;                 // scalar
+    const uint64_t q1 = (uint64_t)kPhiloxM1 * d2;                   // vector
+    uint32_t c0v = (uint32_t)(q1 >> 32) ^ (d1u ^ (k0 + kPhiloxW0));  // one scalar operand
+    uint32_t c2v = d3 ^ ((uint32_t)(q0u >> 32) ^ (k1 + kPhiloxW1));  // one scalar operand
+    uint32_t c1v = (uint32_t)q1;
+    uint32_t c3v = (uint32_t)q0u;  // scalar until round 2 (its product's operand is c2v)
+#pragma unroll
+    for (int r = 2; r < 10; ++r) {
+        const uint64_t p0r = (uint64_t)kPhiloxM0 * c0v;
+        const uint64_t p1r = (uint64_t)kPhiloxM1 * c2v;
+        const uint32_t n0 = xor3_key((uint32_t)(p1r >> 32), c1v, k0 + (uint32_t)r * kPhiloxW0);
+        const uint32_t n2 = xor3_key((uint32_t)(p0r >> 32), c3v, k1 + (uint32_t)r * kPhiloxW1);
+        c0v = n0;
+        c1v = (uint32_t)p1r;
+        c2v = n2;
+        c3v = (uint32_t)p0r;
+    }
+    return {c0v, c1v, c2v, c3v};
+}
+
 struct DrawKey {
     uint32_t k0, k1;  // Philox key = seed
     uint32_t s0, s1;  // Philox stream words (counter words 2, 3)

@@ -375,8 +375,11 @@ hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, 
     if (hi <= lo) return hipSuccess;
     const uint64_t g_end = (hi + 15) >> 4;
     constexpr uint64_t kMaxGroups = 1ull << 31;  // block offsets are 32-bit queue entries
-    for (uint64_t g_begin = lo >> 4; g_begin < g_end; g_begin += kMaxGroups) {
-        const uint64_t n_groups = std::min<uint64_t>(g_end - g_begin, kMaxGroups);
+    uint64_t n_groups = 0;
+    for (uint64_t g_begin = lo >> 4; g_begin < g_end; g_begin += n_groups) {
+        // and no launch crosses a multiple of 2^32 blocks: the counter's high word is a scalar
+        const uint64_t g_wrap = ((g_begin >> 32) + 1) << 32;
+        n_groups = std::min<uint64_t>(std::min<uint64_t>(g_end, g_wrap) - g_begin, kMaxGroups);
         // two resident rounds of 4-wave workgroups (8 waves per SIMD): measured best (tools/micro_k1)
         const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 16);
         hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,

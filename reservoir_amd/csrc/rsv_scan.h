@@ -236,15 +236,20 @@ __device__ __forceinline__ void k1_body_bits(const DrawKey& dk, uint32_t k, uint
     const uint32_t stride = gridDim.x * blockDim.x * U;
     uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
     // per-lane level-0 counter kept in VGPRs and stepped by `stride` (rebuilding it from a
-    // scalar base every iteration made the compiler pad SALU->VALU hazards with 15 s_nop)
-    uint64_t gl = g_begin + base + lane;
+    // scalar base every iteration made the compiler pad SALU->VALU hazards with 15 s_nop).  The
+    // launch never crosses a multiple of 2^32 blocks (launch_k1_last_writer splits there), so the
+    // counter's high word is one scalar for the whole launch: Philox round 0's first output and
+    // round 1's first product are then wave-uniform and leave the VALU (19 -> 18 v_mad_u64_u32 and
+    // 20 -> 19 v_bitop3 per block); only the low word is carried per lane.
+    const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g_begin >> 32));
+    uint32_t gl = (uint32_t)g_begin + base + lane;
     while (base < ng) {  // wave-uniform
         const uint32_t base0 = base;
         uint32_t bits = 0;
         for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride) {
             u32x4 w[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) w[u] = level0(dk, gl + u * 64);
+            for (int u = 0; u < U; ++u) w[u] = philox4x32_10_uniform_hi(gl + u * 64, ghi, dk.s0, dk.s1, dk.k0, dk.k1);
             if (base >= off_sparse && base + U * 64 <= ng) {  // steady state: zero-byte test only
 #pragma unroll
                 for (int u = 0; u < U; ++u) bits |= (uint32_t)any_zero_byte(w[u]) << (t * U + u);

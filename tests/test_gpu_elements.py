@@ -254,9 +254,11 @@ def test_full_size_split_invariance(cuda):
 
 
 @pytest.mark.parametrize("i0,k,n", [(2**32 - 100, 1024, 1_000_000), (5 * 10**9, 65_536, 2_000_000),
-                                    (2**40 + 3, 1 << 20, 8_000_000)])
+                                    (2**40 + 3, 1 << 20, 8_000_000), (2**36 - 3_000_001, 1 << 20, 6_000_000)])
 def test_high_index_offsets(cuda, oracle, i0, k, n):
-    """Ranks beyond the first 2^32 indices (8-GPU C2 reaches 8e9): 64-bit draw arithmetic."""
+    """Ranks beyond the first 2^32 indices (8-GPU C2 reaches 8e9): 64-bit draw arithmetic.  The
+    last case crosses index 2^36 = level-0 block 2^32, where K1 splits its launch (the Philox
+    counter's high word is a per-launch scalar)."""
     import ctypes as C
 
     import torch
