@@ -599,10 +599,16 @@ __global__ __launch_bounds__(kBlock) void bucket_emit(int64_t m, int64_t cand_ca
     }
 }
 
-// ctl[0..5] -> coherent host memory + flag (one wave; the host spins instead of a stream sync)
-__global__ __launch_bounds__(64) void ctl_publish(const int64_t* __restrict__ ctl, int64_t* dst, uint32_t* flag,
+// ctl[0..5] -> coherent host memory + flag (one wave; the host spins instead of a stream sync);
+// then the candidate counter and overflow word are re-armed for the next filter pass (each lane
+// clears only the word it read itself, so the copy sees the old value)
+__global__ __launch_bounds__(64) void ctl_publish(int64_t* __restrict__ ctl, int64_t* dst, uint32_t* flag,
                                                   uint32_t gen) {
-    if (threadIdx.x < 6) dst[threadIdx.x] = ctl[threadIdx.x];
+    if (threadIdx.x < 6) {
+        const int64_t v = ctl[threadIdx.x];
+        dst[threadIdx.x] = v;
+        if (threadIdx.x < 2) ctl[threadIdx.x] = 0;
+    }
     publish_flag(flag, gen);
 }
 
@@ -901,7 +907,7 @@ static unsigned span_bits(int64_t top) {
 static hipError_t read_ctl(DistinctState* d, int64_t* out, hipStream_t st) {
     const uint32_t gen = ++d->hc_gen;
     uint32_t* flag = (uint32_t*)(d->hc + 8);
-    hipLaunchKernelGGL(ctl_publish, dim3(1), dim3(64), 0, st, (const int64_t*)d->ctl, d->hc_dev,
+    hipLaunchKernelGGL(ctl_publish, dim3(1), dim3(64), 0, st, d->ctl, d->hc_dev,
                        (uint32_t*)(d->hc_dev + 8), gen);
     if (hipError_t e = hipGetLastError()) return e;
     const auto t0 = std::chrono::steady_clock::now();
@@ -1297,7 +1303,12 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
             const double rate = (double)d->rate_c / (double)d->rate_m * (span_now / d->rate_span);
             m = (int64_t)std::min<double>(std::max<double>(0.75 * (double)ccap / rate, 65536.0), (double)(1ll << 31));
         } else {
-            m = std::max<int64_t>(d->seen, 65536);
+            // first chunk at a full heap: a distinct element passes with probability ~ the span
+            // below the threshold (the scrambled hash is uniform); repeats of members pass too,
+            // so aim at half the usual target (an overflow only costs a shorter retry)
+            const double frac = ((double)((uint64_t)tinc - (uint64_t)INT64_MIN) + 1.0) / 18446744073709551616.0;
+            m = (int64_t)std::min<double>(std::max<double>(0.375 * (double)ccap / std::max(frac, 1e-18), 65536.0),
+                                          (double)(1ll << 31));
         }
         m = std::min(std::min(m, n - pos), std::min<int64_t>(full ? ((int64_t)1 << 31) : ccap, (int64_t)1 << 31));
         if (d->log_n + ccap > d->log_limit && !d->segs.empty()) OTRY(replay_log<KeyT>(d, st));
@@ -1305,7 +1316,7 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
         int64_t* lh = d->log_h + d->log_n;
         KeyT* lk = (KeyT*)d->log_k + d->log_n;
         const bool bucketed = d->log_bmax >= 0 && d->set_cap >= k;
-        OTRY(hipMemsetAsync(d->ctl, 0, 16, st));  // candidate counter, overflow
+        // candidate counter and overflow word: zeroed at creation and re-armed by every read_ctl
         if (d->timer) d->timer->mark(st);
         OTRY(launch_filter_idx<KeyT>(d, keys + pos, hashes ? hashes + pos : nullptr, m, tinc, lh, lk,
                                      d->log_i + d->log_n, ccap, st));
