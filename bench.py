@@ -277,7 +277,7 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": load_traffic(n),
-                "kernel": "k1_last_writer",
+                "kernel": "k1_resolve_publish",
                 "launch_avg_us": round(k1_s * 1e6, 2),
                 "launches_timed": prof[1],
                 "note": "achieved charges 8 B per element (SURVEY.md 8(d)); K1 reads no key "

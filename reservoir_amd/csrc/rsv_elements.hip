@@ -36,6 +36,77 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
     k1_body_bits<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
 }
 
+// K1 + resolve_publish in one dispatch (single-launch batches, k <= kK1FusedMaxK): every
+// workgroup takes a ticket after its winner atomics; the last one -- which then sees all of them --
+// runs the resolve over the k slots (all loads of a lane issued before any store) and publishes
+// the reservoir into coherent host memory, then re-arms the ticket.  Saves the kernel boundary
+// and the resolve dispatch of the two-kernel form.
+constexpr uint32_t kK1FusedMaxK = 8 * kBlock;
+
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void k1_resolve_publish(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi,
+                                                             uint64_t g_begin, uint64_t n_groups,
+                                                             unsigned long long* __restrict__ win,
+                                                             uint32_t* ticket, const KeyT* __restrict__ keys,
+                                                             int64_t base, int64_t n, KeyT* __restrict__ slot_key,
+                                                             int64_t* __restrict__ slot_idx, int fresh, int64_t m,
+                                                             KeyT* dst, uint32_t* flag, uint32_t gen) {
+    __shared__ uint32_t qs[kBlock / 64][63 + 64 + 1];
+    __shared__ uint64_t cqs[kBlock / 64][kQueue];
+    __shared__ uint32_t last;
+    k1_body_bits<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
+    // This wave's winner atomics are performed (acknowledged by the device-coherent L2 side) once
+    // vmcnt drains; K1 makes no plain global stores, so no L2 write-back is needed before the
+    // ticket.  An agent-scope release/acquire fence here costs a buffer_wbl2 per wave and a
+    // buffer_inv per workgroup: measured 112 -> 211 us per launch at C2.  Only the last
+    // workgroup acquires (one L2 invalidate) before it reads the winners.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == gridDim.x - 1;
+        if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;  // workgroup-uniform
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    constexpr int R = kK1FusedMaxK / kBlock;
+    unsigned long long wi[R];
+    KeyT v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t j = threadIdx.x + r * kBlock;
+        wi[r] = j < k ? __hip_atomic_load(&win[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t j = threadIdx.x + r * kBlock;
+        if (j >= k) continue;
+        if (wi[r]) v[r] = keys[(int64_t)wi[r] - base];
+        else if (j >= base && j < base + n) v[r] = keys[j - base];
+        else if (fresh) v[r] = 0;
+        else v[r] = slot_key[j];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t j = threadIdx.x + r * kBlock;
+        if (j >= k) continue;
+        if (wi[r]) {
+            slot_key[j] = v[r];
+            slot_idx[j] = (int64_t)wi[r];
+            win[j] = 0;
+        } else if (j >= base && j < base + n) {
+            slot_key[j] = v[r];
+            slot_idx[j] = j;
+        } else if (fresh) {
+            slot_key[j] = 0;
+            slot_idx[j] = -1;
+        }
+        if (j < m) dst[j] = v[r];
+    }
+    publish_flag(flag, gen);
+}
+
 // Per slot j: the batch's last writer (win[j], then cleared), else the fill of j < k from this
 // batch, else -- first batch of a handle whose slots were never initialised (`fresh`) -- empty.
 template <typename KeyT>
@@ -390,6 +461,32 @@ hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, 
     return hipSuccess;
 }
 
+bool k1_fused_ok(uint64_t lo, uint64_t hi, uint32_t k, int key_width) {
+    if (hi <= lo || k > kK1FusedMaxK || (key_width != 8 && key_width != 4)) return false;
+    const uint64_t g_begin = lo >> 4, g_end = (hi + 15) >> 4;
+    // one launch of launch_k1_last_writer: no 2^32-block crossing, fewer than 2^31 blocks
+    return g_end - g_begin <= (1ull << 31) && g_end <= ((g_begin >> 32) + 1) << 32;
+}
+
+hipError_t launch_k1_resolve_publish(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
+                                     unsigned long long* batch_win, uint32_t* ticket, const void* keys,
+                                     int key_width, int64_t base, int64_t n, void* slot_key, int64_t* slot_idx,
+                                     bool fresh, int64_t m, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen,
+                                     hipStream_t st) {
+    if (!k1_fused_ok(lo, hi, k, key_width)) return hipErrorInvalidValue;
+    const uint64_t g_begin = lo >> 4, n_groups = ((hi + 15) >> 4) - g_begin;
+    const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 16);
+    if (key_width == 8)
+        hipLaunchKernelGGL(k1_resolve_publish<int64_t>, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
+                           g_begin, n_groups, batch_win, ticket, (const int64_t*)keys, base, n, (int64_t*)slot_key,
+                           slot_idx, (int)fresh, m, (int64_t*)dst_host_dev, flag_dev, gen);
+    else
+        hipLaunchKernelGGL(k1_resolve_publish<int32_t>, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
+                           g_begin, n_groups, batch_win, ticket, (const int32_t*)keys, base, n, (int32_t*)slot_key,
+                           slot_idx, (int)fresh, m, (int32_t*)dst_host_dev, flag_dev, gen);
+    return hipGetLastError();
+}
+
 hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,
                           unsigned long long* batch_win, void* slot_key, int64_t* slot_idx, bool fresh,
                           hipStream_t st) {
@@ -411,8 +508,9 @@ hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t
 
 // fresh handle: batch_win = 0, slot_idx = -1 (empty), slot_key = 0
 __global__ __launch_bounds__(kBlock) void init_slots_kernel(uint8_t* slot_key, int key_width, int64_t* slot_idx,
-                                                            unsigned long long* win, uint32_t k) {
+                                                            unsigned long long* win, uint32_t k, uint32_t* ticket) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    if (ticket && blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += stride) {
         win[j] = 0;
         slot_idx[j] = -1;
@@ -426,10 +524,10 @@ __global__ __launch_bounds__(kBlock) void init_slots_kernel(uint8_t* slot_key, i
 }
 
 hipError_t launch_init_slots(void* slot_key, int key_width, int64_t* slot_idx, unsigned long long* win, uint32_t k,
-                             hipStream_t st) {
+                             hipStream_t st, uint32_t* ticket) {
     const unsigned grid = (unsigned)std::min<uint64_t>((k + kBlock - 1) / kBlock, 256 * 64);
     hipLaunchKernelGGL(init_slots_kernel, dim3(grid), dim3(kBlock), 0, st, (uint8_t*)slot_key, key_width, slot_idx,
-                       win, k);
+                       win, k, ticket);
     return hipGetLastError();
 }
 

@@ -83,10 +83,19 @@ struct DrawParams {
 // batch_win[k] (0 = no writer in this batch; atomicMax keeps the largest index).
 hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
                                  unsigned long long* batch_win, hipStream_t st);
+// K1 + resolve_publish as one dispatch (see launch_resolve_publish), when k1_fused_ok: a batch
+// whose range K1 covers in one launch, k <= 2048, 4- or 8-byte keys.  ticket: a zeroed device
+// word, re-armed by the launch.
+bool k1_fused_ok(uint64_t lo, uint64_t hi, uint32_t k, int key_width);
+hipError_t launch_k1_resolve_publish(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
+                                     unsigned long long* batch_win, uint32_t* ticket, const void* keys,
+                                     int key_width, int64_t base, int64_t n, void* slot_key, int64_t* slot_idx,
+                                     bool fresh, int64_t m, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen,
+                                     hipStream_t st);
 // Resolve: fill phase for slots in [base, base+n) and winners of batch_win; resets batch_win.
-// slot_idx may be null.
+// slot_idx may be null.  init_slots also zeroes `ticket` when non-null.
 hipError_t launch_init_slots(void* slot_key, int key_width, int64_t* slot_idx, unsigned long long* win, uint32_t k,
-                             hipStream_t st);
+                             hipStream_t st, uint32_t* ticket = nullptr);
 hipError_t launch_publish(const void* src, int64_t bytes, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen,
                           hipStream_t st);
 // the same from up to 32 workgroups (large buffers); ticket_dev: a zeroed device word, re-armed

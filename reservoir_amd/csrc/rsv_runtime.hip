@@ -3,6 +3,7 @@
 // per-element calls into pinned batches, host->device batching, engine dispatch, multi-GPU
 // state export/merge.  All data-parallel work runs in the kernels of rsv_elements.hip and
 // rsv_distinct.hip; there is no CPU compute path.
+#include <cstdlib>
 #include <string.h>
 
 #include <algorithm>
@@ -109,7 +110,7 @@ struct rsv_sampler {
     int kw = 8;
     uint32_t k = 0;
     // ELEMENTS
-    void* slots = nullptr;  // one pooled block: batch_win[k] | slot_idx[k] | slot_key[k]
+    void* slots = nullptr;  // one pooled block: batch_win[k] | slot_idx[k] | slot_key[k] | k1_ticket
     // device-state knowledge, in stream order: batch_win all zero (resolve leaves it so) / slot
     // arrays initialised.  Creation enqueues no device work; the first batch initialises.
     bool win_zero = false;
@@ -117,6 +118,7 @@ struct rsv_sampler {
     void* slot_key = nullptr;
     int64_t* slot_idx = nullptr;
     unsigned long long* batch_win = nullptr;
+    uint32_t* k1_ticket = nullptr;  // fused K1 + resolve_publish: zero between launches
     AlgoLState algo_l;
     std::vector<int64_t> ev_pos_h;
     std::vector<int32_t> ev_slot_h;
@@ -254,7 +256,7 @@ rsv_status ensure_events(rsv_sampler* s, int64_t n) {
 rsv_status ensure_slots(rsv_sampler* s) {
     if (s->slots_init || s->cfg.kind != RSV_KIND_ELEMENTS) return RSV_OK;
     touch(s);
-    RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream));
+    RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream, s->k1_ticket));
     s->slots_init = s->win_zero = true;
     s->pub_valid = false;
     return RSV_OK;
@@ -349,7 +351,7 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
     bool fresh = false;
     if (s->cfg.kind == RSV_KIND_ELEMENTS) {
         if (!s->win_zero) {  // never-used block: full init
-            RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream));
+            RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream, s->k1_ticket));
             s->slots_init = s->win_zero = true;
         }
         fresh = !s->slots_init;
@@ -376,10 +378,33 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
     } else {
         const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
         const uint64_t lo = std::max<uint64_t>((uint64_t)base, s->k), hi = (uint64_t)(base + n);
-        const bool pm = prof_begin(s, s->stream);
-        RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
-        prof_end(s, s->stream, pm);
-        if (rsv_status st = resolve_batch(s, keys, base, n, fresh)) return st;
+        // RSV_K1_FUSE=0 keeps the two-dispatch form (A/B measurements)
+        static const bool fuse_on = [] {
+            const char* e = std::getenv("RSV_K1_FUSE");
+            return !(e && e[0] == '0');
+        }();
+        const bool fuse = fuse_on && k1_fused_ok(lo, hi, s->k, s->kw);
+        if (fuse) {
+            if (rsv_status st = ensure_result_buffer(s)) return st;
+        }
+        if (fuse && s->result_publish) {
+            // one dispatch: K1, then the last workgroup resolves and publishes (resolve_batch's form)
+            const uint32_t gen = ++s->result_gen;
+            const int64_t m = std::min<int64_t>(base + n, (int64_t)s->k);
+            const bool pm = prof_begin(s, s->stream);
+            RSV_HIP_TRY(launch_k1_resolve_publish(dp, s->k, lo, hi, s->batch_win, s->k1_ticket, keys, s->kw, base, n,
+                                                  s->slot_key, s->slot_idx, fresh, m, s->result_dev,
+                                                  s->result_flag_dev, gen, s->stream));
+            prof_end(s, s->stream, pm);
+            s->pub_ops = s->ops;
+            s->pub_gen = gen;
+            s->pub_valid = true;
+        } else {
+            const bool pm = prof_begin(s, s->stream);
+            RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
+            prof_end(s, s->stream, pm);
+            if (rsv_status st = resolve_batch(s, keys, base, n, fresh)) return st;
+        }
     }
     if (s->cfg.kind == RSV_KIND_ELEMENTS) s->slots_init = s->win_zero = true;
     s->count = base + n;
@@ -531,11 +556,12 @@ rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out) {
         if (s->slots)
             s->win_zero = true;
         else
-            e = pool_device_alloc(&s->slots, k * 16 + ((k * s->kw + 7) & ~(size_t)7));
+            e = pool_device_alloc(&s->slots, k * 16 + ((k * s->kw + 7) & ~(size_t)7) + 8);
         if (e == hipSuccess) {
             s->batch_win = (unsigned long long*)s->slots;
             s->slot_idx = (int64_t*)((uint8_t*)s->slots + k * 8);
             s->slot_key = (uint8_t*)s->slots + k * 16;
+            s->k1_ticket = (uint32_t*)((uint8_t*)s->slots + k * 16 + ((k * s->kw + 7) & ~(size_t)7));
         }
         if (e != hipSuccess)
             return bail(e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE,

@@ -19,7 +19,7 @@ if [ -n "$PMC" ]; then
   done
 fi
 if [ -n "$PMC" ]; then
-  python tools/pmc_summary.py k1_last_writer 1000000000 gpurun_out/pmc_k1.json \
+  python tools/pmc_summary.py k1_resolve_publish 1000000000 gpurun_out/pmc_k1.json \
     gpurun_out/pmc_FETCH_SIZE/pmc_counter_collection.csv gpurun_out/pmc_WRITE_SIZE/pmc_counter_collection.csv
 fi
 find gpurun_out/prof -name "*.csv" 2>/dev/null || true

@@ -31,6 +31,6 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
         python3 tools/bench_paths.py --only c4i
 done
 f() { find "$O/$1" -name "*counter_collection.csv" | head -1; }
-python tools/pmc_summary.py k1_last_writer 1000000000 "$O/pmc_k1.json" "$(f pmc_k1_FETCH_SIZE)" "$(f pmc_k1_WRITE_SIZE)"
+python tools/pmc_summary.py k1_resolve_publish 1000000000 "$O/pmc_k1.json" "$(f pmc_k1_FETCH_SIZE)" "$(f pmc_k1_WRITE_SIZE)"
 python tools/pmc_summary.py k3_filter 500000000 "$O/pmc_k3.json" "$(f pmc_c4_FETCH_SIZE)" "$(f pmc_c4_WRITE_SIZE)"
 find "$O" -name "*stats.csv"

@@ -316,3 +316,31 @@ def test_recycled_handle_resources(cuda, oracle, kt):
         assert got.size == m
         assert np.array_equal(got, want[:m].astype(dt))
         s.close()
+
+
+@pytest.mark.parametrize("kt", ["long", "int"])
+def test_fused_k1_resolve_publish(cuda, oracle, kt):
+    """Batches that K1 covers in one launch with k <= 2048 run as one dispatch whose last
+    workgroup resolves and publishes (rsv_elements.hip k1_resolve_publish); k = 2049 takes the
+    two-kernel form.  The completion ticket is re-armed by every launch: back-to-back samplers
+    of different grid sizes, batches inside and across the fill phase, all equal the oracle."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    dt = np.int64 if kt == "long" else np.int32
+    rng = np.random.default_rng(7)
+    for it in range(24):
+        k = [1, 64, 1000, 2047, 2048, 2049][it % 6]
+        n = int(rng.integers(0, 3 * 10**6)) if it % 4 else int(rng.integers(0, 3 * k))
+        keys = oracle.splitmix_keys(70_000 + it, n).astype(dt)
+        want, _ = oracle.algo_r(555 + it, it, k, keys.astype(np.int64))
+        s = Sampler(k, seed=555 + it, stream_id=it, key_type=kt)()
+        kd = _dev_keys(torch, cuda, keys)
+        cuts = np.r_[0, np.sort(rng.choice(np.arange(0, n + 1), 3)), n]
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            if b > a:
+                s.sample_all(kd[a:b])
+        got = s.result()
+        assert got.size == min(n, k)
+        assert np.array_equal(got, want[: got.size].astype(dt)), (it, k, n)
