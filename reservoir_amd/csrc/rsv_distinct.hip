@@ -1080,7 +1080,8 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
         }
         // the merge needs the set arrays at their full size (set_h/set_k are written by rank)
         const bool bucketed = d->log_bmax >= 0 && d->set_cap >= d->k;
-        DTRY(hipMemsetAsync(d->ctl, 0, 16, st));  // candidate counter, overflow
+        // candidate counter and overflow word: zeroed at creation and re-armed by every read_ctl
+        // (ctl_publish), so no memset dispatch ahead of the filter
         if (d->timer) d->timer->mark(st);
         DTRY(launch_filter<KeyT>(d, keys, hashes, n, tinc, st));
         if (d->timer) d->timer->mark(st);
