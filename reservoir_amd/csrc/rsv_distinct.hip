@@ -612,6 +612,33 @@ __global__ __launch_bounds__(64) void ctl_publish(int64_t* __restrict__ ctl, int
     publish_flag(flag, gen);
 }
 
+// Speculative publication of a set-mode merge (large batches): as publish_multi_kernel, but the
+// set's size is read on the device (ctl[2], the merged distinct count, capped at k), so the host
+// enqueues it right behind ctl_publish and it runs while the host turns the ctl read around.  The
+// host uses it only if that merge turns out to be the batch's last (distinct_spec_take).
+__global__ __launch_bounds__(1024) void publish_set_kernel(const uint32_t* __restrict__ src, uint32_t* dst,
+                                                           const int64_t* __restrict__ ctl, int64_t k,
+                                                           int32_t key_words, uint32_t* flag, uint32_t gen,
+                                                           uint32_t* ticket) {
+    const int64_t words = std::min<int64_t>(ctl[2], k) * key_words;
+    const int64_t vecs = words >> 2;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = t0; i < vecs; i += stride) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    for (int64_t i = (vecs << 2) + t0; i < words; i += stride) dst[i] = src[i];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        const uint32_t prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence_system();
+            __hip_atomic_store(flag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 inline unsigned grid_1d(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 }  // namespace
@@ -627,6 +654,14 @@ struct DistinctState {
     int64_t* set_h = nullptr;     // [set_cap <= k], ascending (h, key)
     void* set_k = nullptr;
     int64_t set_cap = 0;
+    // speculative set publication (set mode, batches >= kSpecMinBatch): target from the runtime
+    void* spec_dst = nullptr;     // coherent host buffer (device alias)
+    uint32_t* spec_flag = nullptr;
+    uint32_t* spec_gen_ctr = nullptr;  // the handle's publication generation counter
+    bool spec_arm = false;        // read_ctl enqueues publish_set_kernel behind ctl_publish
+    bool spec_ok = false;         // the last enqueued publication holds the batch's final set
+    uint32_t spec_gen = 0;
+    int64_t spec_min = 1ll << 27;  // smallest batch that publishes speculatively (~180 us of filter)
     int64_t cand_limit = 0;       // 4k + 4096: the most candidates one filter pass may keep
     int64_t cand_cap = 0;         // allocated (grows on demand up to cand_limit)
     int64_t* cand_h = nullptr;
@@ -774,6 +809,8 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
     d->log_limit = std::max<int64_t>(d->cand_limit, std::min<int64_t>(std::max<int64_t>(32 * d->cand_limit, 1 << 22), 1 << 27));
     if (const char* v = std::getenv("RSV_ORDERED_LOG_LIMIT"))  // test hook: force eager replays
         d->log_limit = std::max<int64_t>(d->cand_limit, std::atoll(v));
+    if (const char* v = std::getenv("RSV_SPEC_MIN_BATCH"))  // test hook: speculative publication
+        d->spec_min = std::max<int64_t>(1, std::atoll(v));
     hipError_t e = hipSuccess;
     auto A = [&](void** p, size_t bytes) {
         if (e == hipSuccess) e = pool_device_alloc(p, bytes ? bytes : 16);
@@ -836,6 +873,22 @@ void distinct_destroy(DistinctState* d) {
 
 int64_t distinct_size(const DistinctState* d) { return d->m; }
 const void* distinct_keys_dev(const DistinctState* d) { return d->set_k; }
+
+void distinct_spec_target(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t* gen_counter) {
+    if (d->ordered || d->log_bmax < 0) return;  // set mode with the bucketed merge only
+    d->spec_dst = dst_host_dev;
+    d->spec_flag = flag_dev;
+    d->spec_gen_ctr = gen_counter;
+    d->spec_ok = false;
+}
+
+bool distinct_spec_take(DistinctState* d, uint32_t* gen) {
+    const bool ok = d->spec_ok && d->spec_dst;
+    if (ok) *gen = d->spec_gen;
+    d->spec_dst = nullptr;
+    d->spec_arm = d->spec_ok = false;
+    return ok;
+}
 
 int distinct_publish(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st) {
     RSV_HIP_TRY(launch_publish_multi(d->set_k, d->m * d->kw, dst_host_dev, flag_dev, gen, (uint32_t*)(d->ctl + 4), st));
@@ -910,6 +963,18 @@ static hipError_t read_ctl(DistinctState* d, int64_t* out, hipStream_t st) {
     hipLaunchKernelGGL(ctl_publish, dim3(1), dim3(64), 0, st, d->ctl, d->hc_dev,
                        (uint32_t*)(d->hc_dev + 8), gen);
     if (hipError_t e = hipGetLastError()) return e;
+    if (d->spec_arm) {  // behind ctl_publish (which re-arms ctl[0..1]; the kernel reads ctl[2])
+        d->spec_arm = false;
+        const uint32_t g = ++*d->spec_gen_ctr;
+        const int64_t per = 32 * 1024;  // bytes per workgroup, as launch_publish_multi
+        const unsigned grid =
+            (unsigned)std::min<int64_t>(32, std::max<int64_t>(1, ((int64_t)d->k * d->kw + per - 1) / per));
+        hipLaunchKernelGGL(publish_set_kernel, dim3(grid), dim3(1024), 0, st, (const uint32_t*)d->set_k,
+                           (uint32_t*)d->spec_dst, (const int64_t*)d->ctl, (int64_t)d->k, d->kw / 4, d->spec_flag,
+                           g, (uint32_t*)(d->ctl + 4));
+        if (hipError_t e = hipGetLastError()) return e;
+        d->spec_gen = g;
+    }
     const auto t0 = std::chrono::steady_clock::now();
     bool seen = false;
     for (uint32_t spin = 1;; ++spin) {
@@ -1035,6 +1100,7 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
             return _e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;   \
         }                                                                            \
     } while (0)
+    d->spec_ok = false;
     if (n <= 0) return RSV_OK;
     const bool full = d->m == d->k;
     // Set mode keeps the bottom-k by (h, key): an element tied with the current maximum hash can
@@ -1086,6 +1152,9 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
         DTRY(launch_filter<KeyT>(d, keys, hashes, n, tinc, st));
         if (d->timer) d->timer->mark(st);
         if (bucketed) DTRY(launch_bucket_merge<KeyT>(d, tinc, st));
+        // large batches: publish the merged set speculatively (used if this pass is the last)
+        const bool spec = bucketed && d->spec_dst && n >= d->spec_min;
+        d->spec_arm = spec;
         DTRY(read_ctl(d, d->h_pinned + 4, st));
         const int64_t c = d->h_pinned[4];
         if (c > d->cand_cap) {  // threshold too loose for the candidate buffer: tighten
@@ -1113,7 +1182,10 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
             DTRY(merge_into_set<KeyT>(d, d->cand_h, (const KeyT*)d->cand_k, c, &nd, st, tinc));
         }
         // exact once every batch element below the new k-th hash was a candidate
-        if (tinc >= t_allowed || (d->m == d->k && d->max_h <= tinc)) return RSV_OK;
+        if (tinc >= t_allowed || (d->m == d->k && d->max_h <= tinc)) {
+            d->spec_ok = spec && d->h_pinned[5] == 0;  // merged on the device: the publication holds it
+            return RSV_OK;
+        }
         // too tight: widen (the partial merge is harmless: bottom-k(bottom-k(S u C1) u C2) equals
         // bottom-k(S u C2) for C1 a subset of C2)
         if (ns == 0) {

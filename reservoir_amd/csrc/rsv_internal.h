@@ -151,6 +151,12 @@ int distinct_finalize(DistinctState* d, hipStream_t st);
 const void* distinct_keys_dev(const DistinctState* d);  // the current set's keys (m of them)
 // the set's m keys into coherent host memory (device-mapped pointer) + flag = gen
 int distinct_publish(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st);
+// Speculative publication (set mode, large batches): the next distinct_sample_device enqueues the
+// merged set's publication into dst_host_dev + flag_dev (generation ++*gen_counter) right behind
+// its ctl read; distinct_spec_take says whether the last one holds the batch's final set (its
+// generation in *gen) and clears the target.
+void distinct_spec_target(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t* gen_counter);
+bool distinct_spec_take(DistinctState* d, uint32_t* gen);
 // copies the set (ascending hash) to device buffers; either may be null
 int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStream_t st);
 // merge external (key, hash) entries (device) into the set

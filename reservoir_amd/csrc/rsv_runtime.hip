@@ -358,8 +358,18 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
         s->win_zero = false;  // until this batch's resolve is enqueued
     }
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
+        // set mode: large batches publish the merged set speculatively (distinct_spec_target)
+        if (rsv_status st = ensure_result_buffer(s)) return st;
+        if (s->result_publish) distinct_spec_target(s->distinct, s->result_dev, s->result_flag_dev, &s->result_gen);
         int rc = distinct_sample_device(s->distinct, keys, hashes, n, s->stream);
+        uint32_t gen = 0;
+        const bool published = distinct_spec_take(s->distinct, &gen);
         if (rc != RSV_OK) return (rsv_status)rc;
+        s->pub_valid = published;  // result() waits for it instead of publishing
+        if (published) {
+            s->pub_ops = s->ops;
+            s->pub_gen = gen;
+        }
     } else if (s->cfg.engine == RSV_ENGINE_JAVA_L) {
         s->ev_pos_h.clear();
         s->ev_slot_h.clear();
@@ -715,15 +725,24 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
             } else {
                 if (rsv_status st = ensure_result_buffer(s)) return st;
                 const void* set_k = distinct_keys_dev(s->distinct);
-                touch(s);
                 if (s->result_publish) {  // the set straight into coherent host memory + flag spin
-                    const uint32_t gen = ++s->result_gen;
-                    if (int rc = distinct_publish(s->distinct, s->result_dev, s->result_flag_dev, gen, s->stream))
-                        return (rsv_status)rc;
-                    s->pub_valid = false;  // the element publication state is not this one
+                    uint32_t gen = s->pub_gen;
+                    if (!(s->pub_valid && s->pub_ops == s->ops)) {  // no speculative publication of it
+                        touch(s);
+                        gen = ++s->result_gen;
+                        if (int rc = distinct_publish(s->distinct, s->result_dev, s->result_flag_dev, gen, s->stream))
+                            return (rsv_status)rc;
+                    }
+                    s->pub_valid = false;
                     if (rsv_status st = wait_flag(s, gen)) return st;
-                    s->ops_done = s->ops;
+                    // the publication was the handle's last work: no stream synchronize
+                    if (s->result_gen == gen) s->ops_done = s->ops;
+                    memcpy(out, s->result_h, (size_t)m * s->kw);
+                    *out_n = m;
+                    if (!s->cfg.reusable) s->open = false;
+                    return RSV_OK;
                 } else {
+                    touch(s);
                     RSV_HIP_TRY(hipMemcpyAsync(s->result_h, set_k, m * s->kw, hipMemcpyDeviceToHost, s->stream));
                     RSV_HIP_TRY(sync_stream(s));
                 }

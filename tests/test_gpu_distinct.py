@@ -406,3 +406,42 @@ def test_maximum_sample_size(cuda, oracle):
     ref = oracle.Distinct(1 << 20, 3, oracle.HASH_IDENTITY)  # k above the distinct count: all kept
     ref.sample_all(vals)
     assert np.array_equal(d.result(), ref.result()[0])
+
+
+@pytest.mark.parametrize("key_type", ["long", "int"])
+def test_set_mode_speculative_publication(cuda, oracle, monkeypatch, key_type):
+    """Set-mode batches of at least RSV_SPEC_MIN_BATCH keys (test hook, read at creation; the
+    product default is 2^27) publish the merged set right behind the ctl read, and result() only
+    waits for it.  Forced on every batch here: several batches, a reusable sampler read between
+    batches, threshold retries (heavy duplication), the few-hash-values slice fallback, and host
+    batches -- every result equals the oracle's."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    monkeypatch.setenv("RSV_SPEC_MIN_BATCH", "1")
+    dt = np.int64 if key_type == "long" else np.int32
+    hi = 2**31 - 1 if key_type == "int" else 2**62
+    rng = np.random.default_rng(21)
+    for k, n, uniq in [(1000, 2_000_000, 0.7), (65_536, 1_500_000, 0.05), (10, 5_000, 1.0)]:
+        base = rng.integers(-hi, hi, size=max(1, int(n * uniq)), dtype=np.int64)
+        vals = np.concatenate([base, base[rng.integers(0, base.size, size=n - base.size)]])
+        rng.shuffle(vals)
+        vals = vals.astype(dt)
+        d = Sampler.distinct(k, seed=23, key_type=key_type, reusable=True)(hash="identity")
+        ref = oracle.Distinct(k, 23, oracle.HASH_IDENTITY)
+        vd = torch.from_numpy(vals).to(cuda)
+        for part_i, (a, b) in enumerate([(0, n // 4), (n // 4, n // 2), (n // 2, n)]):
+            if part_i == 1:
+                d.sample_all(vals[a:b])  # host batch
+            else:
+                d.sample_all(vd[a:b])
+            ref.sample_all(vals[a:b].astype(np.int64))
+            assert np.array_equal(d.result(), ref.result()[0].astype(dt)), (k, n, part_i)
+    # few hash values: the slice fallback (sub-batches below the hook's threshold still publish)
+    xs = rng.integers(-hi, hi, size=30_000, dtype=np.int64).astype(dt)
+    d = Sampler.distinct(300, seed=11, key_type=key_type, order="set")(hash=lambda x: (x * 0x9E3779B1) % 3)
+    d.sample_all(xs)
+    r = oracle.Distinct(300, 11, oracle.HASH_IDENTITY)
+    ent = sorted({(oracle.scramble(r.r0, r.r1, (int(x) * 0x9E3779B1) % 3), int(x)) for x in xs.tolist()})
+    assert d.result().tolist() == [x for _, x in ent[:300]]
