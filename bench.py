@@ -2,16 +2,26 @@
 
 A step is one full pass of the hot path over the batch: a fresh Sampler (Sampler.apply, created
 and closed inside the step) samples the device-resident keys (K1 last-writer kernel + resolve),
-then result() brings the k-slot reservoir to the host.  With N GPUs the stream is N x 1e9 elements split by index range (each
-rank seeks to its offset, weak scaling) and the per-rank reservoirs are combined with one RCCL
-all_gather + merge kernel inside the step.
+then result() brings the k-slot reservoir to the host.  With N GPUs the stream is N x 1e9 elements
+split by index range (each rank seeks to its offset, weak scaling) and the per-rank reservoirs are
+combined with one all_gather + merge kernel inside the step.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+--gpus N > 1 without a torch.distributed environment (WORLD_SIZE unset) launches N ranks itself
+(a torch.distributed.run child process; this process never touches the GPU).  Inside a launched
+job WORLD_SIZE must equal N.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including
-  roofline      -- K1's average launch time, measured with HIP events on the sampler's stream
-  cpu_baseline  -- the oracle's C restatement of the reference (Algorithm L) on one host core
-  secondary     -- (N = 1) the other configs of BASELINE.json, measured after the headline:
-                   C3 segmented, C4 distinct (identity; Long.hashCode in set and ordered order),
-                   C2 on engine java_l, and the CPU distinct baseline (tools/bench_paths.py)
+  roofline      -- K1's VALU roofline (tools/roofline.py): algorithmic Philox calls per launch over
+                   the fused kernel's average launch time, measured with HIP events on the
+                   sampler's stream, against the gfx950 issue peak; HBM traffic from PMC
+  cpu_baseline  -- the oracle's C restatement of the reference (Algorithm L / RandomValues) on the
+                   host cores, median of 5 runs per leg (C2 headline leg on one core; C1, C3 on
+                   all cores, C4 prefix)
+  secondary     -- (N = 1) the other configs of BASELINE.json: C3 segmented (with K2's VALU
+                   roofline), C4 distinct (identity; Long.hashCode in set and ordered order; the
+                   ordered replay branch), C2 on engine java_l (tools/bench_paths.py)
 """
 from __future__ import annotations
 
@@ -20,109 +30,127 @@ import ctypes as C
 import json
 import mmap
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 METRIC = "elements sampled/sec (Gelem/s) + % HBM roofline, 1B Long keys k=1024, 1/2/4/8 GPU"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-BYTES_PER_ELEM = 8     # each 64-bit key charged once
 
 
-def splitmix_fill(out: torch.Tensor, base: int, chunk: int = 1 << 27) -> None:
+def splitmix_fill(out, base: int, chunk: int = 1 << 27) -> None:
     """key[i] = splitmix64(0x5EED0000 + i), generated on the device."""
-    def s64(c):
-        return c - (1 << 64) if c >= 1 << 63 else c
+    import workloads
 
-    g, m1, m2 = s64(0x9E3779B97F4A7C15), s64(0xBF58476D1CE4E5B9), s64(0x94D049BB133111EB)
-    n = out.numel()
-    for a in range(0, n, chunk):
-        b = min(n, a + chunk)
-        z = torch.arange(base + a, base + b, dtype=torch.int64, device=out.device) + g
-        z = (z ^ ((z >> 30) & ((1 << 34) - 1))) * m1
-        z = (z ^ ((z >> 27) & ((1 << 37) - 1))) * m2
-        out[a:b] = z ^ ((z >> 31) & ((1 << 33) - 1))
+    workloads.splitmix_fill(out, base, chunk)
 
 
-def cpu_baseline(k: int, n_stream: int, seed: int) -> dict:
-    """Time the oracle (C restatement of Sampler.scala) on one host core, bounded to ~10 s."""
+def _median(fn, reps: int = 5) -> float:
+    return statistics.median(fn() for _ in range(reps))
+
+
+def host_cores() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(k: int, n_stream: int, seed: int, c4_host=None) -> dict:
+    """The oracle (C restatement of Sampler.scala) on the host, median of 5 runs per leg.
+
+    The headline leg (`value`) is C2's streaming path: per-element sample() (Sampler.scala:248-259,
+    what the akka operator calls) on ONE core -- the reference sampler is single-threaded
+    (Sampler.scala:18-19).  Bounded samples keep the whole baseline at ~15-30 s of CPU work.
+    """
     from oracle import oracle as O
 
     L = O.lib()
+    threads = min(16, host_cores())
+    out = np.zeros(max(k, 1 << 10), dtype=np.int64)
+    op = out.ctypes.data_as(C.c_void_p)
+    legs = []
+
+    # C2, per-element: a 2.5e8-element sample of the stream (a 2e7-key prefix replayed)
     buf_n = 20_000_000
     keys = O.splitmix_keys(0x5EED0000, buf_n)
-    out = np.zeros(k, dtype=np.int64)
-    t = L.or_time_algo_l_per_element(k, seed, keys, buf_n, 1, out.ctypes.data_as(C.c_void_p))
-    reps = max(1, min(int(n_stream // buf_n), int(8.0 / max(t, 1e-3))))
-    t = L.or_time_algo_l_per_element(k, seed, keys, buf_n, reps, out.ctypes.data_as(C.c_void_p))
+    reps = 12
+    t = _median(lambda: L.or_time_algo_l_per_element(k, seed, keys, buf_n, reps, op))
     per_elem = reps * buf_n / t / 1e9
-    # sampleAll(IndexedSeq) skip path over the full stream: an untouched zero-page mapping stands in
-    # for the 8 GB array (the path reads only ~k ln(n/k) elements)
+    # C2, sampleAll(IndexedSeq) skip path over the full 1e9 length: an untouched zero-page mapping
+    # stands in for the 8 GB array (the path reads only ~k ln(n/k) elements, all of them zeros)
     zbuf = mmap.mmap(-1, n_stream * 8)
     addr = C.addressof(C.c_char.from_buffer(zbuf))
-    ts = L.or_time_algo_l_indexed(k, seed, C.c_void_p(addr), n_stream, out.ctypes.data_as(C.c_void_p))
+    ts = _median(lambda: L.or_time_algo_l_indexed(k, seed, C.c_void_p(addr), n_stream, op))
     del addr
     zbuf.close()
+    legs.append({"config": "C2 sampleAll(IndexedSeq) skip path (Sampler.scala:261-273)", "cores": 1,
+                 "Gelem_s": round(n_stream / ts / 1e9, 2),
+                 "sample": f"{n_stream:.0e} elements, k={k}; input = an untouched zero-page mapping (the path "
+                           "touches ~k ln(n/k) elements, so their values do not matter)"})
+
+    # C1: 10 M Longs (the first 1e7 of the C2 stream), k = 100, both samplers
+    n1, k1 = 10_000_000, 100
+    c1 = keys[:n1]
+    t = _median(lambda: L.or_time_algo_l_per_element(k1, seed, c1, n1, 1, op))
+    legs.append({"config": "C1 Sampler(100) per-element sample()", "cores": 1, "Gelem_s": round(n1 / t / 1e9, 4),
+                 "sample": "1e7 keys"})
+    t = _median(lambda: L.or_time_algo_l_indexed(k1, seed, c1.ctypes.data_as(C.c_void_p), n1, op))
+    legs.append({"config": "C1 Sampler(100) sampleAll(IndexedSeq)", "cores": 1, "Gelem_s": round(n1 / t / 1e9, 2),
+                 "sample": "1e7 keys"})
+    for hk, name in ((O.HASH_JAVA_LONG, "Long.hashCode (default)"), (O.HASH_IDENTITY, "identity")):
+        t = _median(lambda: L.or_time_distinct(k1, seed, hk, c1, n1))
+        legs.append({"config": f"C1 Sampler.distinct(100), hash = {name}, per element", "cores": 1,
+                     "Gelem_s": round(n1 / t / 1e9, 4), "sample": "1e7 keys"})
+
+    # C3: one reference sampler per stream (4096 Longs, k = 64) on every host core we may use
+    S3, L3 = 1 << 16, 4096
+    k3 = O.splitmix_keys(0, S3 * L3)
+    for mode, name in ((0, "per-element sample()"), (1, "sampleAll(IndexedSeq)")):
+        t = _median(lambda: L.or_time_segmented_algo_l(64, k3, S3, L3, mode, threads, None))
+        legs.append({"config": f"C3 one Sampler(64) per stream, {name}", "cores": threads,
+                     "Gelem_s": round(S3 * L3 / t / 1e9, 3), "sample": f"2^16 of the 2^20 streams x {L3} keys"})
+    del k3
+
+    # C4: Sampler.distinct(65536), default Long.hashCode, over a prefix of one GPU's C4 share
+    if c4_host is not None:
+        n4 = c4_host.size
+        t = _median(lambda: L.or_time_distinct(65536, 7, O.HASH_JAVA_LONG, c4_host, n4))
+        legs.append({"config": "C4 Sampler.distinct(65536), hash = Long.hashCode, per element", "cores": 1,
+                     "Gelem_s": round(n4 / t / 1e9, 4),
+                     "sample": f"the first {n4:.1e} keys of C4's per-GPU share (30 % duplicates, Feistel order)"})
     return {
         "value": round(per_elem, 4),
         "unit": "Gelem/s",
         "cores": 1,
         "kind": "port",
         "sample": f"per-element sample() (Algorithm L, Sampler.scala:248-259) over one stream of "
-                  f"{reps * buf_n:.3g} keys (a {buf_n:.0e}-key C2 prefix replayed {reps}x), k={k}",
-        "skip_path": {"value": round(n_stream / ts / 1e9, 2), "unit": "Gelem/s",
-                      "sample": f"sampleAll(IndexedSeq) skip path (Sampler.scala:261-273) over "
-                                f"{n_stream:.0e} elements; touches ~k ln(n/k) of them"},
+                  f"{reps * buf_n:.3g} keys (a {buf_n:.0e}-key C2 prefix replayed {reps}x), k={k}; median of 5",
+        "host_cores": host_cores(),
+        "legs": legs,
     }
 
 
-def valu_roofline(n: int, k1_s: float) -> dict:
-    """K1's binding limit: Philox4x32-10 evaluations per second vs the gfx950 VALU peak.
+def secondary(dev) -> list:
+    """The other hot-path configs of BASELINE.json (not the headline `value`).  Same measurement
+    code as tools/bench_paths.py; a failure here is reported in the entry, never fails the line."""
+    import torch
 
-    Per call: 20 v_mad_u64_u32 (3.2 full-rate issue slots each, measured by tools/micro_k1.hip)
-    + 20 v_bitop3 = 84 slots; peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz / 84.  Calls per launch
-    (expected): one level-0 call per 16 indices, a recompute for the 6.07 % of blocks holding a zero
-    byte, and one level-1 call per candidate (1 in 256 indices).
-    """
-    level0 = n / 16
-    calls = level0 * (1 + (1 - (255 / 256) ** 16)) + n / 256
-    peak = 256 * 4 * 32 * 2.4e9 / 84 / 1e9
-    achieved = calls / k1_s / 1e9
-    return {"bound": "valu", "achieved": round(achieved, 1), "peak": round(peak, 1),
-            "unit": "GPhilox/s", "frac": round(achieved / peak, 4),
-            "calls_per_launch": int(calls)}
-
-
-def load_traffic(n: int):
-    """HBM bytes per K1 launch from the committed PMC pass (profiles/), if one matches n."""
-    path = os.path.join(ROOT, "profiles", "pmc_k1.json")
-    try:
-        d = json.load(open(path))
-        if int(d.get("n", -1)) == n:
-            return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
-    return None
-
-
-def secondary(dev, with_cpu: bool) -> list:
-    """The other hot-path configs of BASELINE.json (not the headline `value`): C3 segmented,
-    C4 distinct (one GPU's share; identity hash, and Long.hashCode in set and ordered order), C2 on
-    the reference's Algorithm L (engine java_l).  Same measurement code as tools/bench_paths.py;
-    a failure here is reported in the entry, never fails the headline line."""
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_paths as P
 
     out = []
     jobs = [("C3", lambda: P.c3(dev)), ("C4 identity", lambda: P.c4(dev, "identity")),
             ("C4 default/set", lambda: P.c4(dev, "default", "set")),
-            ("C4 default/ordered", lambda: P.c4(dev, "default")), ("C2 java_l", lambda: P.c2l(dev))]
+            ("C4 default/ordered", lambda: P.c4(dev, "default")),
+            ("C4 default/ordered replay branch", lambda: P.c4_replay(dev)),
+            ("C2 java_l", lambda: P.c2l(dev))]
     for name, fn in jobs:
         try:
             r = fn()
@@ -130,15 +158,42 @@ def secondary(dev, with_cpu: bool) -> list:
             r = {"config": name, "error": f"{type(ex).__name__}: {ex}"}
         out.append({kk: (round(v, 6) if isinstance(v, float) else v) for kk, v in r.items()})
         torch.cuda.empty_cache()
-    if with_cpu:
-        from oracle import oracle as O
-
-        keys = O.splitmix_keys(0xD15C, 10_000_000)
-        t = O.lib().or_time_distinct(65536, 7, O.HASH_IDENTITY, keys, keys.size)
-        out.append({"config": "CPU baseline: Sampler.distinct per element (RandomValues restated, "
-                              "Sampler.scala:394-409), k=65536, identity hash, 1e7 keys, 1 core",
-                    "Gelem_s": round(keys.size / t / 1e9, 4), "kind": "port", "cores": 1})
     return out
+
+
+def load_traffic(n: int):
+    """HBM bytes per K1 launch from the committed PMC pass (profiles/), if one matches n."""
+    for path in (os.path.join(ROOT, "profiles", "r02", "pmc_k1.json"), os.path.join(ROOT, "profiles", "pmc_k1.json")):
+        try:
+            d = json.load(open(path))
+            if int(d.get("n", -1)) == n:
+                return d.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+    return None
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(args) -> int:
+    """--gpus N > 1 outside a torch.distributed job: run N ranks (one per GPU) in a child
+    torch.distributed.run.  Nothing here initialises the GPU (device_count does not, on ROCm)."""
+    import torch
+
+    have = torch.cuda.device_count()
+    if have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this node has {have}; "
+              "refusing to run fewer ranks than requested", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main() -> None:
@@ -157,7 +212,16 @@ def main() -> None:
                     help="skip the other hot-path configs (C3 segmented, C4 distinct, C2 on java_l)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+
+    import torch
+    import torch.distributed as dist
+
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # RSV_BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU
@@ -173,6 +237,7 @@ def main() -> None:
 
     from reservoir_amd import Sampler, _native
     from reservoir_amd import distributed as D
+    import roofline as R
 
     n, k = args.n, args.k
     offset = rank * n
@@ -181,7 +246,6 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     L = _native.load()
-    prof = [0.0, 0]  # K1 milliseconds, launches (timed steps)
 
     def step():
         # a fresh Sampler per step (Sampler.apply): creation and close are inside the step
@@ -200,18 +264,16 @@ def main() -> None:
         _native.check(L.rsv_profile_global_read(C.byref(ms), C.byref(cnt)))
         return ms.value, cnt.value
 
-    # Device warm-up (untimed): under sustained load the K1 launch time falls from ~152 to ~140 us
-    # over the first ~30 ms as clocks ramp (rocprofv3 trace); run steps for 0.2 s
-    # before the W warmup steps so the timed region sees the steady state.
-    # Every step holds a collective at N>1, so all ranks must run the same number of steps: the
-    # count comes from one timed step, agreed as the max over ranks.
+    # Device warm-up (untimed): under sustained load the K1 launch time falls as clocks ramp over
+    # the first ~30 ms; run steps for 0.2 s before the W warmup steps so the timed region sees the
+    # steady state.  Every step holds a collective at N>1, so all ranks run the same number of
+    # steps: the count comes from one timed step, agreed as the max over ranks.
     t_w = time.perf_counter()
     step()
     torch.cuda.synchronize()
     n_ramp = max(1, int(0.2 / max(time.perf_counter() - t_w, 1e-4)))
     if world > 1:
-        t = torch.tensor([min(n_ramp, 10_000)], dtype=torch.int64,
-                         device=dev if backend == "nccl" else "cpu")
+        t = torch.tensor([min(n_ramp, 10_000)], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         n_ramp = int(t.item())
     for _ in range(min(n_ramp, 10_000)):
@@ -236,19 +298,26 @@ def main() -> None:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     _native.check(L.rsv_profile_global(0))
-    prof[0], prof[1] = profile_read()
+    k1_ms, k1_launches = profile_read()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # K1 launch time (HIP events on the launch stream), averaged over the timed steps
-    k1_s = prof[0] / max(prof[1], 1) / 1e3
+    k1_s = k1_ms / max(k1_launches, 1) / 1e3  # K1 launch time (HIP events on the launch stream)
     assert res is not None and res.size == k
 
     if rank == 0:
         total = n * world * args.steps
-        achieved = BYTES_PER_ELEM * n / k1_s / 1e9
+        l0, l1 = R.k1_calls(n, k, offset)
+        roof = R.valu_roofline(
+            l0, l1, k1_s, "k1_resolve_publish (K1 + the last workgroup's resolve/publish tail)",
+            note="bound = integer VALU (Philox): K1 reads only the k winning keys (draws depend on the index "
+                 "alone, like the reference's sampleAll(IndexedSeq) skip, Sampler.scala:261-273), so the "
+                 "SURVEY 8(d) 8 B/elem HBM convention would read " +
+                 f"{8 * n / k1_s / 1e9:.0f} GB/s (> the 8 TB/s peak): it is not this kernel's bound")
+        roof["traffic"] = load_traffic(n)
+        roof["launches_timed"] = k1_launches
         line = {
             "metric": METRIC,
             "value": round(total / elapsed / 1e9, 3),
@@ -267,31 +336,28 @@ def main() -> None:
                             "Algorithm R last-writer (engine philox_r); step = create Sampler, "
                             "sampleAll over device-resident keys, result() to host, close",
                 "keys_per_gpu": n, "k": k, "stream_elements": n * world,
-                "parallelism": f"index-range split over {world} GPU(s), RCCL all_gather combine"
+                "parallelism": (f"index-range split over {world} ranks, "
+                                f"{'RCCL' if backend == 'nccl' else backend} all_gather combine")
                                if world > 1 else "single GPU",
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic(n),
-                "kernel": "k1_resolve_publish",
-                "launch_avg_us": round(k1_s * 1e6, 2),
-                "launches_timed": prof[1],
-                "note": "achieved charges 8 B per element (SURVEY.md 8(d)); K1 reads no key "
-                        "(draws depend only on the index), so it is bound by Philox integer "
-                        "VALU work, not HBM -- see the valu_roofline object and DESIGN.md",
-            },
-            "valu_roofline": valu_roofline(n, k1_s),
+            "roofline": roof,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(k, n, args.seed)
+        c4_host = None
         if world == 1 and not args.no_secondary:
             del keys
             torch.cuda.empty_cache()
-            line["secondary"] = secondary(dev, with_cpu=not args.no_cpu_baseline)
+            line["secondary"] = secondary(dev)
+        if world == 1 and not args.no_cpu_baseline:
+            import workloads
+
+            c4 = workloads.c4_data(500_000_000, dev)
+            c4_host = c4[:400_000_000].cpu().numpy()
+            del c4
+            torch.cuda.empty_cache()
+            try:
+                line["cpu_baseline"] = cpu_baseline(k, n, args.seed, c4_host)
+            except Exception as ex:  # noqa: BLE001 -- the headline line is printed regardless
+                line["cpu_baseline"] = {"error": f"{type(ex).__name__}: {ex}"}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -412,6 +412,102 @@ void or_algo_r_segmented(uint64_t seed, uint64_t stream_base, int32_t k, const i
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* Full-size form of or_algo_r (C2: 1e9 indices): the same last writers, computed by the exact   */
+/* shortcut of draw format R2.  j_i = floor(U_i (i+1) / 2^64) with U_i >= b_i 2^56, so j_i < k     */
+/* implies b_i (i+1) < 256 k: an index failing that test cannot write any slot and its level-1    */
+/* Philox is skipped.  Every index passing it is evaluated exactly (or_draw_j's arithmetic), so    */
+/* the result equals or_algo_r's res_idx bit for bit.  Slot j's writer is the LARGEST index that  */
+/* draws j (Algorithm R's last writer), so disjoint index ranges reduce by max: threads.         */
+/* ------------------------------------------------------------------------------------------ */
+#include <pthread.h>
+#include <unistd.h>
+
+typedef struct {
+    uint64_t seed, stream, lo, hi; /* [lo, hi) */
+    int32_t k;
+    int64_t* win;                  /* k slots, this thread's */
+} lw_job;
+
+static uint32_t r2_byte(const uint32_t w[4], unsigned e) {
+    uint32_t b = 0;
+    for (int p = 0; p < 8; p++) b |= ((w[p >> 1] >> (16 * (p & 1) + e)) & 1u) << p;
+    return b;
+}
+
+static void lw_eval(const lw_job* jb, uint64_t i, uint32_t b) {
+    uint32_t w1[4];
+    philox_at(jb->seed, jb->stream, i >> 1, 1, w1);
+    uint64_t L = ((uint64_t)w1[2 * (i & 1)] << 32) | w1[2 * (i & 1) + 1];
+    uint64_t U = ((uint64_t)b << 56) | (L >> 8);
+    uint64_t j = (uint64_t)(((unsigned __int128)U * ((unsigned __int128)i + 1)) >> 64);
+    if (j < (uint64_t)jb->k && (int64_t)i > jb->win[j]) jb->win[j] = (int64_t)i;
+}
+
+static void* lw_run(void* arg) {
+    lw_job* jb = (lw_job*)arg;
+    const uint64_t k = (uint64_t)jb->k, lim = 256 * k;
+    for (uint64_t i = jb->lo; i < jb->hi && i < k; i++) jb->win[i] = (int64_t)i; /* fill phase */
+    uint64_t start = jb->lo > k ? jb->lo : k;
+    for (uint64_t g = start >> 4; (g << 4) < jb->hi; g++) {
+        uint32_t w0[4];
+        philox_at(jb->seed, jb->stream, g, 0, w0);
+        uint64_t i0 = g << 4;
+        if (i0 + 1 >= lim) { /* sparse: only b_i == 0 passes -- bit e of every plane clear */
+            uint32_t x = w0[0] | w0[1] | w0[2] | w0[3];
+            uint32_t zero = ~(x | (x >> 16)) & 0xFFFFu;
+            while (zero) {
+                unsigned e = (unsigned)__builtin_ctz(zero);
+                zero &= zero - 1;
+                uint64_t i = i0 + e;
+                if (i >= start && i < jb->hi) lw_eval(jb, i, 0);
+            }
+        } else {
+            for (unsigned e = 0; e < 16; e++) {
+                uint64_t i = i0 + e;
+                if (i < start || i >= jb->hi) continue;
+                uint32_t b = r2_byte(w0, e);
+                if ((unsigned __int128)b * (i + 1) < lim) lw_eval(jb, i, b);
+            }
+        }
+    }
+    return NULL;
+}
+
+static int or_threads(int nthreads) {
+    if (nthreads > 0) return nthreads;
+    long c = sysconf(_SC_NPROCESSORS_ONLN);
+    if (c < 1) c = 1;
+    return c > 16 ? 16 : (int)c; /* the GPU box grants 16 host cores per GPU */
+}
+
+void or_algo_r_last_writers(uint64_t seed, uint64_t stream, int32_t k, uint64_t i0, int64_t n,
+                            int64_t* win, int nthreads) {
+    for (int32_t j = 0; j < k; j++) win[j] = -1;
+    if (n <= 0 || k <= 0) return;
+    int T = or_threads(nthreads);
+    if ((uint64_t)n < (1u << 20)) T = 1;
+    lw_job* jobs = (lw_job*)calloc((size_t)T, sizeof(lw_job));
+    pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
+    uint64_t per = (((uint64_t)n + (uint64_t)T - 1) / (uint64_t)T + 15) & ~(uint64_t)15;
+    for (int t = 0; t < T; t++) {
+        uint64_t lo = i0 + per * (uint64_t)t, hi = lo + per;
+        if (lo > i0 + (uint64_t)n) lo = i0 + (uint64_t)n;
+        if (hi > i0 + (uint64_t)n) hi = i0 + (uint64_t)n;
+        jobs[t] = (lw_job){seed, stream, lo, hi, k, (int64_t*)malloc((size_t)k * sizeof(int64_t))};
+        for (int32_t j = 0; j < k; j++) jobs[t].win[j] = -1;
+        pthread_create(&th[t], NULL, lw_run, &jobs[t]);
+    }
+    for (int t = 0; t < T; t++) {
+        pthread_join(th[t], NULL);
+        for (int32_t j = 0; j < k; j++)
+            if (jobs[t].win[j] > win[j]) win[j] = jobs[t].win[j];
+        free(jobs[t].win);
+    }
+    free(jobs);
+    free(th);
+}
+
+/* ------------------------------------------------------------------------------------------ */
 uint64_t or_splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ULL;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -455,6 +551,51 @@ double or_time_algo_l_indexed(int32_t k, int64_t seed, const int64_t* keys, int6
     double t1 = now_s();
     if (out) or_algo_l_result(&s, out);
     or_algo_l_free(&s);
+    return t1 - t0;
+}
+
+/* C3 leg: S independent samplers (one reference Sampler per stream of L keys, seed = stream
+ * index), split over threads (the reference has no threads of its own: one sampler per core).
+ * mode 0: per-element sample() (Sampler.scala:248-259); mode 1: sampleAll(IndexedSeq) (:261-273). */
+typedef struct {
+    int32_t k;
+    const int64_t* keys;
+    int64_t s0, s1, L;
+    int mode;
+    int64_t* out;
+} seg_job;
+
+static void* seg_run(void* arg) {
+    seg_job* jb = (seg_job*)arg;
+    for (int64_t s = jb->s0; s < jb->s1; s++) {
+        or_algo_l a;
+        if (or_algo_l_init(&a, jb->k, s, 0)) return NULL;
+        const int64_t* x = jb->keys + s * jb->L;
+        if (jb->mode == 0)
+            for (int64_t i = 0; i < jb->L; i++) or_algo_l_sample(&a, x[i]);
+        else
+            or_algo_l_sample_all_indexed(&a, x, jb->L);
+        if (jb->out) or_algo_l_result(&a, jb->out + s * (int64_t)jb->k);
+        or_algo_l_free(&a);
+    }
+    return NULL;
+}
+
+double or_time_segmented_algo_l(int32_t k, const int64_t* keys, int64_t S, int64_t L, int mode,
+                                int nthreads, int64_t* out) {
+    int T = or_threads(nthreads);
+    if (T > S) T = (int)(S > 0 ? S : 1);
+    seg_job* jobs = (seg_job*)calloc((size_t)T, sizeof(seg_job));
+    pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
+    double t0 = now_s();
+    for (int t = 0; t < T; t++) {
+        jobs[t] = (seg_job){k, keys, S * t / T, S * (t + 1) / T, L, mode, out};
+        pthread_create(&th[t], NULL, seg_run, &jobs[t]);
+    }
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    double t1 = now_s();
+    free(jobs);
+    free(th);
     return t1 - t0;
 }
 

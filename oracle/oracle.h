@@ -94,6 +94,12 @@ int64_t or_algo_r(uint64_t seed, uint64_t stream, int32_t k, uint64_t i0,
 /* Algorithm R fed with an explicit per-element draw sequence j[0..n) for indices [i0, i0+n). */
 void    or_algo_r_replay(int32_t k, uint64_t i0, const uint64_t* j, const int64_t* keys, int64_t n,
                          int64_t* res);
+/* Last writer per slot over indices [i0, i0+n) (win[j] = largest index writing slot j, or j
+ * itself in the fill phase; -1 = none), identical to or_algo_r's res_idx but evaluated with the
+ * exact R2 shortcut (an index with b_i (i+1) >= 256k cannot hit) on nthreads threads (0 = up to
+ * 16): the full-size C2 check (1e9 indices) in seconds. */
+void    or_algo_r_last_writers(uint64_t seed, uint64_t stream, int32_t k, uint64_t i0, int64_t n,
+                               int64_t* win, int nthreads);
 /* S independent streams, keys[offsets[s] .. offsets[s+1]), stream id = s (+stream_base). */
 void    or_algo_r_segmented(uint64_t seed, uint64_t stream_base, int32_t k, const int64_t* keys,
                             const int64_t* offsets, int64_t S, int64_t* out, int64_t* counts);
@@ -103,6 +109,10 @@ double or_time_algo_l_per_element(int32_t k, int64_t seed, const int64_t* keys, 
                                   int64_t reps, int64_t* out);
 double or_time_algo_l_indexed(int32_t k, int64_t seed, const int64_t* keys, int64_t n, int64_t* out);
 double or_time_distinct(int32_t k, int64_t seed, int hash_kind, const int64_t* keys, int64_t n);
+/* S independent Algorithm-L samplers over S x L keys on nthreads threads (0 = up to 16); mode 0 =
+ * per-element sample(), 1 = sampleAll(IndexedSeq); out (S x k, optional) receives the reservoirs */
+double or_time_segmented_algo_l(int32_t k, const int64_t* keys, int64_t S, int64_t L, int mode,
+                                int nthreads, int64_t* out);
 
 /* synthetic inputs */
 uint64_t or_splitmix64(uint64_t x);

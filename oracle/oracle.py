@@ -82,6 +82,11 @@ def lib():
     L.or_time_algo_l_indexed.restype = C.c_double
     L.or_time_distinct.argtypes = [C.c_int32, C.c_int64, C.c_int, i64p, C.c_int64]
     L.or_time_distinct.restype = C.c_double
+    L.or_algo_r_last_writers.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_int64, i64p,
+                                         C.c_int]
+    L.or_time_segmented_algo_l.argtypes = [C.c_int32, i64p, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                                           C.c_void_p]
+    L.or_time_segmented_algo_l.restype = C.c_double
     L.or_splitmix64.argtypes = [C.c_uint64]; L.or_splitmix64.restype = C.c_uint64
     L.or_fill_splitmix.argtypes = [C.c_uint64, C.c_int64, i64p]
     _lib = L
@@ -224,6 +229,14 @@ def algo_r(seed: int, stream: int, k: int, keys, i0: int = 0, res=None):
     repl = lib().or_algo_r(seed, stream, k, i0, keys, keys.size, res, None)
     m = min(i0 + keys.size, k)
     return res[:m].copy() if m < k else res, repl
+
+
+def algo_r_last_writers(seed: int, stream: int, k: int, i0: int, n: int, threads: int = 0) -> np.ndarray:
+    """Per slot, the global index of its last writer over [i0, i0+n) (-1: none) -- or_algo_r's
+    res_idx at full size (exact R2 shortcut, multi-threaded; oracle.c or_algo_r_last_writers)."""
+    win = np.empty(k, dtype=np.int64)
+    lib().or_algo_r_last_writers(seed, stream, k, i0, n, win, threads)
+    return win
 
 
 def algo_r_replay(k: int, j, keys, i0: int = 0) -> np.ndarray:

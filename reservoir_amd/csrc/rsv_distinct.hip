@@ -882,6 +882,9 @@ void distinct_spec_target(DistinctState* d, void* dst_host_dev, uint32_t* flag_d
     d->spec_ok = false;
 }
 
+bool distinct_is_ordered(const DistinctState* d) { return d->ordered; }
+int64_t distinct_spec_min(const DistinctState* d) { return d->spec_min; }
+
 bool distinct_spec_take(DistinctState* d, uint32_t* gen) {
     const bool ok = d->spec_ok && d->spec_dst;
     if (ok) *gen = d->spec_gen;
@@ -1152,8 +1155,10 @@ static int sample_impl(DistinctState* d, const KeyT* keys, const int64_t* hashes
         DTRY(launch_filter<KeyT>(d, keys, hashes, n, tinc, st));
         if (d->timer) d->timer->mark(st);
         if (bucketed) DTRY(launch_bucket_merge<KeyT>(d, tinc, st));
-        // large batches: publish the merged set speculatively (used if this pass is the last)
-        const bool spec = bucketed && d->spec_dst && n >= d->spec_min;
+        // large batches: publish the merged set speculatively (used if this pass is the last) --
+        // armed only on a pass expected to be final: the analytic first pass, or one whose
+        // threshold admits everything; a retry that tightens or widens publishes at result()
+        const bool spec = bucketed && d->spec_dst && n >= d->spec_min && (attempt == 0 || tinc >= t_allowed);
         d->spec_arm = spec;
         DTRY(read_ctl(d, d->h_pinned + 4, st));
         const int64_t c = d->h_pinned[4];

@@ -55,11 +55,16 @@ __global__ __launch_bounds__(kBlock) void k1_resolve_publish(DrawKey dk, uint32_
     __shared__ uint64_t cqs[kBlock / 64][kQueue];
     __shared__ uint32_t last;
     k1_body_bits<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
-    // This wave's winner atomics are performed (acknowledged by the device-coherent L2 side) once
-    // vmcnt drains; K1 makes no plain global stores, so no L2 write-back is needed before the
-    // ticket.  An agent-scope release/acquire fence here costs a buffer_wbl2 per wave and a
-    // buffer_inv per workgroup: measured 112 -> 211 us per launch at C2.  Only the last
-    // workgroup acquires (one L2 invalidate) before it reads the winners.
+    // This wave's winner atomics are performed once vmcnt drains: on gfx942/gfx950 a global atomic
+    // without return still counts in vmcnt until the memory system acknowledges it (there is no
+    // separate vscnt), and an agent-scope atomic is performed at the agent's coherence point (the
+    // sc1 atomic path, LLVM AMDGPUUsage "Memory Model GFX942": agent-scope atomics bypass the
+    // non-coherent per-XCD L2 state), where the last workgroup's agent-scope loads below read.
+    // K1 makes no plain global stores, so there are no dirty L2 lines a release would have to
+    // write back.  Measured alternatives: an agent-scope release/acquire fence per wave (a
+    // buffer_wbl2 per wave + buffer_inv per workgroup) took the launch from 112 to 211 us at C2.
+    // Only the last workgroup acquires (one L2 invalidate) before it reads the winners; the
+    // parity tests (test_fused_k1_resolve_publish, the full-size C2 check) exercise this path.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {

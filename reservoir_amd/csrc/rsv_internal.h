@@ -156,6 +156,8 @@ int distinct_publish(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, u
 // its ctl read; distinct_spec_take says whether the last one holds the batch's final set (its
 // generation in *gen) and clears the target.
 void distinct_spec_target(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t* gen_counter);
+bool distinct_is_ordered(const DistinctState* d);
+int64_t distinct_spec_min(const DistinctState* d);  // smallest batch that publishes speculatively
 bool distinct_spec_take(DistinctState* d, uint32_t* gen);
 // copies the set (ascending hash) to device buffers; either may be null
 int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStream_t st);

@@ -358,9 +358,14 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
         s->win_zero = false;  // until this batch's resolve is enqueued
     }
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
-        // set mode: large batches publish the merged set speculatively (distinct_spec_target)
-        if (rsv_status st = ensure_result_buffer(s)) return st;
-        if (s->result_publish) distinct_spec_target(s->distinct, s->result_dev, s->result_flag_dev, &s->result_gen);
+        // set mode: large batches publish the merged set speculatively (distinct_spec_target) --
+        // only where a publication can happen at all (a coherent result buffer of k keys); other
+        // samplers (huge k, ordered mode, device-only consumers) keep the result buffer lazy
+        if ((int64_t)s->k * s->kw <= kPublishMaxBytes && !distinct_is_ordered(s->distinct) &&
+            n >= distinct_spec_min(s->distinct)) {
+            if (rsv_status st = ensure_result_buffer(s)) return st;
+            if (s->result_publish) distinct_spec_target(s->distinct, s->result_dev, s->result_flag_dev, &s->result_gen);
+        }
         int rc = distinct_sample_device(s->distinct, keys, hashes, n, s->stream);
         uint32_t gen = 0;
         const bool published = distinct_spec_take(s->distinct, &gen);
@@ -869,6 +874,8 @@ rsv_status rsv_seek(rsv_sampler* s, int64_t index) {
         if (rsv_status st = flush_stage(s)) return st;
     }
     if (index < s->count) return fail(RSV_E_ILLEGAL_ARGUMENT, "rsv_seek cannot move backwards");
+    // a publication holds min(count, k) keys: once the count crosses k it covers too few
+    if (std::min<int64_t>(index, s->k) != std::min<int64_t>(s->count, s->k)) s->pub_valid = false;
     s->count = index;
     return RSV_OK;
 }

@@ -1,0 +1,104 @@
+"""reservoir_amd.distributed with the REAL engine: 2 gloo ranks sharing one GPU.
+
+Each rank samples its index range of one stream with a GpuSampler (seek + sample_all on device
+keys), then distributed.combine runs the one-collective exchange: export_packed -> all_gather ->
+merge_packed for element samplers, export_state -> all_gather -> merge_state for distinct ones.
+Every rank must end with the oracle's single-stream result (oracle.algo_r, oracle.Distinct).
+RCCL cannot put two ranks on one device, so this rehearsal uses gloo (CUDA tensors through host
+copies); bench.py at N GPUs uses RCCL with one rank per GPU and the same calls.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from reservoir_amd import Sampler
+        from reservoir_amd import distributed as D
+
+        out = {}
+        n, k = 3_000_017, 1024
+        keys = O.splitmix_keys(0x5EED0000, n)
+        lo, hi = D.shard_range(n, rank, world)
+        for kt in ("long", "int"):
+            dt = torch.int64 if kt == "long" else torch.int32
+            kd = torch.from_numpy(keys[lo:hi]).to(dev).to(dt)
+            s = Sampler(k, seed=0xC0FFEE, stream_id=0x5A5A, key_type=kt)()
+            D.sample_shard(s, kd, lo)
+            D.combine(s, device=dev)  # count rides along in the row
+            out[f"elements_{kt}"] = (s.result().astype(np.int64).tolist(), s.count)
+            s2 = Sampler(k, seed=0xC0FFEE, stream_id=0x5A5A, key_type=kt)()
+            D.sample_shard(s2, kd, lo)
+            D.combine(s2, device=dev, total_count=n)  # bench.py's form
+            out[f"elements_{kt}_total"] = (s2.result().astype(np.int64).tolist(), s2.count)
+        vals = np.random.default_rng(3).integers(-2**63, 2**63 - 1, size=400_000, dtype=np.int64)
+        vals = np.concatenate([vals, vals[: 150_000]])
+        dlo, dhi = D.shard_range(vals.size, rank, world)
+        d = Sampler.distinct(5000, seed=9)(hash="identity")
+        D.sample_shard(d, torch.from_numpy(vals[dlo:dhi]).to(dev), dlo)
+        D.combine(d, device=dev)
+        out["distinct"] = (sorted(d.result().tolist()), d.count)
+        q.put((rank, out))
+    except BaseException as ex:  # noqa: BLE001 -- reported to the parent
+        q.put((rank, repr(ex)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_gloo_ranks_real_engine(cuda, oracle):
+    import torch.multiprocessing as mp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, out in outs:
+        assert isinstance(out, dict), out
+    for p in procs:
+        assert p.exitcode == 0
+    n, k = 3_000_017, 1024
+    keys = oracle.splitmix_keys(0x5EED0000, n)
+    want, _ = oracle.algo_r(0xC0FFEE, 0x5A5A, k, keys)
+    want32, _ = oracle.algo_r(0xC0FFEE, 0x5A5A, k, keys.astype(np.int32).astype(np.int64))
+    vals = np.random.default_rng(3).integers(-2**63, 2**63 - 1, size=400_000, dtype=np.int64)
+    vals = np.concatenate([vals, vals[: 150_000]])
+    ref = oracle.Distinct(5000, 9, oracle.HASH_IDENTITY)
+    ref.sample_all(vals)
+    for rank, out in outs:
+        for key in ("elements_long", "elements_long_total"):
+            assert out[key] == (want.tolist(), n), (rank, key)
+        for key in ("elements_int", "elements_int_total"):
+            assert out[key] == (want32.tolist(), n), (rank, key)
+        assert out["distinct"] == (sorted(ref.result()[0].tolist()), vals.size), rank

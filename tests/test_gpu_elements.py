@@ -344,3 +344,19 @@ def test_fused_k1_resolve_publish(cuda, oracle, kt):
         got = s.result()
         assert got.size == min(n, k)
         assert np.array_equal(got, want[: got.size].astype(dt)), (it, k, n)
+
+
+def test_seek_past_k_after_partial_fill(cuda, oracle):
+    """A batch that fills part of the reservoir, then a seek past k (the slots of other ranks'
+    indices), then result(): min(count, k) keys -- the filled ones, then the empty slots as
+    zeros -- never a stale publication of the partial fill (rsv_seek / pub_valid)."""
+    from reservoir_amd import Sampler
+
+    keys = oracle.splitmix_keys(61, 40)
+    for kt, dt in (("long", np.int64), ("int", np.int32)):
+        s = Sampler(100, seed=1, key_type=kt)()
+        s.sample_all(keys.astype(dt))
+        s.seek(5000)
+        got = s.result()
+        assert got.size == 100
+        assert np.array_equal(got[:40], keys.astype(dt)) and (got[40:] == 0).all()

@@ -1,5 +1,7 @@
 """Host-side logic on CPU: the Sampler mirror's validation and the akka Sample-operator semantics
 (SampleImpl.scala:27-57), driven with an oracle-backed stand-in sampler (no GPU here)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -133,3 +135,16 @@ def test_exports():
     for name in ("Sampler", "Sample", "IllegalStateException", "ReservoirError"):
         assert hasattr(reservoir_amd, name)
     assert np.int64 is reservoir_amd.sampler._KEY["long"][1]
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """bench.py --gpus N launches N ranks itself; with fewer visible GPUs it fails loudly (exit 2)
+    instead of running one rank (this container has no GPU)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, env={**os.environ, "HIP_VISIBLE_DEVICES": ""})
+    assert r.returncode == 2, r.stdout + r.stderr
+    assert "--gpus 2 needs 2 visible GPUs" in r.stderr

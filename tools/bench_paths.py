@@ -22,7 +22,9 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from bench import splitmix_fill  # noqa: E402
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import roofline as R  # noqa: E402
+from workloads import c4_data, hash_twins, splitmix_fill  # noqa: E402
 
 HBM = 8000.0
 
@@ -52,37 +54,27 @@ def c3(dev):
     splitmix_fill(keys, 0)
     offs = torch.arange(0, n + 1, L, dtype=torch.int64, device=dev)
     t = timed(lambda: batch.sample_segmented(keys, offs, k, seed=1), reps=5)
-    bytes_alg = n * 8 + S * k * 8
+    l0, l1 = R.k2_calls(S, L, k)
     return {"config": "C3 segmented 2^20 x 4096, k=64", "elements": n, "seconds": t,
-            "Gelem_s": n / t / 1e9, "alg_bytes_per_elem": bytes_alg / n,
-            "achieved_GBs": bytes_alg / t / 1e9, "hbm_frac": bytes_alg / t / 1e9 / HBM}
+            "Gelem_s": n / t / 1e9,
+            "roofline": R.valu_roofline(l0, l1, t, "k2_segmented",
+                                        note="launch time = median of 5 (HIP events); K2 reads only the "
+                                             "64 winning keys per stream (gather), so its bound is VALU"),
+            "winner_gather_bytes": S * k * 8}
 
 
-def c4_data(n, dev):
-    D = int(n * 0.7)
-    v = torch.empty(n, dtype=torch.int64, device=dev)
-    splitmix_fill(v[:D], 0xD15C << 32)
-    # duplicates: element i >= D copies a pseudo-random earlier distinct value
-    idx = (torch.arange(D, n, dtype=torch.int64, device=dev) * 2654435761) % D
-    v[D:] = v[idx]
-    # scatter positions by an affine bijection of [0, n)
-    a = 1_000_000_007
-    perm = (torch.arange(n, dtype=torch.int64, device=dev) * a + 12345) % n
-    out = torch.empty_like(v)
-    out[perm] = v
-    return out
-
-
-def c4(dev, hash_kind="identity", order="auto"):
+def c4(dev, hash_kind="identity", order="auto", twins=False, seed=7):
     from reservoir_amd import Sampler, _native
 
     n, k = 500_000_000, 65536
     vals = c4_data(n, dev)
+    if twins:
+        vals = hash_twins(vals, 26)
     torch.cuda.synchronize()
     L = _native.load()
     times, kern = [], []
     for rep in range(4):
-        mk = Sampler.distinct(k, seed=7, order=order)
+        mk = Sampler.distinct(k, seed=seed, order=order)
         d = mk(hash=hash_kind) if hash_kind != "default" else mk()
         d.set_stream(torch.cuda.current_stream().cuda_stream)
         _native.check(L.rsv_profile_enable(d.handle, 1))
@@ -102,10 +94,17 @@ def c4(dev, hash_kind="identity", order="auto"):
     kt, passes = kern[0]
     ordered = order == "ordered" or (order == "auto" and hash_kind == "default")
     read = n * 8 if ordered else n * 8 * passes  # ordered: one chunked pass; set: every pass reads all
-    return {"config": f"C4 (one GPU's share) distinct 5e8 keys 30% dup, k=65536, hash={hash_kind}, order={order}",
+    name = "hash twins (~5 distinct keys per Long.hashCode: the boundary bucket is oversubscribed, the host " \
+           "replay of the logged candidates runs)" if twins else "30% dup"
+    return {"config": f"C4 (one GPU's share) distinct 5e8 keys {name}, k=65536, hash={hash_kind}, order={order}",
             "elements": n, "seconds_end_to_end": t, "Gelem_s": n / t / 1e9,
             "filter_launches": passes, "filter_seconds_total": kt,
             "filter_achieved_GBs": read / kt / 1e9, "hbm_frac_filter": read / kt / 1e9 / HBM}
+
+
+def c4_replay(dev):
+    """C4's share with hash twins: the ordered mode's host-replay branch, as its own line."""
+    return c4(dev, "default", twins=True, seed=11)
 
 
 def c2l(dev):
@@ -147,6 +146,8 @@ def main():
         torch.cuda.empty_cache()
     if "c4o" in todo:  # default hash, auto -> ordered only (for traces)
         print(json.dumps(c4(dev, "default")), flush=True)
+    if "c4r" in todo:  # the ordered replay branch
+        print(json.dumps(c4_replay(dev)), flush=True)
     if "c4i" in todo:  # identity hash only (for traces)
         print(json.dumps(c4(dev, "identity")), flush=True)
     if "c2l" in todo:

@@ -1,0 +1,90 @@
+"""Synthetic inputs of BASELINE.json's configs, generated on the device with torch.
+
+Shared by bench.py, tools/bench_paths.py and the full-size parity tests (tests/test_gpu_configs.py).
+torch int64 arithmetic wraps like Java Long; logical right shifts are emulated with a mask.
+
+  splitmix_fill(out, base)      out[i] = splitmix64(base + i)                        (C1, C2, C3)
+  c4_data(n, dev)               C4: D = 0.7 n distinct values v_j = splitmix64(j ^ 0xD15C); element
+                                i takes v_i for i < D and v_{hash(i) mod D} otherwise (the 30 %
+                                duplicates), hash(i) = splitmix64(i ^ 0xD0B) >>> 1; positions
+                                shuffled by a 4-round Feistel permutation of [0, n) (seed 7,
+                                cycle-walking)
+  hash_twins(keys, bits)        keys whose java.lang.Long.hashCode takes only 2^bits values (many
+                                distinct keys per hash bucket: the ordered distinct path's replay)
+"""
+from __future__ import annotations
+
+import torch
+
+_G = 0x9E3779B97F4A7C15 - (1 << 64)
+_M1 = 0xBF58476D1CE4E5B9 - (1 << 64)
+_M2 = 0x94D049BB133111EB - (1 << 64)
+
+
+def _srl(z: torch.Tensor, s: int) -> torch.Tensor:
+    """Logical right shift of int64 (Java >>>)."""
+    return (z >> s) & ((1 << (64 - s)) - 1)
+
+
+def smix(x: torch.Tensor) -> torch.Tensor:
+    """splitmix64(x) elementwise (x as int64 bits)."""
+    z = x + _G
+    z = (z ^ _srl(z, 30)) * _M1
+    z = (z ^ _srl(z, 27)) * _M2
+    return z ^ _srl(z, 31)
+
+
+def splitmix_fill(out: torch.Tensor, base: int, chunk: int = 1 << 27) -> None:
+    """out[i] = splitmix64(base + i) (C2 base 0x5EED0000, C3 base 0)."""
+    n = out.numel()
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        out[a:b] = smix(torch.arange(base + a, base + b, dtype=torch.int64, device=out.device))
+
+
+def feistel_perm(n: int, seed: int, device, chunk: int = 1 << 26) -> torch.Tensor:
+    """A bijection of [0, n): 4-round balanced Feistel network on 2h >= log2(n) bits, cycle-walked
+    back into range."""
+    bits = max(2, (n - 1).bit_length())
+    bits += bits & 1
+    h = bits // 2
+    mask = (1 << h) - 1
+
+    def enc(x):
+        lo, hi = x & mask, x >> h
+        for r in range(4):
+            f = smix(lo + ((seed * 4 + r) << 40)) & mask
+            lo, hi = hi ^ f, lo
+        return (hi << h) | lo
+
+    y = torch.empty(n, dtype=torch.int64, device=device)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        y[a:b] = enc(torch.arange(a, b, dtype=torch.int64, device=device))
+    while True:
+        bad = torch.nonzero(y >= n).flatten()
+        if bad.numel() == 0:
+            return y
+        y[bad] = enc(y[bad])
+
+
+def c4_data(n: int, device, dup: float = 0.3, seed: int = 7, chunk: int = 1 << 26) -> torch.Tensor:
+    """C4: n Long keys, D = (1 - dup) n distinct values, Feistel-shuffled."""
+    D = int(round(n * (1.0 - dup)))
+    vals = torch.empty(n, dtype=torch.int64, device=device)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        i = torch.arange(a, b, dtype=torch.int64, device=device)
+        vi = torch.where(i < D, i, _srl(smix(i ^ 0xD0B), 1) % max(D, 1))
+        vals[a:b] = smix(vi ^ 0xD15C)
+    perm = feistel_perm(n, seed, device)
+    out = torch.empty_like(vals)
+    out[perm] = vals
+    return out
+
+
+def hash_twins(keys: torch.Tensor, bits: int = 24) -> torch.Tensor:
+    """(hi, lo) -> (hi, hi ^ (lo & (2^bits - 1))): Long.hashCode = hi ^ lo' = lo & (2^bits - 1)."""
+    hi = _srl(keys, 32)
+    lo = (hi ^ (keys & ((1 << bits) - 1))) & 0xFFFFFFFF
+    return (hi << 32) | lo
