@@ -30,11 +30,11 @@ constexpr uint32_t kPhiloxW0 = 0x9E3779B9u;
 constexpr uint32_t kPhiloxW1 = 0xBB67AE85u;
 constexpr uint32_t kDomainLevel1 = 0x80000000u;
 
-// three-input xor in one VALU op (gfx950 has no v_xor3_b32; v_bitop3_b32 with truth table 0x96)
+// three-input xor in one VALU op (gfx950 has no v_xor3_b32; v_bitop3_b32 with truth table 0x96).
+// The builtin, not inline asm: the hazard recognizer pads every inline-asm block with an s_nop
+// (13 per K1 iteration of two blocks, ~14 % of its issue slots), and the scheduler cannot move it.
 __device__ __forceinline__ uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t key) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(key));
-    return r;
+    return __builtin_amdgcn_bitop3_b32(a, b, key, 0x96);
 }
 
 // Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11).  k0/k1 are wave-uniform (kernel args), so
@@ -59,12 +59,14 @@ __device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_
 // and round 1's first product are then scalar (SALU, hoisted out of any loop over c0), and round
 // 1's xors take one scalar operand each -- 18 v_mad_u64_u32 + 1 v_bitop3 + 2 v_xor per call
 // instead of 19 + 20 (the asm xor3 forces VGPR operands, so the uniform part must stay in C).
+// `add0` = kPhiloxM0 * d for counter c0 + d (d wave-uniform): the addend of the first product's
+// v_mad_u64_u32, so a lane evaluating the blocks at c0 and c0 + 64 needs no v_add for the second.
 __device__ __forceinline__ u32x4 philox4x32_10_uniform_hi(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                                          uint32_t k0, uint32_t k1) {
+                                                          uint32_t k0, uint32_t k1, uint64_t add0 = 0) {
     // round 0
     const uint64_t p1u = (uint64_t)kPhiloxM1 * c2;                  // scalar
     const uint32_t n0u = (uint32_t)(p1u >> 32) ^ c1 ^ k0;           // scalar
-    const uint64_t p0 = (uint64_t)kPhiloxM0 * c0;                   // vector
+    const uint64_t p0 = (uint64_t)kPhiloxM0 * c0 + add0;            // vector: M0 (c0 + d) mod 2^64
     uint32_t d2 = xor3_key((uint32_t)(p0 >> 32), c3, k1);           // vector (c3 ^ k1 is scalar)
     const uint32_t d1u = (uint32_t)p1u;                             // scalar
     uint32_t d3 = (uint32_t)p0;                                     // vector

@@ -4,7 +4,7 @@
 //   K1  k1_last_writer   single stream: per-slot last writer (max index) of an index range
 //   --  resolve          fill phase + gather of the winning keys into the reservoir
 //   K1' replay_events    the reference's Algorithm-L eviction events -> per-slot last writer
-//   K2  k2_segmented     one wave per independent stream, slot table in LDS
+//   K2  k2_segmented_v1  round-1 segmented kernel (K2 is rsv_segmented.hip)
 //   --  merge_slots      multi-GPU combine of exported partial reservoirs (last writer wins)
 //
 // None of these kernels streams the key array: a draw depends only on (seed, stream, index), so
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void export_draws_kernel(DrawKey dk, uint64
 // waves of a workgroup never synchronise with each other (no __syncthreads); each wave walks its
 // own sequence of streams and prefetches the next stream's offsets.
 template <typename KeyT>
-__global__ __launch_bounds__(kBlock) void k2_segmented(const KeyT* __restrict__ keys,
+__global__ __launch_bounds__(kBlock) void k2_segmented_v1(const KeyT* __restrict__ keys,
                                                        const int64_t* __restrict__ offsets, int64_t S,
                                                        uint32_t k, uint32_t k0, uint32_t k1,
                                                        uint64_t stream_base, KeyT* __restrict__ out,
@@ -632,9 +632,10 @@ int segmented_waves_per_block(uint32_t k) {
     return (int)(w < 1 ? 1 : (w > 4 ? 4 : w));
 }
 
-hipError_t launch_segmented(const void* keys, int key_width, const int64_t* offsets, int64_t S,
-                            uint32_t k, const DrawParams& dp, void* out, int64_t* counts,
-                            hipStream_t st) {
+// the round-1 K2 (rsv_segmented.hip launch_segmented: RSV_K2=1, or a table too big for its LDS)
+hipError_t launch_segmented_v1(const void* keys, int key_width, const int64_t* offsets, int64_t S,
+                               uint32_t k, const DrawParams& dp, void* out, int64_t* counts,
+                               hipStream_t st) {
     if (S <= 0) return hipSuccess;
     const int wpb = segmented_waves_per_block(k);
     const size_t lds = (size_t)wpb * (k + kQueue) * sizeof(unsigned long long);
@@ -643,10 +644,10 @@ hipError_t launch_segmented(const void* keys, int key_width, const int64_t* offs
     const unsigned grid = (unsigned)(blocks < cap ? blocks : cap);
     const uint32_t k0 = (uint32_t)dp.seed, k1 = (uint32_t)(dp.seed >> 32);
     if (key_width == 8)
-        hipLaunchKernelGGL(k2_segmented<int64_t>, dim3(grid), dim3(64 * wpb), lds, st,
+        hipLaunchKernelGGL(k2_segmented_v1<int64_t>, dim3(grid), dim3(64 * wpb), lds, st,
                            (const int64_t*)keys, offsets, S, k, k0, k1, dp.stream, (int64_t*)out, counts);
     else
-        hipLaunchKernelGGL(k2_segmented<int32_t>, dim3(grid), dim3(64 * wpb), lds, st,
+        hipLaunchKernelGGL(k2_segmented_v1<int32_t>, dim3(grid), dim3(64 * wpb), lds, st,
                            (const int32_t*)keys, offsets, S, k, k0, k1, dp.stream, (int32_t*)out, counts);
     return hipGetLastError();
 }

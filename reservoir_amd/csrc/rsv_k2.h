@@ -1,0 +1,252 @@
+// rsv_k2.h -- the K2 segmented kernel (rsv_segmented.hip launches it; tools/micro_k2.hip includes
+// it for variant timing).  See rsv_segmented.hip for the design.
+#pragma once
+#include <algorithm>
+#include <type_traits>
+
+#include "rsv_device.h"
+
+namespace rsv {
+namespace k2 {
+
+constexpr int kWaves = 4;          // waves per workgroup
+constexpr uint32_t kRing = 4;      // level-0 iterations whose block words stay addressable
+constexpr uint32_t kQCap = 2048;   // FIFO entries: < 64 pending + <= 64 x 16 appended per iteration
+constexpr uint32_t kStashBytes = kRing * 64 * 16;
+constexpr uint32_t kQueueBytes = kQCap * 2;
+constexpr uint32_t kLut = 1024;    // blocks (16 indices each) whose threshold T is tabulated per workgroup
+constexpr uint32_t kLutBytes = kLut * 2;
+constexpr int64_t kSmallLen = 1ll << 27;  // streams shorter than this use 32-bit index arithmetic
+
+// bytes of dynamic LDS per workgroup: T table + per wave (stash | FIFO | k-slot table)
+__host__ __device__ inline size_t lds_bytes(uint32_t k) {
+    return kLutBytes + (size_t)kWaves * (kStashBytes + kQueueBytes + (size_t)k * 8);
+}
+
+// T = ceil(256 k / (i0 + 1)), the block threshold of the dense region (T > 255: every byte is a
+// candidate -> 256); 0 marks the sparse region (i0 + 1 >= 256 k: only b == 0 can hit)
+__device__ __forceinline__ uint32_t block_threshold(uint64_t i0, uint64_t dense_lim) {
+    if (i0 + 1 >= dense_lim) return 0;
+    const uint64_t T = (dense_lim + i0) / (i0 + 1);
+    return T > 255 ? 256u : (uint32_t)T;
+}
+
+// b_e < T for the 16 bytes of a block (1 <= T <= 255), bit-sliced: the borrow out of (T - 1) - b,
+// planes LSB first, one v_bitop3 per plane (borrow' = bit p of T-1 ? plane & borrow : plane | borrow;
+// table 0xD4 in the A = 0xF0, B = 0xCC, C = 0xAA convention).  The high 16 bits are don't-care.
+__device__ __forceinline__ uint32_t lt_mask16_borrow(const u32x4& w, uint32_t T) {
+    const uint32_t M = T - 1;
+    const uint32_t words[4] = {w.x, w.y, w.z, w.w};
+    uint32_t br = 0;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const uint32_t plane = (p & 1) ? (words[p >> 1] >> 16) : words[p >> 1];
+        const uint32_t mm = (uint32_t)((int32_t)(M << (31 - p)) >> 31);  // all ones iff bit p of T-1
+        br = __builtin_amdgcn_bitop3_b32(plane, br, mm, 0xD4);
+    }
+    return ~br & 0xFFFFu;
+}
+
+__device__ __forceinline__ uint32_t mask_for(const u32x4& w, uint32_t T) {
+    return T == 0 ? zero_byte_mask16(w) : T > 255 ? 0xFFFFu : lt_mask16_borrow(w, T);
+}
+
+__device__ __forceinline__ uint32_t clip16(uint64_t i0, uint64_t lo, uint64_t hi) {
+    uint32_t m = 0xFFFFu;
+    if (i0 < lo) m = (lo - i0 >= 16) ? 0u : ((0xFFFFu << (uint32_t)(lo - i0)) & 0xFFFFu);
+    if (i0 + 16 > hi) m &= (hi <= i0) ? 0u : (0xFFFFu >> (uint32_t)(16 - (hi - i0)));
+    return m;
+}
+
+// inclusive prefix sum over the wave (DPP: row shifts within 16-lane rows, then row broadcasts)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return x;
+}
+
+// b_i * (i+1) / 2^8 .. with the level-1 word: j = floor(((b << 56) | (L >> 8)) (i + 1) / 2^64)
+__device__ __forceinline__ uint64_t draw_j(uint32_t b, uint64_t L, uint64_t i1, bool small) {
+    const uint64_t U = ((uint64_t)b << 56) | (L >> 8);
+    if (small) {  // i + 1 < 2^32: a 64 x 32 product
+        const uint32_t x = (uint32_t)i1;
+        const uint64_t lo = (uint64_t)(uint32_t)U * x;
+        const uint64_t hi = (uint64_t)(uint32_t)(U >> 32) * x + (lo >> 32);
+        return hi >> 32;
+    }
+    return __umul64hi(U, i1);
+}
+
+struct Wave {
+    u32x4* stash;
+    uint16_t* q;
+    void* tab;
+    const uint16_t* lut;
+    uint32_t lane, k, k0, k1;
+    uint64_t dense_lim;
+};
+
+// One stream on one wave.  SMALL: n < 2^27 -- 32-bit indices, u32 winner table, and Philox counters
+// whose high words are wave-uniform (level 0: g < 2^32; level 1: i/2 < 2^32).
+// DEFER (k <= 64): the lane's winner key is returned instead of stored -- the caller stores it
+// after the next stream's draws, so the random gather's latency overlaps them
+template <typename KeyT, int V, bool SMALL, bool DEFER>
+__device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict__ keys, int64_t off, int64_t len,
+                                          uint64_t stream, KeyT* __restrict__ o) {
+    using IdxT = typename std::conditional<SMALL, uint32_t, uint64_t>::type;
+    const uint32_t lane = W.lane, k = W.k;
+    IdxT* tab = (IdxT*)W.tab;
+    for (uint32_t j = lane; j < k; j += 64) tab[j] = 0;
+    const uint32_t s0 = (uint32_t)stream, s1 = (uint32_t)(stream >> 32);
+    const DrawKey dk{W.k0, W.k1, s0, s1};
+    const IdxT n_groups = (IdxT)(((uint64_t)len + 15) >> 4);
+    uint32_t head = 0, tail = 0;  // FIFO positions (wave-uniform, wrap mod 2^32)
+    uint32_t ring = 0;
+    IdxT gb = (IdxT)(k >> 4);
+
+    // resolve FIFO entries [head, head + nvalid) (nvalid <= 64), one per lane; (last_gb, last_ring)
+    // = the most recently stashed iteration, so an entry's age is (last_ring - r) & 3
+    auto resolve_round = [&](uint32_t nvalid, IdxT last_gb, uint32_t last_ring) {
+        __builtin_amdgcn_wave_barrier();
+        const bool valid = lane < nvalid;
+        const uint32_t ent = valid ? W.q[(head + lane) & (kQCap - 1)] : 0u;
+        const uint32_t r = ent >> 10, e = ent & 15u;
+        const u32x4 w = W.stash[ent >> 4];  // ring slot * 64 + lane
+        const IdxT gbr = last_gb - (IdxT)64 * ((last_ring - r) & (kRing - 1));
+        const IdxT i = (gbr << 4) + (ent & 0x3FFu);  // ((gbr + ln) << 4) + e
+        const uint32_t b = level0_byte(w, e);
+        const IdxT g1 = i >> 1;
+        u32x4 w1;
+        if constexpr ((V & 2) != 0) {  // variant: no level-1 Philox (cost probe)
+            w1 = u32x4{(uint32_t)g1 * 0x9E3779B9u, (uint32_t)g1 ^ s0, w.x, w.y};
+        } else if constexpr (SMALL) {
+            w1 = philox4x32_10_uniform_hi((uint32_t)g1, kDomainLevel1, s0, s1, W.k0, W.k1);
+        } else {
+            w1 = philox4x32_10((uint32_t)g1, (uint32_t)((uint64_t)g1 >> 32) | kDomainLevel1, s0, s1, W.k0, W.k1);
+        }
+        const uint64_t L = (i & 1) ? (((uint64_t)w1.z << 32) | w1.w) : (((uint64_t)w1.x << 32) | w1.y);
+        const uint64_t j = draw_j(b, L, (uint64_t)i + 1, SMALL);
+        if (valid && j < k) atomicMax(&tab[(uint32_t)j], i);
+        head += nvalid;
+        __builtin_amdgcn_wave_barrier();
+    };
+
+    for (; gb < n_groups; gb += 64, ring = (ring + 1) & (kRing - 1)) {
+        // the oldest pending candidate still refers to the ring slot about to be overwritten
+        if (tail != head && ((uint32_t)__builtin_amdgcn_readfirstlane((int)W.q[head & (kQCap - 1)]) >> 10) == ring) {
+            while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head), gb - 64, ring - 1);
+        }
+        const IdxT g = gb + lane;
+        const bool valid = g < n_groups;
+        u32x4 w;
+        if constexpr (SMALL) w = philox4x32_10_uniform_hi((uint32_t)g, 0u, s0, s1, W.k0, W.k1);
+        else w = level0(dk, (uint64_t)g);
+        const uint64_t i0 = (uint64_t)g << 4;
+        const uint32_t T = g < kLut ? (uint32_t)W.lut[(uint32_t)g] : block_threshold(i0, W.dense_lim);
+        uint32_t mask = valid ? mask_for(w, T) : 0u;
+        if (__builtin_amdgcn_readfirstlane((int)(((uint64_t)gb << 4) < k || (((uint64_t)gb + 64) << 4) > (uint64_t)len)))
+            mask &= clip16(i0, k, (uint64_t)len);
+        W.stash[ring * 64 + lane] = w;
+        // FIFO offsets: one wave prefix sum of the per-lane candidate counts
+        const uint32_t cnt = (uint32_t)__popc(mask);
+        const uint32_t incl = wave_incl_scan(cnt);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        uint32_t pos = tail + incl - cnt;
+        const uint32_t tag = (ring << 10) | (lane << 4);
+        while (mask) {
+            const uint32_t e = __builtin_ctz(mask);
+            mask &= mask - 1;
+            W.q[pos & (kQCap - 1)] = (uint16_t)(tag | e);
+            ++pos;
+        }
+        tail += tot;
+        if constexpr ((V & 8) != 0) head = tail;  // variant: candidates dropped (cost probe)
+        while (tail - head >= 64) resolve_round(64u, gb, ring);
+    }
+    while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head), gb - 64, ring - 1);
+    __builtin_amdgcn_wave_barrier();
+    if constexpr (DEFER) {
+        KeyT v = 0;
+        if (lane < k) {
+            const IdxT wi = tab[lane];
+            v = wi ? keys[off + (int64_t)wi] : ((int64_t)lane < len ? keys[off + lane] : (KeyT)0);
+        }
+        __builtin_amdgcn_wave_barrier();
+        return v;
+    }
+    for (uint32_t j = lane; j < k; j += 64) {
+        const IdxT wi = tab[j];
+        if constexpr ((V & 1) != 0)  // variant: no winner-key gather (cost probe)
+            o[j] = (KeyT)wi;
+        else
+            o[j] = wi ? keys[off + (int64_t)wi] : ((int64_t)j < len ? keys[off + j] : (KeyT)0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return (KeyT)0;
+}
+
+// V: development variants for tools/micro_k2.hip (0 = the product kernel)
+template <typename KeyT, int V = 0>
+__global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restrict__ keys,
+                                                            const int64_t* __restrict__ offsets, int64_t S,
+                                                            uint32_t k, uint32_t k0, uint32_t k1, uint64_t stream_base,
+                                                            KeyT* __restrict__ out, int64_t* __restrict__ counts) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    uint16_t* lut = (uint16_t*)lds;
+    const uint64_t dense_lim = 256ull * k;
+    for (uint32_t g = threadIdx.x; g < kLut; g += blockDim.x) lut[g] = (uint16_t)block_threshold((uint64_t)g << 4, dense_lim);
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // per wave: stash [kRing][64] x 16 B | FIFO kQCap x u16 | last-writer table k x (u32 | u64)
+    unsigned char* base = lds + kLutBytes + (size_t)wave * (kStashBytes + kQueueBytes + (size_t)k * 8);
+    const Wave W{(u32x4*)base, (uint16_t*)(base + kStashBytes), base + kStashBytes + kQueueBytes, lut, lane, k,
+                 k0, k1, dense_lim};
+    const int64_t wave_stride = (int64_t)gridDim.x * kWaves;
+    int64_t s = (int64_t)blockIdx.x * kWaves + wave;
+    int64_t off = 0, end = 0;
+    if (s < S) {
+        off = offsets[s];
+        end = offsets[s + 1];
+    }
+    const bool defer = k <= 64 && (V & 16) == 0 && (V & 1) == 0;
+    KeyT* pend_o = nullptr;
+    KeyT pend_v = 0;
+    for (; s < S; s += wave_stride) {
+        // wave-uniform stream bounds (scalar registers: uniform control flow below)
+        off = ((int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)off)) |
+              ((int64_t)__builtin_amdgcn_readfirstlane((int)(off >> 32)) << 32);
+        end = ((int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)end)) |
+              ((int64_t)__builtin_amdgcn_readfirstlane((int)(end >> 32)) << 32);
+        const int64_t len = end - off;
+        const int64_t s_next = s + wave_stride;
+        int64_t off_next = 0, end_next = 0;
+        if (s_next < S) {  // prefetch: in flight during this stream's work
+            off_next = offsets[s_next];
+            end_next = offsets[s_next + 1];
+        }
+        const uint64_t stream = stream_base + (uint64_t)s;
+        KeyT* o = out + s * (int64_t)k;
+        if (defer) {  // k <= 64: this stream's key is stored after the next stream's draws
+            const KeyT v = len < kSmallLen ? k2_stream<KeyT, V, true, true>(W, keys, off, len, stream, o)
+                                           : k2_stream<KeyT, V, false, true>(W, keys, off, len, stream, o);
+            if (pend_o && lane < k) pend_o[lane] = pend_v;
+            pend_o = o;
+            pend_v = v;
+        } else if (len < kSmallLen) {
+            k2_stream<KeyT, V, true, false>(W, keys, off, len, stream, o);
+        } else {
+            k2_stream<KeyT, V, false, false>(W, keys, off, len, stream, o);
+        }
+        if (lane == 0) counts[s] = len < (int64_t)k ? len : (int64_t)k;
+        off = off_next;
+        end = end_next;
+    }
+    if (pend_o && lane < k) pend_o[lane] = pend_v;
+}
+
+}  // namespace k2
+}  // namespace rsv

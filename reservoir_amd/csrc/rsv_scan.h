@@ -193,11 +193,12 @@ __device__ __forceinline__ void k1_body(const DrawKey& dk, uint32_t k, uint64_t 
 // into a register mask; every W = 32 / U iterations the wave pushes the set bits in rounds -- each
 // round every lane with bits left pushes its lowest one (ballot + prefix count), so a round is one
 // wave-uniform step and the queue needs room for just one round (64) beyond a partial batch.
-// Bit b of a window starting at `base0` is the block at offset base0 + (b / U) * stride + (b % U) * 64
-// + lane (all 32-bit: offsets < 2^31 per launch, stride * W < 2^32).
+// The window's nb bits are shifted in oldest first (bits = bits * 2 + has: one v_lshl_or per block),
+// so bit b is window block idx = nb - 1 - b, the block at offset base0 + (idx / U) * stride +
+// (idx % U) * 64 + lane (all 32-bit: offsets < 2^31 per launch, stride * W < 2^32).
 template <int U, class Hit>
-__device__ __forceinline__ void push_bits(uint32_t bits, uint32_t base0, uint32_t stride, uint32_t* q, uint32_t& qn,
-                                          uint64_t* cq, uint32_t& cqn, uint32_t lane, const DrawKey& dk,
+__device__ __forceinline__ void push_bits(uint32_t bits, uint32_t nb, uint32_t base0, uint32_t stride, uint32_t* q,
+                                          uint32_t& qn, uint64_t* cq, uint32_t& cqn, uint32_t lane, const DrawKey& dk,
                                           uint64_t g_begin, uint64_t lo, uint64_t hi, uint64_t dense_lim, uint32_t k,
                                           Hit& hit) {
     const unsigned long long lt = lanemask_lt64();
@@ -205,9 +206,9 @@ __device__ __forceinline__ void push_bits(uint32_t bits, uint32_t base0, uint32_
         const bool has = bits != 0;
         const unsigned long long bal = __ballot(has);
         if (has) {
-            const uint32_t b = __builtin_ctz(bits);
+            const uint32_t idx = nb - 1 - __builtin_ctz(bits);
             bits &= bits - 1;
-            q[qn + __popcll(bal & lt)] = base0 + (b / U) * stride + (b % U) * 64u + lane;
+            q[qn + __popcll(bal & lt)] = base0 + (idx / U) * stride + (idx % U) * 64u + lane;
         }
         qn += (uint32_t)__popcll(bal);
         if (qn >= 64) {
@@ -245,25 +246,27 @@ __device__ __forceinline__ void k1_body_bits(const DrawKey& dk, uint32_t k, uint
     uint32_t gl = (uint32_t)g_begin + base + lane;
     while (base < ng) {  // wave-uniform
         const uint32_t base0 = base;
-        uint32_t bits = 0;
-        for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride) {
+        uint32_t bits = 0, nb = 0;
+        for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride, nb += U) {
             u32x4 w[U];
+            // block u's counter is gl + 64 u: the addend rides in the first product (no v_add)
 #pragma unroll
-            for (int u = 0; u < U; ++u) w[u] = philox4x32_10_uniform_hi(gl + u * 64, ghi, dk.s0, dk.s1, dk.k0, dk.k1);
+            for (int u = 0; u < U; ++u)
+                w[u] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
             if (base >= off_sparse && base + U * 64 <= ng) {  // steady state: zero-byte test only
 #pragma unroll
-                for (int u = 0; u < U; ++u) bits |= (uint32_t)any_zero_byte(w[u]) << (t * U + u);
+                for (int u = 0; u < U; ++u) bits = (bits << 1) | (uint32_t)any_zero_byte(w[u]);
             } else {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t off = base + u * 64 + lane;
                     const bool has =
                         (off < ng) & (((((g_begin + off) << 4) + 1) < dense_lim) | any_zero_byte(w[u]));
-                    bits |= (uint32_t)has << (t * U + u);
+                    bits = (bits << 1) | (uint32_t)has;
                 }
             }
         }
-        push_bits<U>(bits, base0, stride, q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
+        push_bits<U>(bits, nb, base0, stride, q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
     }
     drain_blocks(q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
 }

@@ -11,8 +11,8 @@ while [ $# -gt 0 ]; do
     name=$1 limit=$2
     shift 2
     cmd=()
-    while [ $# -gt 0 ] && [ "$1" != "--" ]; do cmd+=("$1"); shift; done
-    [ "$1" == "--" ] && shift
+    while [ $# -gt 0 ] && [ "$1" != "::" ]; do cmd+=("$1"); shift; done
+    [ "$1" == "::" ] && shift
     echo "== $name (limit $limit s): ${cmd[*]}"
     timeout -k 10 "$limit" "${cmd[@]}" > "$O/$name.log" 2>&1
     rc=$?

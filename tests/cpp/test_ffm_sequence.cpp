@@ -1,0 +1,327 @@
+// test_ffm_sequence.cpp -- replays, on the GPU and without a JDK, exactly the call sequences the two
+// JVM bindings drive:
+//   ffm   FfmMirror below: statement for statement the Panama FFM binding
+//         bindings/scala/lgbt/princess/reservoir/gpu/FfmSampler.scala over the raw C ABI
+//         (stage_acquire / commit per ~1 Mi keys, open tracked on the JVM side, the single-use
+//         result() destroys the handle and nothing touches it afterwards)
+//   jni   bindings/jvm/rsv_jvm.c, the session logic every JNI native method of
+//         bindings/jni/reservoir_jni.c consists of (sample per element, sampleAll over arrays)
+//   abi   per-element rsv_sample (the engine's own staging), for the akka path at C5's k = 1 Mi
+// Each case line of argv[1] names the sampler, its keys (splitmix64(base + i), or a binary key file)
+// and a binary file with the oracle's expected result (tests/test_gpu_ffm.py writes them);
+// distinct results compare as sets.
+// Prints PASS/FAIL per case; exit status = number of failures.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../bindings/jvm/rsv_jvm.h"
+#include "../../include/reservoir_hip.h"
+
+static int failures = 0;
+#define EXPECT(c, what)                                                                  \
+    do {                                                                                 \
+        if (!(c)) {                                                                      \
+            std::printf("FAIL %s: %s (%s:%d)\n", what, #c, __FILE__, __LINE__);          \
+            ++failures;                                                                  \
+        }                                                                                \
+    } while (0)
+
+struct JvmException : std::runtime_error {
+    rsv_status status;
+    JvmException(rsv_status st, const std::string& m) : std::runtime_error(m), status(st) {}
+};
+
+// Native.check of FfmSampler.scala: status -> the reference's exception
+static void check(rsv_status st) {
+    if (st != RSV_OK) throw JvmException(st, rsv_last_error());
+}
+
+static uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// ---- FfmMirror: FfmSampler.scala, line for line ------------------------------------------------
+struct FfmMirror {
+    rsv_sampler* handle = nullptr;
+    bool open = true;  // tracked on the JVM side: isOpen makes no downcall
+    bool reusable, precomputed;
+    int width, k;
+    uint8_t* stage = nullptr;
+    int64_t* stage_hash = nullptr;
+    int64_t cap = 0, filled = 0;
+
+    FfmMirror(const rsv_config& c)
+        : reusable(c.reusable != 0), precomputed(c.kind == RSV_KIND_DISTINCT && c.hash_kind == RSV_HASH_PRECOMPUTED),
+          width(c.key_width), k(c.max_sample_size) {
+        check(rsv_create(&c, &handle));
+    }
+    void next_stage() {
+        if (filled > 0) {
+            const int64_t f = filled;
+            filled = 0;
+            cap = 0;
+            check(rsv_stage_commit(handle, f));
+        }
+        void* keys = nullptr;
+        int64_t* hashes = nullptr;
+        check(rsv_stage_acquire(handle, &keys, precomputed ? &hashes : nullptr, &cap));
+        stage = (uint8_t*)keys;
+        stage_hash = hashes;
+    }
+    void sample(const void* key, int64_t hash) {
+        if (!open) throw JvmException(RSV_E_ILLEGAL_STATE, "use of sampler after calling `result()`");
+        if (filled == cap) next_stage();
+        std::memcpy(stage + filled * width, key, (size_t)width);
+        if (precomputed) stage_hash[filled] = hash;
+        filled += 1;
+    }
+    std::vector<uint8_t> result(int64_t* n_out) {
+        if (!open) throw JvmException(RSV_E_ILLEGAL_STATE, "use of sampler after calling `result()`");
+        if (filled > 0) {
+            const int64_t f = filled;
+            filled = 0;
+            check(rsv_stage_commit(handle, f));
+        }
+        cap = 0;  // the staging pointers die with the next call on the handle
+        std::vector<uint8_t> out((size_t)k * width);
+        int64_t n = 0;
+        check(rsv_result(handle, out.data(), k, &n));
+        out.resize((size_t)n * width);
+        if (!reusable) {  // SingleUse.close: the handle is destroyed and never touched again
+            open = false;
+            rsv_destroy(handle);
+            handle = nullptr;
+        }
+        *n_out = n;
+        return out;
+    }
+    ~FfmMirror() {
+        if (handle) rsv_destroy(handle);  // the Cleaner of a reusable sampler
+    }
+};
+
+// ---- cases ---------------------------------------------------------------------------------------
+struct Case {
+    std::string name, path, expected, keyfile;  // keyfile (optional): the keys, else splitmix64(base + i)
+    std::vector<uint8_t> keys;
+    int kind, k, kw, reusable, hash_kind, order, engine;
+    uint64_t seed, stream, base;
+    int64_t n;
+};
+
+static std::vector<uint8_t> read_file(const std::string& p) {
+    std::ifstream f(p, std::ios::binary);
+    return std::vector<uint8_t>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+// key i of the case, written into `dst` (kw bytes), and its precomputed hash (31 x + 7)
+static int64_t make_key(const Case& c, int64_t i, void* dst) {
+    if (!c.keys.empty()) {
+        std::memcpy(dst, c.keys.data() + i * c.kw, (size_t)c.kw);
+        int64_t v = 0;
+        if (c.kw == 8) std::memcpy(&v, dst, 8);
+        else {
+            int32_t w;
+            std::memcpy(&w, dst, 4);
+            v = w;
+        }
+        return (int64_t)((uint64_t)v * 31u + 7u);
+    }
+    const int64_t v = (int64_t)splitmix64(c.base + (uint64_t)i);
+    if (c.kw == 8) {
+        std::memcpy(dst, &v, 8);
+        return (int64_t)((uint64_t)v * 31u + 7u);
+    }
+    const int32_t w = (int32_t)(v >> 33);
+    std::memcpy(dst, &w, 4);
+    return (int64_t)((uint64_t)(int64_t)w * 31u + 7u);
+}
+
+static bool same(const Case& c, std::vector<uint8_t> got, int64_t n) {
+    std::vector<uint8_t> want = read_file(c.expected);
+    if ((int64_t)want.size() != n * c.kw || got.size() != want.size()) {
+        std::printf("  %s: size %lld keys, expected %zu\n", c.name.c_str(), (long long)n, want.size() / c.kw);
+        return false;
+    }
+    if (c.kind == RSV_KIND_DISTINCT) {  // HashSet order in the reference: compare as sets
+        auto sort_keys = [&](std::vector<uint8_t>& b) {
+            if (c.kw == 8) std::sort((int64_t*)b.data(), (int64_t*)b.data() + n);
+            else std::sort((int32_t*)b.data(), (int32_t*)b.data() + n);
+        };
+        sort_keys(got);
+        sort_keys(want);
+    }
+    return got == want;
+}
+
+static rsv_config config_of(const Case& c) {
+    rsv_config cfg;
+    rsv_config_init(&cfg);
+    cfg.kind = c.kind;
+    cfg.max_sample_size = c.k;
+    cfg.key_width = c.kw;
+    cfg.reusable = c.reusable;
+    cfg.hash_kind = c.hash_kind;
+    cfg.distinct_order = c.order;
+    cfg.engine = c.engine;
+    cfg.seed = c.seed;
+    cfg.stream_id = c.stream;
+    return cfg;
+}
+
+static void run_ffm(const Case& c) {
+    FfmMirror s(config_of(c));
+    uint8_t key[8];
+    for (int64_t i = 0; i < c.n; ++i) {
+        const int64_t h = make_key(c, i, key);
+        s.sample(key, h);
+    }
+    int64_t n = 0;
+    std::vector<uint8_t> r = s.result(&n);
+    EXPECT(same(c, r, n), c.name.c_str());
+    if (!c.reusable) {
+        EXPECT(!s.open && s.handle == nullptr, c.name.c_str());  // isOpen == false, handle gone
+        bool ise = false;
+        try {
+            s.sample(key, 0);
+        } catch (const JvmException& e) {
+            ise = e.status == RSV_E_ILLEGAL_STATE;
+        }
+        EXPECT(ise, c.name.c_str());
+        ise = false;
+        try {
+            s.result(&n);
+        } catch (const JvmException& e) {
+            ise = e.status == RSV_E_ILLEGAL_STATE;
+        }
+        EXPECT(ise, c.name.c_str());
+    } else {  // MultiResult: still open, the next result equals the last, sampling continues
+        int64_t n2 = 0;
+        std::vector<uint8_t> r2 = s.result(&n2);
+        EXPECT(s.open && n2 == n && r2 == r, c.name.c_str());
+        s.sample(key, 0);
+        s.result(&n2);
+        EXPECT(s.open, c.name.c_str());
+    }
+}
+
+static void run_jni(const Case& c) {
+    rsv_jvm s;
+    const rsv_config cfg = config_of(c);
+    rsv_status st = rsv_jvm_create(&s, &cfg);
+    EXPECT(st == RSV_OK, c.name.c_str());
+    if (st != RSV_OK) return;
+    // sampleAll over JVM arrays of 65536 keys (JniSampler's buffer), the odd tail per element
+    const int64_t B = 65536;
+    std::vector<uint8_t> buf((size_t)B * c.kw);
+    std::vector<int64_t> hb((size_t)B);
+    int64_t i = 0;
+    for (; i + B <= c.n; i += B) {
+        for (int64_t t = 0; t < B; ++t) hb[(size_t)t] = make_key(c, i + t, buf.data() + t * c.kw);
+        st = rsv_jvm_sample_array(&s, buf.data(), s.precomputed ? hb.data() : nullptr, B);
+        EXPECT(st == RSV_OK, c.name.c_str());
+    }
+    uint8_t key[8];
+    for (; i < c.n; ++i) {
+        const int64_t h = make_key(c, i, key);
+        st = rsv_jvm_sample(&s, key, h);
+        EXPECT(st == RSV_OK, c.name.c_str());
+    }
+    std::vector<uint8_t> out((size_t)c.k * c.kw);
+    int64_t n = 0;
+    st = rsv_jvm_result(&s, out.data(), c.k, &n);
+    EXPECT(st == RSV_OK, c.name.c_str());
+    out.resize((size_t)n * c.kw);
+    EXPECT(same(c, out, n), c.name.c_str());
+    if (!c.reusable) {
+        EXPECT(rsv_jvm_is_open(&s) == 0 && s.h == nullptr, c.name.c_str());
+        st = rsv_jvm_sample(&s, key, 0);
+        EXPECT(st == RSV_E_ILLEGAL_STATE, c.name.c_str());
+        EXPECT(std::strstr(rsv_jvm_last_error(), "result()") != nullptr, c.name.c_str());
+        EXPECT(std::strcmp(rsv_jvm_exception_class(st), "java/lang/IllegalStateException") == 0, c.name.c_str());
+        st = rsv_jvm_result(&s, out.data(), c.k, &n);
+        EXPECT(st == RSV_E_ILLEGAL_STATE, c.name.c_str());
+        void* p = nullptr;
+        int64_t cap = 0;
+        EXPECT(rsv_jvm_stage_acquire(&s, &p, &cap) == RSV_E_ILLEGAL_STATE, c.name.c_str());
+    } else {
+        EXPECT(rsv_jvm_is_open(&s) == 1, c.name.c_str());
+        std::vector<uint8_t> out2((size_t)c.k * c.kw);
+        int64_t n2 = 0;
+        EXPECT(rsv_jvm_result(&s, out2.data(), c.k, &n2) == RSV_OK, c.name.c_str());
+        out2.resize((size_t)n2 * c.kw);
+        EXPECT(n2 == n && out2 == out, c.name.c_str());
+    }
+    rsv_jvm_destroy(&s);
+}
+
+static void run_abi(const Case& c) {  // per-element rsv_sample: the engine stages and flushes
+    const rsv_config cfg = config_of(c);
+    rsv_sampler* h = nullptr;
+    check(rsv_create(&cfg, &h));
+    uint8_t key[8];
+    for (int64_t i = 0; i < c.n; ++i) {
+        int64_t hv = make_key(c, i, key);
+        rsv_status st = rsv_sample(h, key, &hv);
+        if (st != RSV_OK) {
+            EXPECT(st == RSV_OK, c.name.c_str());
+            break;
+        }
+    }
+    std::vector<uint8_t> out((size_t)c.k * c.kw);
+    int64_t n = 0;
+    EXPECT(rsv_result(h, out.data(), c.k, &n) == RSV_OK, c.name.c_str());
+    out.resize((size_t)n * c.kw);
+    EXPECT(same(c, out, n), c.name.c_str());
+    EXPECT(rsv_is_open(h) == c.reusable, c.name.c_str());
+    rsv_destroy(h);
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: %s cases.txt\n", argv[0]);
+        return 2;
+    }
+    // the exception mapping of both bindings (Sampler.scala:80-81)
+    for (int bad : {0, -1, 2147483647}) {
+        rsv_config cfg;
+        rsv_config_init(&cfg);
+        cfg.max_sample_size = bad;
+        rsv_jvm s;
+        const rsv_status st = rsv_jvm_create(&s, &cfg);
+        EXPECT(st == RSV_E_ILLEGAL_ARGUMENT, "create with a bad maxSampleSize");
+        EXPECT(std::strcmp(rsv_jvm_exception_class(st), "java/lang/IllegalArgumentException") == 0, "IAE class");
+    }
+    std::ifstream f(argv[1]);
+    std::string line;
+    while (std::getline(f, line)) {
+        if (line.empty() || line[0] == '#') continue;
+        std::istringstream is(line);
+        Case c;
+        is >> c.name >> c.path >> c.kind >> c.k >> c.kw >> c.reusable >> c.hash_kind >> c.order >> c.engine >> c.seed >>
+            c.stream >> c.n >> c.base >> c.expected;
+        if (is >> c.keyfile) c.keys = read_file(c.keyfile);
+        const int before = failures;
+        try {
+            if (c.path == "ffm") run_ffm(c);
+            else if (c.path == "jni") run_jni(c);
+            else if (c.path == "abi") run_abi(c);
+            else throw std::runtime_error("unknown path " + c.path);
+        } catch (const std::exception& e) {
+            std::printf("FAIL %s: exception %s\n", c.name.c_str(), e.what());
+            ++failures;
+        }
+        if (failures == before) std::printf("PASS %s\n", c.name.c_str());
+        std::fflush(stdout);
+    }
+    return failures;
+}

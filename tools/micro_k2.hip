@@ -1,0 +1,83 @@
+// micro_k2.hip -- K2 (segmented, rsv_k2.h) variant timing at C3's shape: 2^20 streams x 4096 keys,
+// k = 64 (development tool, not product).  Variants: 0 = product kernel, 1 = no winner-key gather,
+// 2 = no level-1 Philox, 8 = candidates dropped after the FIFO append, 9 = 8 + 1, 16 = the
+// winner keys stored right after their gather (the product defers the store by one stream).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/micro_k2.hip -o tools/micro_k2
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../reservoir_amd/csrc/rsv_k2.h"
+
+using namespace rsv;
+
+#define CK(x)                                                                          \
+    do {                                                                               \
+        hipError_t e = (x);                                                            \
+        if (e != hipSuccess) {                                                         \
+            printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+            return 1;                                                                  \
+        }                                                                              \
+    } while (0)
+
+__global__ void fill(int64_t* keys, int64_t n, int64_t* offs, int64_t S, int64_t L) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t z = (uint64_t)i + 0x9E3779B97F4A7C15ULL;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        keys[i] = (int64_t)(z ^ (z >> 31));
+        if (i <= S && i * L <= n) offs[i] = i * L;
+    }
+}
+
+int main(int argc, char** argv) {
+    const int64_t S = 1 << 20, L = 4096, n = S * L;
+    const uint32_t k = 64;
+    int64_t *keys, *offs, *out, *cnt;
+    CK(hipMalloc(&keys, n * 8));
+    CK(hipMalloc(&offs, (S + 1) * 8));
+    CK(hipMalloc(&out, S * k * 8));
+    CK(hipMalloc(&cnt, S * 8));
+    hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, keys, n, offs, S, L);
+    CK(hipDeviceSynchronize());
+    const size_t lds = k2::lds_bytes(k);
+    const unsigned grid = (unsigned)std::min<int64_t>(S / k2::kWaves, 256 * 16);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<int64_t> ref(S * k), got(S * k);
+    auto run = [&](auto kern, const char* name, bool check) -> int {
+        std::vector<float> ts;
+        for (int rep = 0; rep < 7; ++rep) {
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * k2::kWaves), lds, 0, (const int64_t*)keys,
+                               (const int64_t*)offs, S, k, 1u, 0u, 0ull, out, cnt);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (rep) ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        printf("{\"variant\": \"%s\", \"median_ms\": %.4f, \"min_ms\": %.4f}\n", name, ts[ts.size() / 2], ts[0]);
+        if (check) {
+            CK(hipMemcpy(got.data(), out, S * k * 8, hipMemcpyDeviceToHost));
+            printf("  identical to variant 0: %s\n", got == ref ? "yes" : "NO");
+        }
+        return 0;
+    };
+    if (run(k2::k2_segmented<int64_t, 0>, "0 product", false)) return 1;
+    CK(hipMemcpy(ref.data(), out, S * k * 8, hipMemcpyDeviceToHost));
+    if (argc > 1 && argv[1][0] == 'p') return 0;  // one variant only (rocprofv3 --pmc passes)
+    if (run(k2::k2_segmented<int64_t, 1>, "1 no gather", false)) return 1;
+    if (run(k2::k2_segmented<int64_t, 2>, "2 no level-1 philox", false)) return 1;
+    if (run(k2::k2_segmented<int64_t, 16>, "16 gather stored at once (no deferral)", true)) return 1;
+    if (run(k2::k2_segmented<int64_t, 8>, "8 candidates dropped", false)) return 1;
+    if (run(k2::k2_segmented<int64_t, 9>, "9 dropped + no gather", false)) return 1;
+    if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+    return 0;
+}
