@@ -1,0 +1,59 @@
+package lgbt.princess.reservoir.gpu
+
+import java.security.SecureRandom
+
+import scala.reflect.ClassTag
+
+import lgbt.princess.reservoir.Sampler
+
+/** Backend selection behind the unchanged factories `Sampler.apply` / `Sampler.distinct`
+  * (Sampler.scala:128-136, :171-180; SURVEY.md section 5 "Config / flags"): no signature changes.
+  *
+  *   -Dreservoir.backend=gpu        use the MI355X engine for B = Long or Int (else the JVM classes)
+  *   -Dreservoir.binding=ffm|jni    default: FFM on JDK 22+, JNI below
+  *   -Dreservoir.engine=java_l      the reference's Algorithm L over java.util.Random, bit-identical
+  *                                  to the JVM sampler for the same seed (default philox_r: Algorithm R)
+  *
+  * The akka operators need nothing: they take the sampler by name (Sample.scala:23-24,
+  * SampleImpl.scala:10), so `Sample(k)(map)` picks the backend through `Sampler.apply`. */
+private[reservoir] object Backend {
+  private[this] val enabled = System.getProperty("reservoir.backend", "cpu") == "gpu"
+  private[this] val ffm = System.getProperty("reservoir.binding") match {
+    case "ffm" => true
+    case "jni" => false
+    case _ =>
+      val v = System.getProperty("java.specification.version", "1.8")
+      !v.startsWith("1.") && v.toInt >= 22
+  }
+  private[this] val engine = if (System.getProperty("reservoir.engine", "") == "java_l") Abi.EngineJavaL else Abi.EnginePhiloxR
+  private[this] val seeds  = new SecureRandom() // a fresh seed per sampler, like `new Random()` (Sampler.scala:199)
+
+  private[this] def make[A, B](kind: Int, k: Int, reusable: Boolean, keys: KeyKind[B], hashKind: Int)(
+      map: A => B,
+      hash: B => Long,
+  ): Sampler[A, B] = {
+    val seed = seeds.nextLong()
+    if (ffm) FfmFactory.make[A, B](kind, k, reusable, keys, hashKind, engine, seed)(map, hash)
+    else new JniSampler[A, B](kind, k, reusable, keys, hashKind, engine, seed)(map, hash)
+  }
+
+  /** Sampler.apply (validation already done by validateNonDistinctParams). */
+  def elements[A, B: ClassTag](maxSampleSize: Int, reusable: Boolean)(map: A => B): Option[Sampler[A, B]] =
+    if (!enabled) None
+    else KeyKind.of[B].map(kk => make[A, B](Abi.KindElements, maxSampleSize, reusable, kk, Abi.HashDefault)(map, null))
+
+  /** Sampler.distinct: the default `hashCode` and the identity hash run on the GPU; any other `hash`
+    * is evaluated here per element and shipped beside the key (RSV_HASH_PRECOMPUTED). */
+  def distinct[A, B: ClassTag](maxSampleSize: Int, reusable: Boolean)(map: A => B, hash: B => Long)(
+      defaultHash: Any => Long
+  ): Option[Sampler[A, B]] =
+    if (!enabled) None
+    else
+      KeyKind.of[B].map { kk =>
+        val hashKind =
+          if (hash eq defaultHash) Abi.HashDefault
+          else if (kk == KeyKind.LongKey && (hash eq Hashes.identity)) Abi.HashIdentity
+          else Abi.HashPrecomputed
+        make[A, B](Abi.KindDistinct, maxSampleSize, reusable, kk, hashKind)(map, hash)
+      }
+}

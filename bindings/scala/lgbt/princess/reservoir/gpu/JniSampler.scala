@@ -1,0 +1,107 @@
+package lgbt.princess.reservoir.gpu
+
+import java.util.Arrays
+
+import scala.collection.immutable.ArraySeq
+
+import lgbt.princess.reservoir.Sampler
+
+/** JNI natives of bindings/jni/reservoir_jni.c, for the reference's CI JDKs 8/11/15 (build.sbt:37-42).
+  * A session is a native rsv_jvm (bindings/jvm/rsv_jvm.h) held as a Long. */
+private[reservoir] object Jni {
+  System.loadLibrary("reservoir_jni")
+
+  @native def create(
+      kind: Int,
+      k: Int,
+      keyWidth: Int,
+      reusable: Boolean,
+      engine: Int,
+      hashKind: Int,
+      order: Int,
+      seed: Long,
+      streamId: Long,
+      device: Int,
+  ): Long
+  @native def sampleLong(session: Long, key: Long, hash: Long): Unit
+  @native def sampleInt(session: Long, key: Int, hash: Long): Unit
+  @native def sampleLongs(session: Long, keys: Array[Long], hashes: Array[Long], n: Int): Unit
+  @native def sampleInts(session: Long, keys: Array[Int], hashes: Array[Long], n: Int): Unit
+  @native def resultLongs(session: Long, out: Array[Long]): Int
+  @native def resultInts(session: Long, out: Array[Int]): Int
+  @native def isOpen(session: Long): Boolean
+  @native def destroy(session: Long): Unit
+  @native def stageAcquire(session: Long): java.nio.ByteBuffer
+  @native def stageCommit(session: Long, n: Long): Unit
+}
+
+/** A GPU-backed `Sampler[A, B]` over JNI, B = Long or Int: keys are buffered in a JVM array and handed
+  * over 65536 at a time (one JNI call per batch, none per element); the native session copies them
+  * into the engine's pinned staging buffer.  Lifecycle as FfmSampler: `isOpen` tracked here, the
+  * single-use `result()` destroys the session at once. */
+private[reservoir] final class JniSampler[A, B](
+    kind: Int,
+    maxSampleSize: Int,
+    reusable: Boolean,
+    keys: KeyKind[B],
+    hashKind: Int,
+    engine: Int,
+    seed: Long,
+)(map: A => B, hash: B => Long)
+    extends Sampler[A, B] {
+  private[this] final val Batch = 65536
+  private[this] val isLong      = keys.width == 8
+  private[this] val precomputed = kind == Abi.KindDistinct && hashKind == Abi.HashPrecomputed
+  private[this] var session =
+    Jni.create(kind, maxSampleSize, keys.width, reusable, engine, hashKind, Abi.OrderAuto, seed, 0L, -1)
+  private[this] val longs  = if (isLong) new Array[Long](Batch) else null
+  private[this] val ints   = if (isLong) null else new Array[Int](Batch)
+  private[this] val hashes = if (precomputed) new Array[Long](Batch) else null
+  private[this] var n      = 0
+  private[this] var open   = true
+
+  private[this] def flush(): Unit =
+    if (n > 0) {
+      if (isLong) Jni.sampleLongs(session, longs, hashes, n) else Jni.sampleInts(session, ints, hashes, n)
+      n = 0
+    }
+
+  def sample(element: A): Unit = {
+    if (!open) throw new IllegalStateException(Abi.ClosedMessage)
+    val b = map(element)
+    if (isLong) longs(n) = b.asInstanceOf[Long] else ints(n) = b.asInstanceOf[Int]
+    if (precomputed) hashes(n) = hash(b)
+    n += 1
+    if (n == Batch) flush()
+  }
+
+  def result(): IndexedSeq[B] = {
+    if (!open) throw new IllegalStateException(Abi.ClosedMessage)
+    flush()
+    val res =
+      if (isLong) {
+        val out = new Array[Long](maxSampleSize)
+        val m   = Jni.resultLongs(session, out)
+        ArraySeq.unsafeWrapArray(if (m == out.length) out else Arrays.copyOf(out, m))
+      } else {
+        val out = new Array[Int](maxSampleSize)
+        val m   = Jni.resultInts(session, out)
+        ArraySeq.unsafeWrapArray(if (m == out.length) out else Arrays.copyOf(out, m))
+      }
+    if (!reusable) { // the native side destroyed the handle inside result(); free the session now
+      open = false
+      Jni.destroy(session)
+      session = 0L
+    }
+    res.asInstanceOf[IndexedSeq[B]]
+  }
+
+  def isOpen: Boolean = open
+
+  // JDK 8 has no java.lang.ref.Cleaner: a reusable sampler's session goes with the object
+  override protected def finalize(): Unit =
+    if (session != 0L) {
+      Jni.destroy(session)
+      session = 0L
+    }
+}
