@@ -10,8 +10,10 @@ winning keys are read -- which makes them integer-VALU bound, not HBM bound.  Th
                      straddles an integer -- otherwise j_i = floor(b_i (i+1) / 256) needs no level 1).
                      Work the kernels do beyond this (recomputes, queue traffic, masks) is overhead
                      and is NOT credited.
-  issue cost         cycles per wave-instruction on one SIMD, measured by tools/micro_valu.hip
-                     (8 waves per SIMD, s_memtime; profiles/r02/valu_costs.json):
+  issue cost         cycles per wave-instruction on one SIMD, measured with tools/micro_valu.hip under
+                     rocprofv3 --pmc (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs / SQ_INSTS_VALU; 8 waves per
+                     SIMD; profiles/r02/valu_costs.json): 4 cycles for every integer op used, the
+                     64-bit v_mad_u64_u32 included (4.02-4.09 sustained in Philox-only loops):
                        level-0 call (counter words 1..3 wave-uniform): 18 v_mad_u64_u32 + 17 v_bitop3
                                                                        + 2 v_xor   (ISA of K1's loop)
                        level-1 call (full Philox4x32-10):             20 v_mad_u64_u32 + 20 v_bitop3
@@ -31,23 +33,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 COSTS_PATH = os.path.join(ROOT, "profiles", "r02", "valu_costs.json")
 SIMDS = 256 * 4
 CLOCK_HZ = 2.4e9
-# fallbacks if the measured file is absent: full rate = 2 cycles per wave64 VALU instruction
-_DEFAULT = {"v_mad_u64_u32": 6.4, "v_bitop3_b32": 2.0, "v_xor_b32": 2.0}
+# measured on MI355X (profiles/r02/valu_costs.json "model"): one wave64 integer VALU instruction per
+# 4 cycles per SIMD, whatever the op
+_CYCLES = 4.0
 
 
 def costs() -> dict:
-    c = dict(_DEFAULT)
-    src = "default (2 cycles full rate; v_mad_u64_u32 3.2 slots, round-1 measurement)"
+    cyc, src = _CYCLES, "profiles/r02/valu_costs.json (model: 4 cycles per wave64 VALU instruction)"
     try:
         with open(COSTS_PATH) as f:
-            for line in f:
-                line = line.strip()
-                if line.startswith("{"):
-                    d = json.loads(line)
-                    c[d["op"]] = float(d["cycles_per_wave_instr_per_simd"])
-        src = os.path.relpath(COSTS_PATH, ROOT)
-    except OSError:
-        pass
+            cyc = float(json.load(f)["model"]["cycles_per_wave_instr"])
+    except (OSError, KeyError, ValueError):
+        src = "built-in 4 cycles per wave64 VALU instruction (profiles/r02/valu_costs.json absent)"
+    c = {op: cyc for op in ("v_mad_u64_u32", "v_bitop3_b32", "v_xor_b32")}
     c["_source"] = src
     return c
 
