@@ -13,6 +13,7 @@
 // a strided sample of the batch; a threshold that proves too tight (fewer than k distinct
 // candidates) or too loose (candidate buffer overflow) is corrected and the pass re-run, so the
 // result is exact regardless of the estimate.
+#include <cstdio>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -22,6 +23,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <limits>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/reservoir_hip.h"
@@ -46,7 +48,9 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
 // one atomic per candidate cost 1.5 ms at 132k candidates).  IDX: each candidate also carries its
 // pass-relative index (the ordered mode's arrival order); its chunks run at ~3k candidates per
 // pass, so it stages B = 256 (64: ~35 us of atomics per short chunk).
-template <typename KeyT, bool IDX = false>
+// Sink (the scheduled pass): also files each written candidate into its merge bucket, so the
+// bucket atomics ride under the HBM-bound stream instead of a scatter kernel after it
+template <typename KeyT, bool IDX = false, typename Sink = void>
 struct CandOut {
     static constexpr uint32_t B = IDX ? 256 : 64;  // batch; the LDS queue holds B + 64
     int64_t* qh;  // LDS: B + 64 hashes of this wave
@@ -58,6 +62,7 @@ struct CandOut {
     int64_t cap;
     uint32_t* qi = nullptr;      // LDS: B + 64 indices (IDX)
     uint32_t* cand_i = nullptr;  // (IDX)
+    Sink* sink = nullptr;
 
     __device__ __forceinline__ void write64(uint32_t from, uint32_t cnt) {
         const uint32_t lane = threadIdx.x & 63;
@@ -77,6 +82,7 @@ struct CandOut {
                     cand_h[pos] = qh[from + j];
                     cand_k[pos] = qk[from + j];
                     if constexpr (IDX) cand_i[pos] = qi[from + j];
+                    if constexpr (!std::is_void<Sink>::value) sink->put(qh[from + j], qk[from + j], qi[from + j] + 1u);
                 }
             }
         }
@@ -152,10 +158,38 @@ struct Vec<int32_t> {
 // K3 filter: streaming pass.  The main loop covers whole grid tiles with unguarded loads (U x 16 B
 // per lane issued back to back, so each wave keeps U loads in flight); per-element work is the
 // scrambled hash and one compare, and the rare candidates take one wave-uniform slow path.
-template <typename KeyT, int HASH, int U, bool GUARD, typename Out>
+// filter bounds: one inclusive bound for the pass, or (the ordered mode's scheduled pass) a bound
+// per index range, looked up with a cursor -- a thread's indices only increase between resets
+struct ConstBound {
+    int64_t t;
+    __device__ __forceinline__ int64_t operator()(int64_t) { return t; }
+    __device__ __forceinline__ void reset() {}
+};
+
+struct RangeBound {
+    const int64_t* b;  // LDS: range starts, b[nr] = n
+    const int64_t* t;  // LDS: bound of range r
+    int r;
+    int64_t next, cur;
+    __device__ __forceinline__ void reset() {
+        r = 0;
+        next = b[1];
+        cur = t[0];
+    }
+    __device__ __forceinline__ int64_t operator()(int64_t idx) {
+        while (idx >= next) {
+            ++r;
+            next = b[r + 1];
+            cur = t[r];
+        }
+        return cur;
+    }
+};
+
+template <typename KeyT, int HASH, int U, bool GUARD, typename Out, typename Bound>
 __device__ __forceinline__ void k3_tile(const typename Vec<KeyT>::T* x, int64_t v0, int64_t T, int64_t n_vec,
                                         const KeyT* keys, const int64_t* hashes, int64_t r0, int64_t r1,
-                                        int64_t tinc, Out& out, uint32_t ioff) {
+                                        Bound& bound, Out& out, uint32_t ioff) {
     using V = Vec<KeyT>;
     int64_t h[U][V::N];
     bool c[U][V::N];
@@ -168,7 +202,7 @@ __device__ __forceinline__ void k3_tile(const typename Vec<KeyT>::T* x, int64_t 
 #pragma unroll
         for (int e = 0; e < V::N; ++e) {
             h[u][e] = elem_hash<KeyT, HASH>(keys, hashes, vi * V::N + e, V::get(x[u], e), r0, r1);
-            c[u][e] = ok & (h[u][e] <= tinc);
+            c[u][e] = ok & (h[u][e] <= bound((int64_t)ioff + vi * V::N + e));
             any |= c[u][e];
         }
     }
@@ -182,25 +216,24 @@ __device__ __forceinline__ void k3_tile(const typename Vec<KeyT>::T* x, int64_t 
 }
 
 // IDX (the ordered mode's chunk pass): candidates also carry their index in [0, n < 2^32).
-template <typename KeyT, int HASH, bool IDX = false>
-__global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ keys,
-                                                    const int64_t* __restrict__ hashes, int64_t n,
-                                                    int64_t r0, int64_t r1, int64_t tinc,
-                                                    int64_t* __restrict__ cand_h,
-                                                    KeyT* __restrict__ cand_k,
-                                                    unsigned long long* __restrict__ counter,
-                                                    int64_t cap, uint32_t* __restrict__ cand_i = nullptr) {
+template <typename KeyT, int HASH, bool IDX, typename Bound, typename Sink = void>
+__device__ __forceinline__ void k3_filter_body(const KeyT* __restrict__ keys, const int64_t* __restrict__ hashes,
+                                               int64_t n, int64_t r0, int64_t r1, Bound bound,
+                                               int64_t* __restrict__ cand_h, KeyT* __restrict__ cand_k,
+                                               unsigned long long* __restrict__ counter, int64_t cap,
+                                               uint32_t* __restrict__ cand_i, Sink* sink = nullptr) {
     using V = Vec<KeyT>;
     constexpr int U = 8;  // 8 x 16-B loads in flight per lane (tools/micro_k3: 6.0 -> 6.4 TB/s vs 4)
     constexpr uint32_t Q = CandOut<KeyT, IDX>::B + 64;
     __shared__ int64_t sh_h[kBlock / 64][Q];
     __shared__ KeyT sh_k[kBlock / 64][Q];
     __shared__ uint32_t sh_i[IDX ? kBlock / 64 : 1][IDX ? Q : 1];
-    CandOut<KeyT, IDX> out{sh_h[threadIdx.x >> 6], sh_k[threadIdx.x >> 6], 0u, cand_h, cand_k, counter, cap};
+    CandOut<KeyT, IDX, Sink> out{sh_h[threadIdx.x >> 6], sh_k[threadIdx.x >> 6], 0u, cand_h, cand_k, counter, cap};
     if constexpr (IDX) {
         out.qi = sh_i[threadIdx.x >> 6];
         out.cand_i = cand_i;
     }
+    out.sink = sink;
     const int64_t T = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     // the vector loads start at the first 16-B boundary (a batch may begin anywhere in a tensor);
@@ -212,12 +245,13 @@ __global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ key
     const int64_t n_vec = nb / V::N;
     const typename V::T* kv = reinterpret_cast<const typename V::T*>(kb);
     const int64_t full = n_vec / (T * U);  // whole tiles: every lane has U vectors
+    bound.reset();
     for (int64_t it = 0; it < full; ++it) {
         const int64_t v0 = it * T * U + tid;
         typename V::T x[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(kv + v0 + u * T);
-        k3_tile<KeyT, HASH, U, false>(x, v0, T, n_vec, kb, hb, r0, r1, tinc, out, (uint32_t)head);
+        k3_tile<KeyT, HASH, U, false>(x, v0, T, n_vec, kb, hb, r0, r1, bound, out, (uint32_t)head);
     }
     if (full * T * U < n_vec) {  // the partial last tile, same shape: out-of-range lanes re-load the
         const int64_t v0 = full * T * U + tid;  // last vector (no guarded loads) and are masked out
@@ -227,25 +261,38 @@ __global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ key
             const int64_t v = v0 + u * T;
             x[u] = __builtin_nontemporal_load(kv + (v < n_vec ? v : n_vec - 1));
         }
-        k3_tile<KeyT, HASH, U, true>(x, v0, T, n_vec, kb, hb, r0, r1, tinc, out, (uint32_t)head);
+        k3_tile<KeyT, HASH, U, true>(x, v0, T, n_vec, kb, hb, r0, r1, bound, out, (uint32_t)head);
     }
     // then the head and the nb % V::N tail elements
+    bound.reset();
     for (int64_t idx = tid; idx - tid < head; idx += T) {
         const bool ok = idx < head;
         const KeyT key = ok ? keys[idx] : (KeyT)0;
         const int64_t h = ok ? elem_hash<KeyT, HASH>(keys, hashes, idx, key, r0, r1) : 0;
-        out.push(ok && h <= tinc, h, key, (uint32_t)idx);
+        out.push(ok && h <= bound(ok ? idx : 0), h, key, (uint32_t)idx);
     }
+    bound.reset();
     for (int64_t idx = head + n_vec * V::N + tid; idx - tid < n; idx += T) {
         const bool ok = idx < n;
         const KeyT key = ok ? keys[idx] : (KeyT)0;
         const int64_t h = ok ? elem_hash<KeyT, HASH>(keys, hashes, idx, key, r0, r1) : 0;
-        out.push(ok && h <= tinc, h, key, (uint32_t)idx);
+        out.push(ok && h <= bound(ok ? idx : n - 1), h, key, (uint32_t)idx);
     }
     __shared__ uint32_t s_q[kBlock / 64];
     __shared__ unsigned long long s_base;
     __builtin_amdgcn_wave_barrier();
     out.template flush_block<kBlock / 64>(s_q, &s_base);
+}
+
+template <typename KeyT, int HASH, bool IDX = false>
+__global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ keys,
+                                                    const int64_t* __restrict__ hashes, int64_t n,
+                                                    int64_t r0, int64_t r1, int64_t tinc,
+                                                    int64_t* __restrict__ cand_h,
+                                                    KeyT* __restrict__ cand_k,
+                                                    unsigned long long* __restrict__ counter,
+                                                    int64_t cap, uint32_t* __restrict__ cand_i = nullptr) {
+    k3_filter_body<KeyT, HASH, IDX>(keys, hashes, n, r0, r1, ConstBound{tinc}, cand_h, cand_k, counter, cap, cand_i);
 }
 
 template <typename KeyT, int HASH>
@@ -319,6 +366,17 @@ __device__ __forceinline__ uint32_t* bucket_distinct(int64_t* ctl, int32_t log_b
     return (uint32_t*)(ctl + kCtlWords) + ((size_t)kCountStride << log_bmax);
 }
 
+// per-16-bucket sums of the distinct counts (bucket_sort adds, bucket_emit reads): an emit
+// workgroup's rank base is then B / 16 group sums + <= 15 bucket counts instead of every bucket
+// (groups of 256 put 256 same-address atomics in line: bucket_sort 9 -> 28 us at 4096 buckets)
+__device__ __forceinline__ uint32_t* bucket_group(int64_t* ctl, int32_t log_bmax) {
+    return (uint32_t*)(ctl + kCtlWords) + ((size_t)(kCountStride + 1) << log_bmax);
+}
+__device__ __forceinline__ void zero_bucket_groups(int64_t* ctl, int32_t log_bmax) {
+    uint32_t* gs = bucket_group(ctl, log_bmax);
+    for (uint32_t i = threadIdx.x; i <= ((1u << log_bmax) >> 4); i += blockDim.x) gs[i] = 0;
+}
+
 __device__ __forceinline__ uint32_t bucket_log(int64_t total, int32_t log_bmax) {
     uint32_t lb = 0;
     while ((int32_t)lb < log_bmax && ((int64_t)1 << (lb + kBucketAvgLog)) < total) ++lb;
@@ -355,7 +413,10 @@ __global__ __launch_bounds__(kBlock) void bucket_scatter(const int64_t* __restri
                                                          int64_t* __restrict__ ctl, uint64_t q,
                                                          int32_t log_bmax, int64_t* __restrict__ bh,
                                                          KeyT* __restrict__ bk) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctl[5] = 0;  // bucket_emit sets it
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) ctl[5] = 0;  // bucket_emit sets it
+        zero_bucket_groups(ctl, log_bmax);
+    }
     const int64_t c = ctl[0];
     if (c > cand_cap) return;  // the filter overflowed its buffer: the host tightens and reruns
     const int64_t total = m + c;
@@ -412,7 +473,7 @@ __device__ __forceinline__ T shfl_any(T v, int src) {
 // ^ stride; then the first of each run of equal entries is kept and written back compacted;
 // bucket_distinct[b] = their number.
 template <typename KeyT, int R>
-__device__ __forceinline__ void wave_sort_bucket(int64_t* gh, KeyT* gk, uint32_t n, uint32_t* out_cnt) {
+__device__ __forceinline__ uint32_t wave_sort_bucket(int64_t* gh, KeyT* gk, uint32_t n, uint32_t* out_cnt) {
     const uint32_t lane = threadIdx.x & 63;
     constexpr uint32_t N = 64u * R;
     int64_t h[R];
@@ -495,6 +556,7 @@ __device__ __forceinline__ void wave_sort_bucket(int64_t* gh, KeyT* gk, uint32_t
         prev_k_last = shfl_any(k[r], 63);
     }
     if (lane == 0) *out_cnt = base;
+    return base;
 }
 
 template <typename KeyT>
@@ -515,12 +577,10 @@ __global__ __launch_bounds__(kBlock) void bucket_sort(int64_t m, int64_t cand_ca
         if ((threadIdx.x & 63) == 0) *bdist = 0;
         return;
     }
-    if (n <= 64)
-        wave_sort_bucket<KeyT, 1>(gh, gk, n, bdist);
-    else if (n <= 128)
-        wave_sort_bucket<KeyT, 2>(gh, gk, n, bdist);
-    else
-        wave_sort_bucket<KeyT, 4>(gh, gk, n, bdist);
+    const uint32_t nd = n <= 64    ? wave_sort_bucket<KeyT, 1>(gh, gk, n, bdist)
+                        : n <= 128 ? wave_sort_bucket<KeyT, 2>(gh, gk, n, bdist)
+                                   : wave_sort_bucket<KeyT, 4>(gh, gk, n, bdist);
+    if ((threadIdx.x & 63) == 0) atomicAdd(bucket_group(ctl, log_bmax) + (b >> 4), nd);
     if ((threadIdx.x & 63) == 0) *bcnt = 0;  // consumed (n was read before the sort's loads); re-armed
 }
 
@@ -533,23 +593,27 @@ template <typename KeyT>
 __global__ __launch_bounds__(kBlock) void bucket_emit(int64_t m, int64_t cand_cap, int64_t* __restrict__ ctl,
                                                       int32_t log_bmax, const int64_t* __restrict__ bh,
                                                       const KeyT* __restrict__ bk, int64_t k,
-                                                      int64_t* __restrict__ set_h, KeyT* __restrict__ set_k) {
+                                                      int64_t* __restrict__ set_h, KeyT* __restrict__ set_k,
+                                                      int32_t lb_fixed = -1) {
     __shared__ uint64_t s_pre[kBlock / 64], s_tot[kBlock / 64];
     __shared__ uint64_t s_base[kEmitBuckets + 1];
     const int64_t c = ctl[0];
     if (c > cand_cap || ctl[1]) return;
-    const uint32_t lb = bucket_log(m + c, log_bmax);
+    const uint32_t lb = lb_fixed >= 0 ? (uint32_t)lb_fixed : bucket_log(m + c, log_bmax);
     const uint32_t B = 1u << lb;
     const uint32_t b0 = blockIdx.x * kEmitBuckets;
     if (b0 >= B) return;
     const uint32_t* bdist = bucket_distinct(ctl, log_bmax);
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t* gsum = bucket_group(ctl, log_bmax);
+    const uint32_t G = (B + 15) >> 4, g0 = b0 >> 4;
     uint64_t pre = 0, tot = 0;
-    for (uint32_t i = t; i < B; i += kBlock) {
-        const uint64_t v = bdist[i];
+    for (uint32_t i = t; i < G; i += kBlock) {
+        const uint64_t v = gsum[i];
         tot += v;
-        if (i < b0) pre += v;
+        if (i < g0) pre += v;
     }
+    for (uint32_t i = (g0 << 4) + t; i < b0; i += kBlock) pre += bdist[i];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         pre += shfl_xor_any(pre, off);
@@ -597,6 +661,316 @@ __global__ __launch_bounds__(kBlock) void bucket_emit(int64_t m, int64_t cand_ca
             }
         }
     }
+}
+
+// ---- ordered mode: the scheduled pass ---------------------------------------------------------
+// Once the heap is full, the rest of a long batch is filtered in ONE pass whose bound is fixed ahead
+// per index range: range r = [b[r], b[r+1]) keeps h <= t[r], t[0] = the current bound (exact) and
+// t[r] for r >= 1 predicted from the hash's uniformity (SchedPlan, host).  The pass keeps a
+// superset of what the reference admits iff every predicted bound is at least the true one at its
+// range's start, i.e. iff at least k distinct elements that arrived before b[r] have h <= t[r].
+// The merge verifies exactly that: it dedups the candidates by (h, key), keeps each element's
+// first arrival, and counts, per range, the distinct elements that arrived before it with h under
+// its bound (an element counts for the ranges r_a(arrival) .. r_h(h): a difference array).  A
+// failed range (or a full buffer) leaves the batch to the chunk loop with the set restored.
+constexpr int kMaxRanges = 64;
+constexpr int kVerifyCopies = 64;  // verification accumulators (spread the sort kernel's atomics)
+
+struct SchedDev {
+    int64_t b[kMaxRanges + 1];  // range starts (batch-relative), b[nr] = n
+    int64_t t[kMaxRanges];      // inclusive bound per range, non-increasing
+    int32_t nr;                 // ranges
+    uint32_t B, B_lo;           // merge buckets; the first B_lo map h <= t[nr - 1] linearly
+    uint32_t lb;                // log2 B
+    uint64_t lo_mult;           // low region: bucket = umulhi(h - MIN, lo_mult * B_lo)
+    float hi_a[kMaxRanges];     // high region, piece p (t[p + 1] < h <= t[p]): pos = a u + c, u = (h - MIN) / 2^64
+    float hi_c[kMaxRanges];
+};
+
+// bucket of h for the scheduled merge: B_lo buckets map [MIN, t_lo] linearly (monotone: the
+// final set and its tie lie there), the rest map (t_lo, t[0]] by the entries' expected cumulative
+// count (piecewise linear in h; only balance matters there)
+struct SchedMap {
+    const SchedDev* sd;
+    const int64_t* st;  // LDS copy of sd->t
+    uint32_t B, B_lo, nr;
+    int64_t t_lo;
+    uint64_t lo_mult;
+    __device__ __forceinline__ uint32_t operator()(int64_t h) const {
+        const uint64_t u = (uint64_t)h ^ 0x8000000000000000ull;
+        if (h <= t_lo) return std::min<uint32_t>(B_lo - 1, (uint32_t)__umul64hi(u, lo_mult));
+        // piece p = the last range with t[p] >= h (t non-increasing; the set's top sits at t[0] + 1)
+        int lo = 0, hi = (int)nr - 1;  // t[lo] >= h > t[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (st[mid] >= h) lo = mid;
+            else hi = mid;
+        }
+        const float pos = sd->hi_a[lo] * (float)((double)u * 5.421010862427522e-20) + sd->hi_c[lo];
+        const uint32_t bh = (uint32_t)std::max(0.0f, pos * (float)(B - B_lo));
+        return B_lo + std::min(B - B_lo - 1, bh);
+    }
+};
+
+template <typename KeyT>
+struct SchedSink {
+    SchedMap map;
+    uint32_t* bcnt;
+    int64_t* bh;
+    KeyT* bk;
+    uint32_t* bi;
+    int64_t* ovf;
+    __device__ __forceinline__ void put(int64_t h, KeyT key, uint32_t tag) {
+        const uint32_t b = map(h);
+        const uint32_t at = atomicAdd(&bcnt[(size_t)b * kCountStride], 1u);
+        if (at < kBucketCap) {
+            bh[(size_t)b * kBucketCap + at] = h;
+            bk[(size_t)b * kBucketCap + at] = key;
+            bi[(size_t)b * kBucketCap + at] = tag;
+        } else {
+            *ovf = 1;
+        }
+    }
+};
+
+// the scheduled pass: files the set's members (tag 0) and every candidate (tag 1 + batch index)
+// into the merge buckets as it goes, and logs the candidates in arrival order for the replica
+template <typename KeyT, int HASH>
+__global__ __launch_bounds__(kBlock) void sched_filter(const KeyT* __restrict__ keys, const int64_t* __restrict__ hashes,
+                                                       int64_t n, int64_t r0, int64_t r1, const SchedDev* __restrict__ sd,
+                                                       int64_t* __restrict__ cand_h, KeyT* __restrict__ cand_k,
+                                                       uint32_t* __restrict__ cand_i, int64_t* __restrict__ ctl,
+                                                       int64_t cap, const int64_t* __restrict__ set_h,
+                                                       const KeyT* __restrict__ set_k, int64_t m, int64_t* __restrict__ bh,
+                                                       KeyT* __restrict__ bk, uint32_t* __restrict__ bi,
+                                                       int32_t log_bmax, int64_t* __restrict__ bak_h,
+                                                       KeyT* __restrict__ bak_k) {
+    __shared__ int64_t sb[kMaxRanges + 1], stt[kMaxRanges];
+    if (blockIdx.x == 0) {  // the merge's tie word and group sums (bucket_sort adds, bucket_emit sets)
+        if (threadIdx.x == 0) ctl[5] = 0;
+        zero_bucket_groups(ctl, log_bmax);
+    }
+    const int nr = sd->nr;
+    for (int i = threadIdx.x; i <= nr; i += blockDim.x) {
+        sb[i] = sd->b[i];
+        if (i < nr) stt[i] = sd->t[i];
+    }
+    __syncthreads();
+    const uint32_t B_lo = sd->B_lo;
+    const uint64_t q = sd->lo_mult;
+    SchedSink<KeyT> sink{SchedMap{sd, stt, sd->B, B_lo, (uint32_t)nr, stt[nr - 1], q > UINT64_MAX / B_lo ? UINT64_MAX : q * B_lo},
+                         bucket_count(ctl), bh, bk, bi, ctl + 1};
+    const int64_t per = (m + gridDim.x - 1) / gridDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * per + threadIdx.x; i < std::min<int64_t>(m, (int64_t)(blockIdx.x + 1) * per);
+         i += blockDim.x) {
+        const int64_t h = set_h[i];
+        const KeyT key = set_k[i];
+        bak_h[i] = h;  // the set before the pass (restored if a bound fails verification)
+        bak_k[i] = key;
+        sink.put(h, key, 0u);
+    }
+    RangeBound rb{sb, stt, 0, 0, 0};
+    k3_filter_body<KeyT, HASH, true>(keys, hashes, n, r0, r1, rb, cand_h, cand_k, (unsigned long long*)ctl, cap, cand_i,
+                                     &sink);
+}
+
+template <typename KeyT>
+__device__ __forceinline__ bool ent_less3(int64_t ha, KeyT ka, uint32_t ia, int64_t hb, KeyT kb, uint32_t ib) {
+    return ha < hb || (ha == hb && (ka < kb || (ka == kb && ia < ib)));
+}
+
+// one wave per bucket: sort by (h, key, tag), keep the first of each (h, key) run (its earliest
+// arrival), write them back compacted; each kept element adds +1 / -1 at ranges r_a / r_h + 1 of
+// the block's difference array (sdiff, LDS)
+template <typename KeyT, int R>
+__device__ __forceinline__ uint32_t wave_sort_bucket_tagged(int64_t* gh, KeyT* gk, uint32_t* gi, uint32_t n,
+                                                            const int64_t* sb, const int64_t* stt, int nr,
+                                                            int* sdiff) {
+    const uint32_t lane = threadIdx.x & 63;
+    constexpr uint32_t N = 64u * R;
+    int64_t h[R];
+    KeyT k[R];
+    uint32_t g[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = r * 64u + lane;
+        if (i < n) {
+            h[r] = gh[i];
+            k[r] = gk[i];
+            g[r] = gi[i];
+        } else {
+            h[r] = INT64_MAX;
+            k[r] = std::numeric_limits<KeyT>::max();
+            g[r] = 0xFFFFFFFFu;
+        }
+    }
+#pragma unroll
+    for (uint32_t size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 64) {
+                const uint32_t rs = stride / 64;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if ((r & rs) == 0) {
+                        const uint32_t i = r * 64u + lane;
+                        const bool up = (i & size) == 0;
+                        const int r2 = r + rs;
+                        if (ent_less3<KeyT>(h[r2], k[r2], g[r2], h[r], k[r], g[r]) == up) {
+                            const int64_t th = h[r];
+                            const KeyT tk = k[r];
+                            const uint32_t tg = g[r];
+                            h[r] = h[r2];
+                            k[r] = k[r2];
+                            g[r] = g[r2];
+                            h[r2] = th;
+                            k[r2] = tk;
+                            g[r2] = tg;
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t i = r * 64u + lane;
+                    const int64_t oh = shfl_xor_any(h[r], (int)stride);
+                    const KeyT ok = shfl_xor_any(k[r], (int)stride);
+                    const uint32_t og = (uint32_t)__shfl_xor((int)g[r], (int)stride);
+                    const bool lower = (lane & stride) == 0;
+                    const bool up = (i & size) == 0;
+                    const bool other_less = ent_less3<KeyT>(oh, ok, og, h[r], k[r], g[r]);
+                    const bool mine_less = ent_less3<KeyT>(h[r], k[r], g[r], oh, ok, og);
+                    if ((lower == up) ? other_less : mine_less) {
+                        h[r] = oh;
+                        k[r] = ok;
+                        g[r] = og;
+                    }
+                }
+            }
+        }
+    }
+    uint32_t base = 0;
+    int64_t prev_h_last = 0;
+    KeyT prev_k_last = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = r * 64u + lane;
+        int64_t ph = shfl_any(h[r], (int)((lane + 63) & 63));
+        KeyT pk = shfl_any(k[r], (int)((lane + 63) & 63));
+        if (lane == 0) {
+            ph = prev_h_last;
+            pk = prev_k_last;
+        }
+        const bool first = i < n && (i == 0 || ph != h[r] || pk != k[r]);
+        const unsigned long long bal = __ballot(first);
+        if (first) {
+            const uint32_t o = base + (uint32_t)__popcll(bal & lanemask_lt());
+            gh[o] = h[r];
+            gk[o] = k[r];
+            // ranges this element verifies: r_a = first r >= 1 with b[r] >= tag (arrived before b[r]),
+            // r_h = last r with t[r] >= h
+            int lo = 0, hi = nr;  // b[lo] < tag <= b[hi] (b[nr] = n >= every tag)
+            if (g[r] == 0) hi = 1;
+            else
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sb[mid] >= (int64_t)g[r]) hi = mid;
+                    else lo = mid;
+                }
+            const int ra = std::max(1, hi);
+            int a = 0, z = nr;  // t[a] >= h > t[z] (t[nr] treated as -inf)
+            while (z - a > 1) {
+                const int mid = (a + z) >> 1;
+                if (stt[mid] >= h[r]) a = mid;
+                else z = mid;
+            }
+            const int rh = stt[0] >= h[r] ? a : -1;
+            if (ra <= rh) {
+                atomicAdd(&sdiff[ra], 1);
+                atomicAdd(&sdiff[rh + 1], -1);
+            }
+        }
+        base += (uint32_t)__popcll(bal);
+        prev_h_last = shfl_any(h[r], 63);
+        prev_k_last = shfl_any(k[r], 63);
+    }
+    return base;
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap, int64_t* __restrict__ ctl,
+                                                     int32_t log_bmax, int64_t* __restrict__ bh, KeyT* __restrict__ bk,
+                                                     uint32_t* __restrict__ bi, const SchedDev* __restrict__ sd,
+                                                     int* __restrict__ vacc) {
+    __shared__ int64_t sb[kMaxRanges + 1], stt[kMaxRanges];
+    __shared__ int sdiff[kMaxRanges + 1];
+    const int64_t c = ctl[0];
+    if (c > cand_cap || ctl[1]) return;  // uniform over the grid
+    const int nr = sd->nr;
+    for (int i = threadIdx.x; i <= nr; i += blockDim.x) {
+        sb[i] = sd->b[i];
+        sdiff[i] = 0;
+        if (i < nr) stt[i] = sd->t[i];
+    }
+    __syncthreads();
+    const uint32_t b = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (b < sd->B) {
+        uint32_t* bcnt = bucket_count(ctl) + (size_t)b * kCountStride;
+        uint32_t* bdist = bucket_distinct(ctl, log_bmax) + b;
+        const uint32_t n = *bcnt;
+        int64_t* gh = bh + (size_t)b * kBucketCap;
+        KeyT* gk = bk + (size_t)b * kBucketCap;
+        uint32_t* gi = bi + (size_t)b * kBucketCap;
+        uint32_t nd = 0;
+        if (n > 0)
+            nd = n <= 64    ? wave_sort_bucket_tagged<KeyT, 1>(gh, gk, gi, n, sb, stt, nr, sdiff)
+                 : n <= 128 ? wave_sort_bucket_tagged<KeyT, 2>(gh, gk, gi, n, sb, stt, nr, sdiff)
+                            : wave_sort_bucket_tagged<KeyT, 4>(gh, gk, gi, n, sb, stt, nr, sdiff);
+        if ((threadIdx.x & 63) == 0) {
+            *bdist = nd;
+            if (nd) atomicAdd(bucket_group(ctl, log_bmax) + (b >> 4), nd);
+            *bcnt = 0;
+        }
+    }
+    __syncthreads();
+    int* acc = vacc + (size_t)(blockIdx.x % kVerifyCopies) * (kMaxRanges + 1);
+    for (int i = threadIdx.x; i <= nr; i += blockDim.x)
+        if (sdiff[i]) atomicAdd(&acc[i], sdiff[i]);
+}
+
+// ctl[0..5] and the verification verdict (first range r >= 1 short of k elements, or -1) to
+// coherent host memory, then the flag
+// (then re-arms the candidate counter, the overflow word and the accumulators for the next pass)
+__global__ __launch_bounds__(kBlock) void sched_publish(int64_t* __restrict__ ctl, int* __restrict__ vacc,
+                                                        const SchedDev* __restrict__ sd, int64_t k, int64_t* dst,
+                                                        uint32_t* flag, uint32_t gen) {
+    __shared__ int col[kMaxRanges + 1];
+    const int nr = sd->nr;
+    for (int i = threadIdx.x; i <= nr; i += blockDim.x) {
+        int v = 0;
+        for (int j = 0; j < kVerifyCopies; ++j) {
+            v += vacc[(size_t)j * (kMaxRanges + 1) + i];
+            vacc[(size_t)j * (kMaxRanges + 1) + i] = 0;
+        }
+        col[i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t run = 0, fail = -1, minc = INT64_MAX;
+        for (int r = 0; r < nr; ++r) {
+            run += col[r];
+            if (r >= 1) {
+                minc = std::min(minc, run);
+                if (run < k && fail < 0) fail = r;
+            }
+        }
+        for (int i = 0; i < 6; ++i) dst[i] = ctl[i];
+        dst[6] = fail;
+        dst[7] = minc;
+        ctl[0] = 0;
+        ctl[1] = 0;
+    }
+    publish_flag(flag, gen);
 }
 
 // ctl[0..5] -> coherent host memory + flag (one wave; the host spins instead of a stream sync);
@@ -705,6 +1079,22 @@ struct DistinctState {
     void* log_k = nullptr;
     uint32_t* log_i = nullptr;      // chunk-relative arrival index
     int64_t log_n = 0, log_cap = 0, log_limit = 0;
+    // the scheduled pass (sched_sample): range bounds, its own merge area, the set's backup
+    SchedDev* sdev = nullptr;
+    SchedDev* sstage = nullptr;     // pinned
+    int64_t* sctl = nullptr;        // ctl words + bucket counts of the scheduled merge
+    int32_t log_bmax_s = -1;
+    int64_t* sbh = nullptr;
+    void* sbk = nullptr;
+    uint32_t* sbi = nullptr;
+    int* vacc = nullptr;            // [kVerifyCopies][kMaxRanges + 1]
+    int64_t* bak_h = nullptr;       // [k] the set before the pass
+    void* bak_k = nullptr;
+    int64_t* shc = nullptr;         // coherent host: published words + flag at [12]
+    int64_t* shc_dev = nullptr;
+    uint32_t sgen = 0;
+    bool sched = true;              // RSV_ORDERED_SCHED=0: the chunk loop only
+    double sched_beta = 1.6;        // RSV_SCHED_BETA (test hook: a small beta forces the fallback)
     uint32_t* perm = nullptr;       // [ord_cap] one segment's candidates in arrival order
     uint32_t* sorted_i = nullptr;   // [ord_cap] radix-sort key output
     int64_t ord_cap = 0;            // capacity of the two buffers above and of the pinned copies
@@ -809,6 +1199,8 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
     d->log_limit = std::max<int64_t>(d->cand_limit, std::min<int64_t>(std::max<int64_t>(32 * d->cand_limit, 1 << 22), 1 << 27));
     if (const char* v = std::getenv("RSV_ORDERED_LOG_LIMIT"))  // test hook: force eager replays
         d->log_limit = std::max<int64_t>(d->cand_limit, std::atoll(v));
+    if (const char* v = std::getenv("RSV_ORDERED_SCHED")) d->sched = v[0] != '0';
+    if (const char* v = std::getenv("RSV_SCHED_BETA")) d->sched_beta = std::atof(v);
     if (const char* v = std::getenv("RSV_SPEC_MIN_BATCH"))  // test hook: speculative publication
         d->spec_min = std::max<int64_t>(1, std::atoll(v));
     hipError_t e = hipSuccess;
@@ -821,7 +1213,8 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
     while (((int64_t)1 << (log_bmax + kBucketAvgLog)) < (int64_t)k + d->cand_limit) ++log_bmax;
     const double bucket_bytes = (double)((int64_t)1 << log_bmax) * kBucketCap * (8 + key_width);
     const bool bucketed = bucket_bytes <= 256.0 * 1024 * 1024;
-    const size_t ctl_bytes = kCtlWords * 8 + (bucketed ? ((size_t)(kCountStride + 1) * 4 << log_bmax) : 0);
+    const size_t ctl_bytes =
+        kCtlWords * 8 + (bucketed ? ((size_t)(kCountStride + 1) * 4 << log_bmax) + 4 * (((size_t)1 << log_bmax >> 4) + 1) : 0);
     A((void**)&d->ctl, ctl_bytes);
     if (e == hipSuccess) e = hipMemset(d->ctl, 0, ctl_bytes);  // once: bucket_sort keeps the counts zeroed
     d->counter = (unsigned long long*)d->ctl;
@@ -834,6 +1227,7 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
         if (e == hipSuccess) d->log_bmax = log_bmax;
     }
     A((void**)&d->d_count, 32);
+
     A((void**)&d->samp, 2 * kSample * 8);
     if (e == hipSuccess) {
         size_t tb = 0;  // the threshold sample's sort
@@ -861,13 +1255,15 @@ void distinct_destroy(DistinctState* d) {
     if (!d) return;
     void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->ctl, d->bh, d->bk, d->mh0, d->mh1, d->mk0,
                   d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp, d->log_h, d->log_k, d->log_i,
-                  d->perm, d->sorted_i};
+                  d->perm, d->sorted_i, d->sdev, d->sctl, d->sbh, d->sbk, d->sbi, d->vacc, d->bak_h, d->bak_k};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
     pool_host_free(d->h_pinned);
     pool_host_free(d->hc);
     pool_host_free(d->ph);
     pool_host_free(d->pk);
     pool_host_free(d->pp);
+    pool_host_free(d->sstage);
+    pool_host_free(d->shc);
     delete d;
 }
 
@@ -1333,6 +1729,221 @@ static hipError_t replay_log(DistinctState* d, hipStream_t st) {
     return hipSuccess;
 }
 
+// the scheduled pass's buffers for merges of up to `entries` (set + candidates); allocated on first use
+template <typename KeyT>
+static hipError_t sched_ensure(DistinctState* d, int32_t lb, hipStream_t st) {
+    hipError_t e = hipSuccess;
+    if (!d->sdev) {
+        if ((e = pool_device_alloc((void**)&d->sdev, sizeof(SchedDev)))) return e;
+        if ((e = pool_host_alloc((void**)&d->sstage, sizeof(SchedDev), hipHostMallocDefault))) return e;
+        if ((e = pool_host_alloc((void**)&d->shc, 128, hipHostMallocCoherent | hipHostMallocMapped))) return e;
+        if ((e = hipHostGetDevicePointer((void**)&d->shc_dev, d->shc, 0))) return e;
+        ((uint32_t*)(d->shc + 12))[0] = 0;
+        if ((e = pool_device_alloc((void**)&d->vacc, (size_t)kVerifyCopies * (kMaxRanges + 1) * 4))) return e;
+        if ((e = hipMemsetAsync(d->vacc, 0, (size_t)kVerifyCopies * (kMaxRanges + 1) * 4, st))) return e;  // re-armed by sched_publish
+        if ((e = pool_device_alloc((void**)&d->bak_h, (size_t)d->k * 8))) return e;
+        if ((e = pool_device_alloc(&d->bak_k, (size_t)d->k * d->kw))) return e;
+    }
+    if (lb > d->log_bmax_s) {
+        for (void* p : {(void*)d->sctl, (void*)d->sbh, d->sbk, (void*)d->sbi}) pool_device_free(p);
+        d->sctl = nullptr;
+        d->sbh = nullptr;
+        d->sbk = nullptr;
+        d->sbi = nullptr;
+        d->log_bmax_s = -1;
+        if ((e = hipStreamSynchronize(st))) return e;  // the old area may still be read by queued work
+        const size_t B = (size_t)1 << lb;
+        const size_t ctl_bytes = kCtlWords * 8 + (kCountStride + 1) * 4 * B + 4 * ((B >> 4) + 1);
+        if ((e = pool_device_alloc((void**)&d->sctl, ctl_bytes))) return e;
+        if ((e = hipMemsetAsync(d->sctl, 0, ctl_bytes, st))) return e;  // counts, counter: re-armed after each pass
+        if ((e = pool_device_alloc((void**)&d->sbh, B * kBucketCap * 8))) return e;
+        if ((e = pool_device_alloc(&d->sbk, B * kBucketCap * sizeof(KeyT)))) return e;
+        if ((e = pool_device_alloc((void**)&d->sbi, B * kBucketCap * 4))) return e;
+        d->log_bmax_s = lb;
+    }
+    return hipSuccess;
+}
+
+// The scheduled pass over keys[0, n) of a batch, heap full (see SchedDev).  Bounds: with D
+// distinct elements seen, the k-th smallest hash sits near fraction k / D of the range; D at
+// position P is predicted as D0 + dfr (P - S0) (D0 from the current bound, dfr the history's
+// distinct fraction, clamped to [0.5, 1]), and range r's bound keeps fraction beta k / D(start)
+// (beta = 1.6: a stream whose new-distinct rate falls to ~60% of its history's still verifies).
+// Ranges grow geometrically (<= kMaxRanges).  *done = false: nothing changed, run the chunk loop.
+template <typename KeyT>
+static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n, hipStream_t st,
+                        bool* done) {
+#define STRY(x)                                                                                        \
+    do {                                                                                               \
+        hipError_t _e = (x);                                                                           \
+        if (_e != hipSuccess) {                                                                        \
+            set_error(std::string("distinct (scheduled pass): " #x ": ") + hipGetErrorString(_e));    \
+            return _e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;                     \
+        }                                                                                              \
+    } while (0)
+    *done = false;
+    const int64_t k = d->k;
+    if (d->m != k || d->max_h == INT64_MIN || n >= ((int64_t)1 << 31) || d->set_cap < k) return RSV_OK;
+    const double beta = d->sched_beta;
+    const double two64 = 18446744073709551616.0;
+    auto ufrac = [&](int64_t t) { return ((double)((uint64_t)t - (uint64_t)INT64_MIN) + 1.0) / two64; };
+    auto bound_at = [&](double frac) -> int64_t {  // largest t with ufrac(t) <= frac
+        if (frac >= 1.0) return INT64_MAX;
+        const double x = std::floor(frac * two64) - 1.0;
+        return x < 0 ? INT64_MIN : (int64_t)((uint64_t)x ^ 0x8000000000000000ull);
+    };
+    SchedDev plan;
+    SchedDev* sp = &plan;
+    const double S0 = std::max(1.0, (double)d->seen);
+    const int64_t t0 = d->max_h - 1;
+    const double D0 = std::max((double)k, (double)k / ufrac(t0));
+    const double dfr = std::min(1.0, std::max(0.5, D0 / S0));
+    const double g = std::max(1.08, std::pow((S0 + (double)n) / S0, 1.0 / (kMaxRanges - 2)));
+    int nr = 0;
+    sp->b[0] = 0;
+    sp->t[0] = t0;
+    for (double P = S0 * g;; P *= g) {
+        ++nr;
+        int64_t bn = ((int64_t)(P - S0) + 15) & ~(int64_t)15;
+        if (bn >= n - 16 || nr == kMaxRanges) {
+            sp->b[nr] = n;
+            break;
+        }
+        bn = std::max(bn, sp->b[nr - 1] + 16);
+        sp->b[nr] = bn;
+        const double D = D0 + dfr * (double)bn;
+        sp->t[nr] = std::min(sp->t[nr - 1], bound_at(beta * (double)k / D));
+    }
+    sp->nr = nr;
+    if (nr < 2) return RSV_OK;  // one range: the plain chunk loop does the same work
+    // expected candidates (duplicates included), the buffer, and the bucket map's regions.  The
+    // merge's entries are uniform in h below their range's bound: F(h) = sum_r len_r min(u, u_r)
+    // (u = fraction of the hash range below h); the set's k members count as range 0 elements
+    // (uniform below t[0]: k / u_0 of them per unit of u)
+    double c_pred = 0;
+    for (int r = 0; r < nr; ++r) c_pred += (double)(sp->b[r + 1] - sp->b[r]) * std::min(1.0, ufrac(sp->t[r]));
+    auto flen = [&](int r) {
+        return (double)(sp->b[r + 1] - sp->b[r]) + (r == 0 ? (double)k / ufrac(sp->t[0]) : 0.0);
+    };
+    double F_top = 0, L_all = 0;
+    for (int r = 0; r < nr; ++r) {
+        F_top += flen(r) * ufrac(sp->t[r]);
+        L_all += flen(r);
+    }
+    const int64_t cap = std::min<int64_t>((int64_t)(1.5 * c_pred) + 4 * 4096, ((int64_t)1 << 31) - 1);
+    int32_t lb = 1;  // ~<= 64 entries per bucket: most sort in a single 64-lane pass
+    while (((int64_t)1 << (lb + 6)) < k + cap) ++lb;
+    if (((int64_t)kBucketCap * 8 + 20) << lb > ((int64_t)1 << 30)) return RSV_OK;  // > 1 GiB of buckets: chunk loop
+    sp->lb = (uint32_t)lb;
+    sp->B = 1u << lb;
+    const int64_t t_lo = sp->t[nr - 1];
+    const double F_lo = L_all * ufrac(t_lo);
+    const double lo_frac = std::min(0.9, std::max(0.02, F_lo / F_top));
+    sp->B_lo = std::min<uint32_t>(sp->B - 1, std::max<uint32_t>(1, (uint32_t)(lo_frac * sp->B)));
+    const uint64_t span_lo = (uint64_t)t_lo - (uint64_t)INT64_MIN;
+    sp->lo_mult = span_lo == UINT64_MAX ? 1ull : UINT64_MAX / (span_lo + 1);
+    const double Fspan = std::max(F_top - F_lo, 1e-30);
+    for (int p = 0; p + 1 < nr; ++p) {
+        double A = 0, Bc = 0;
+        for (int r = 0; r < nr; ++r) {
+            if (r <= p) A += flen(r);
+            else Bc += flen(r) * ufrac(sp->t[r]);
+        }
+        sp->hi_a[p] = (float)(A / Fspan);
+        sp->hi_c[p] = (float)((Bc - F_lo) / Fspan);
+    }
+    // the log holds this batch's candidates as one segment
+    if (d->log_n + cap > d->log_limit) {
+        if (cap > d->log_limit) return RSV_OK;
+        if (!d->segs.empty()) STRY(replay_log<KeyT>(d, st));
+        if (d->log_n + cap > d->log_limit) return RSV_OK;
+    }
+    STRY(ensure_log(d, d->log_n + cap, st));
+    STRY(sched_ensure<KeyT>(d, lb, st));
+    std::memcpy(d->sstage, sp, sizeof(SchedDev));  // the previous pass has read its copy (we waited on it)
+
+    const size_t kw = sizeof(KeyT);
+    STRY(hipMemcpyAsync(d->sdev, d->sstage, sizeof(SchedDev), hipMemcpyHostToDevice, st));
+    const unsigned B = sp->B;
+    KeyT* bk = (KeyT*)d->sbk;
+    if (d->timer) d->timer->mark(st);
+    {
+        const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 32 + 1), 1), 256 * 32);
+        KeyT* lk = (KeyT*)d->log_k + d->log_n;
+#define RSV_SCHED_FILTER(H)                                                                                             \
+    hipLaunchKernelGGL((sched_filter<KeyT, H>), dim3(grid), dim3(kBlock), 0, st, keys, hashes, n, d->r0, d->r1,          \
+                       (const SchedDev*)d->sdev, d->log_h + d->log_n, lk, d->log_i + d->log_n, d->sctl, cap, d->set_h,  \
+                       (const KeyT*)d->set_k, k, d->sbh, bk, d->sbi, d->log_bmax_s, d->bak_h, (KeyT*)d->bak_k)
+        switch (d->hash_kind) {
+        case kHashJavaLong: RSV_SCHED_FILTER(kHashJavaLong); break;
+        case kHashJavaInt: RSV_SCHED_FILTER(kHashJavaInt); break;
+        case kHashPrecomputed: RSV_SCHED_FILTER(kHashPrecomputed); break;
+        default: RSV_SCHED_FILTER(kHashIdentity);
+        }
+#undef RSV_SCHED_FILTER
+        STRY(hipGetLastError());
+    }
+    if (d->timer) d->timer->mark(st);
+    hipLaunchKernelGGL(sched_sort<KeyT>, dim3((B + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, k, cap,
+                       d->sctl, d->log_bmax_s, d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
+    hipLaunchKernelGGL(bucket_emit<KeyT>, dim3((B + kEmitBuckets - 1) / kEmitBuckets), dim3(kBlock), 0, st, k, cap,
+                       d->sctl, d->log_bmax_s, (const int64_t*)d->sbh, (const KeyT*)bk, k, d->set_h, (KeyT*)d->set_k,
+                       (int32_t)sp->lb);
+    const uint32_t gen = ++d->sgen;
+    uint32_t* flag = (uint32_t*)(d->shc + 12);
+    hipLaunchKernelGGL(sched_publish, dim3(1), dim3(kBlock), 0, st, d->sctl, d->vacc,
+                       (const SchedDev*)d->sdev, k, d->shc_dev, (uint32_t*)(d->shc_dev + 12), gen);
+    STRY(hipGetLastError());
+    {
+        const auto t0w = std::chrono::steady_clock::now();
+        bool seen = false;
+        for (uint32_t spin = 1;; ++spin) {
+            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == gen) {
+                seen = true;
+                break;
+            }
+            __builtin_ia32_pause();
+            if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0w > std::chrono::milliseconds(50)) break;
+        }
+        if (!seen) {
+            STRY(hipStreamSynchronize(st));
+            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != gen) STRY(hipErrorUnknown);
+        }
+    }
+    int64_t hv[8];
+    for (int i = 0; i < 8; ++i) hv[i] = __atomic_load_n(d->shc + i, __ATOMIC_RELAXED);
+    const int64_t c = hv[0];
+    static const bool debug = std::getenv("RSV_SCHED_DEBUG") != nullptr;
+    if (debug)
+        std::fprintf(stderr, "[rsv sched] n=%lld ranges=%d cand=%lld pred=%.0f cap=%lld bucket_overflow=%lld "
+                             "failed_range=%lld min_count=%lld k=%lld\n",
+                     (long long)n, nr, (long long)c, c_pred, (long long)cap, (long long)hv[1], (long long)hv[6],
+                     (long long)hv[7], (long long)k);
+    if (c > cap || hv[1]) {  // buffer or bucket overflow: nothing was merged; the counts were not consumed
+        STRY(hipMemsetAsync(d->sctl + kCtlWords, 0, (size_t)kCountStride * 4 * B, st));
+        return RSV_OK;
+    }
+    if (hv[6] >= 0) {  // a predicted bound was too tight: put the set back, the chunk loop redoes the batch
+        STRY(hipMemcpyAsync(d->set_h, d->bak_h, (size_t)k * 8, hipMemcpyDeviceToDevice, st));
+        STRY(hipMemcpyAsync(d->set_k, d->bak_k, (size_t)k * kw, hipMemcpyDeviceToDevice, st));
+        return RSV_OK;
+    }
+    const int64_t old_max = d->max_h;
+    d->m = std::min<int64_t>(hv[2], k);
+    d->set_top = hv[3];
+    if (d->m == k) d->max_h = d->set_top;
+    if (d->m == k) d->over = hv[5] != 0 || (d->over && d->max_h == old_max);
+    d->rate_c = c;
+    d->rate_m = n;
+    d->rate_span = (double)((uint64_t)t0 - (uint64_t)INT64_MIN) + 1.0;
+    d->segs.push_back(DistinctState::Seg{d->log_n, c, n});
+    d->log_n += c;
+    d->seen += n;
+    *done = true;
+    return RSV_OK;
+#undef STRY
+}
+
 // RSV_DISTINCT_ORDERED: the reference's exact RandomValues (strict `elemHash < maxHash` and the
 // scala PriorityQueue's choice among equal hashes, Sampler.scala:394-409), without replaying the
 // stream on the host unless a tie forces it.
@@ -1365,9 +1976,22 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
     OTRY(ensure_caps(d, 0, std::min<int64_t>(k, ccap + d->m), st));
     int64_t pos = 0;
     int64_t m_next = 0;  // chunk length after an overflow retry
+    bool sched_tried = !d->sched || d->log_bmax < 0;
     while (pos < n) {
         const bool full = d->m == k;
         if (full && d->max_h == INT64_MIN) break;  // nothing is < Long.MinValue
+        // a full heap and a long rest: one scheduled pass (falls back to the chunks below)
+        if (full && !sched_tried && n - pos >= 8 * ccap) {
+            sched_tried = true;
+            bool done = false;
+            if (int rc = sched_sample<KeyT>(d, keys + pos, hashes ? hashes + pos : nullptr, n - pos, st, &done))
+                return rc;
+            if (done) {
+                pos = n;
+                break;
+            }
+            continue;
+        }
         const int64_t tinc = full ? d->max_h - 1 : INT64_MAX;
         int64_t m;
         if (m_next) {

@@ -36,15 +36,15 @@ hipError_t launch_segmented(const void* keys, int key_width, const int64_t* offs
     if (S <= 0) return hipSuccess;
     // RSV_K2=1 keeps the round-1 kernel (A/B measurements); it also serves tables too big for
     // four waves' LDS here
-    static const bool v1 = [] {
+    static const int form = [] {
         const char* e = std::getenv("RSV_K2");
-        return e && e[0] == '1';
+        return e ? std::atoi(e) : 0;
     }();
     const size_t lds = segmented_lds_bytes(k);
-    if (v1 || lds > 160 * 1024) return launch_segmented_v1(keys, key_width, offsets, S, k, dp, out, counts, st);
+    if (form == 1 || lds > 160 * 1024) return launch_segmented_v1(keys, key_width, offsets, S, k, dp, out, counts, st);
+    const uint32_t k0 = (uint32_t)dp.seed, k1 = (uint32_t)(dp.seed >> 32);
     const uint64_t blocks = ((uint64_t)S + kWaves - 1) / kWaves;
     const unsigned grid = (unsigned)std::min<uint64_t>(blocks, 256ull * 16);
-    const uint32_t k0 = (uint32_t)dp.seed, k1 = (uint32_t)(dp.seed >> 32);
     if (key_width == 8)
         hipLaunchKernelGGL(k2_segmented<int64_t>, dim3(grid), dim3(64 * kWaves), lds, st, (const int64_t*)keys,
                            offsets, S, k, k0, k1, dp.stream, (int64_t*)out, counts);

@@ -9,6 +9,7 @@ keeps the order-independent bottom-k by (hash, key): everything below the maximu
 """
 import json
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -445,3 +446,58 @@ def test_set_mode_speculative_publication(cuda, oracle, monkeypatch, key_type):
     r = oracle.Distinct(300, 11, oracle.HASH_IDENTITY)
     ent = sorted({(oracle.scramble(r.r0, r.r1, (int(x) * 0x9E3779B1) % 3), int(x)) for x in xs.tolist()})
     assert d.result().tolist() == [x for _, x in ent[:300]]
+
+
+def _c4_like(cuda, n, seed):
+    sys_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools")
+    if sys_path not in sys.path:
+        sys.path.insert(0, sys_path)
+    import workloads
+
+    return workloads.c4_data(n, cuda, seed=seed)
+
+
+@pytest.mark.parametrize("k,n,seed,batches", [(2048, 4_000_000, 3, 1), (1000, 3_000_000, 5, 3), (64, 2_000_000, 9, 2)])
+def test_ordered_scheduled_pass(cuda, oracle, monkeypatch, k, n, seed, batches):
+    """The scheduled pass (one filter with per-range bounds fixed ahead, verified in the merge,
+    rsv_distinct.hip sched_sample) gives the reference's set; so does the chunk loop alone
+    (RSV_ORDERED_SCHED=0, read at creation), and a schedule too tight to verify
+    (RSV_SCHED_BETA=0.2) that falls back to the chunk loop with the set restored."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    vals = _c4_like(cuda, n, seed)
+    host = vals.cpu().numpy()
+    ref = oracle.Distinct(k, 17, oracle.HASH_JAVA_LONG)
+    ref.sample_all(host)
+    want = ref.result()[0].tolist()
+    cuts = np.linspace(0, n, batches + 1).astype(np.int64)
+    for env in ({}, {"RSV_ORDERED_SCHED": "0"}, {"RSV_SCHED_BETA": "0.2"}):
+        for key, v in env.items():
+            monkeypatch.setenv(key, v)
+        d = Sampler.distinct(k, seed=17)()
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            d.sample_all(vals[a:b])
+        assert d.result().tolist() == want, env
+        for key in env:
+            monkeypatch.delenv(key)
+    del vals
+    torch.cuda.empty_cache()
+
+
+def test_ordered_scheduled_pass_ties(cuda, oracle):
+    """Colliding Long.hashCode values (tied boundary buckets) through the scheduled pass: the pass's
+    candidates form one logged segment, and the host replay over it reproduces the reference."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    rng = np.random.default_rng(44)
+    vals = _colliding(rng, 3_000_000, 400_000)
+    vals = np.concatenate([vals, vals[:1_000_000]])
+    ref = oracle.Distinct(1500, 23, oracle.HASH_JAVA_LONG)
+    ref.sample_all(vals)
+    d = Sampler.distinct(1500, seed=23)()
+    d.sample_all(torch.from_numpy(vals).to(cuda))
+    assert d.result().tolist() == ref.result()[0].tolist()

@@ -83,7 +83,7 @@ def main(src: str, dst: str) -> None:
                     f.write(line)
     k1 = summary.get("k1", {})
     if "hbm_bytes_per_launch" in k1:
-        n = summary.get("bench_line", {}).get("config", {}).get("n_per_step")
+        n = summary.get("bench_line", {}).get("config", {}).get("keys_per_gpu")
         with open(os.path.join(dst, "pmc_k1.json"), "w") as f:
             json.dump({"n": n, "hbm_bytes_per_launch": k1["hbm_bytes_per_launch"], "kernel": k1["kernel"],
                        "source_run": summary["source_run"]}, f, indent=1)
