@@ -22,18 +22,27 @@ namespace {
 constexpr int kBlock = 256;
 
 // K1: grid-stride over level-0 blocks (16 indices each); one bit per block marks a zero byte, and
-// every 16 iterations the marked blocks go through the wave's LDS queue so the level-1 draws run
-// with all 64 lanes busy (rsv_scan.h k1_body_bits).  Hits (k ln(n/k) of them) go straight to
+// every 16 iterations the marked blocks go through the wave's LDS queue -- with their 16-bit
+// zero-byte fold, so a sparse-region resolve needs no level-0 recompute -- and the level-1 draws
+// run with all 64 lanes busy (rsv_scan.h k1_body_z).  Hits (k ln(n/k) of them) go straight to
 // global atomicMax on the k-slot winner table: 14k atomics per 1e9 indices at k = 1024.
 constexpr int kK1Unroll = 2;  // level-0 blocks per lane per iteration (two Philox chains in flight)
+
+// per-wave LDS of k1_body_z: block queue (< 64 waiting + one round of 64), the window's folds,
+// the per-candidate queue
+struct K1Lds {
+    uint64_t q[kBlock / 64][128];
+    uint16_t wy[kBlock / 64][kK1ZWin * 64];
+    uint64_t cq[kBlock / 64][kQueue];
+};
 
 __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k, uint64_t lo,
                                                          uint64_t hi, uint64_t g_begin,
                                                          uint64_t n_groups,
                                                          unsigned long long* __restrict__ win) {
-    __shared__ uint32_t qs[kBlock / 64][63 + 64 + 1];
-    __shared__ uint64_t cqs[kBlock / 64][kQueue];
-    k1_body_bits<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
+    __shared__ K1Lds L;
+    const int w = threadIdx.x >> 6;
+    k1_body_z<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wy[w], L.cq[w]);
 }
 
 // K1 + resolve_publish in one dispatch (single-launch batches, k <= kK1FusedMaxK): every
@@ -51,10 +60,10 @@ __global__ __launch_bounds__(kBlock) void k1_resolve_publish(DrawKey dk, uint32_
                                                              int64_t base, int64_t n, KeyT* __restrict__ slot_key,
                                                              int64_t* __restrict__ slot_idx, int fresh, int64_t m,
                                                              KeyT* dst, uint32_t* flag, uint32_t gen) {
-    __shared__ uint32_t qs[kBlock / 64][63 + 64 + 1];
-    __shared__ uint64_t cqs[kBlock / 64][kQueue];
+    __shared__ K1Lds L;
     __shared__ uint32_t last;
-    k1_body_bits<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
+    k1_body_z<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, L.q[threadIdx.x >> 6], L.wy[threadIdx.x >> 6],
+                         L.cq[threadIdx.x >> 6]);
     // This wave's winner atomics are performed once vmcnt drains: on gfx942/gfx950 a global atomic
     // without return still counts in vmcnt until the memory system acknowledges it (there is no
     // separate vscnt), and an agent-scope atomic is performed at the agent's coherence point (the

@@ -255,7 +255,15 @@ __device__ __forceinline__ void k1_body_bits(const DrawKey& dk, uint32_t k, uint
                 w[u] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
             if (base >= off_sparse && base + U * 64 <= ng) {  // steady state: zero-byte test only
 #pragma unroll
-                for (int u = 0; u < U; ++u) bits = (bits << 1) | (uint32_t)any_zero_byte(w[u]);
+                for (int u = 0; u < U; ++u) {
+                    // some b_e == 0 <=> the 16-bit OR of the planes' halves is not all ones
+                    const uint32_t x = w[u].x | w[u].y | w[u].z | w[u].w;
+                    uint32_t y;
+                    asm("v_or_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
+                        : "=v"(y) : "v"(x));
+                    const bool has = (uint16_t)y != 0xFFFFu;
+                    bits = bits + bits + (uint32_t)has;
+                }
             } else {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -269,6 +277,156 @@ __device__ __forceinline__ void k1_body_bits(const DrawKey& dk, uint32_t k, uint
         push_bits<U>(bits, nb, base0, stride, q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
     }
     drain_blocks(q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
+}
+
+// ---- K1 with the zero-byte mask carried in the queue (k1_body_z) -------------------------------
+// k1_body_bits pushes a block's OFFSET, and the resolve recomputes its level-0 Philox to find the
+// candidate bytes.  In the sparse region (i + 1 >= 256 k) a candidate is exactly a zero byte, so
+// the 16-bit fold of the block's planes (y: bit e clear <=> b_e == 0) says everything the resolve
+// needs: the main loop leaves y in an LDS window beside the bit, the push packs it into the queue
+// entry, and the resolve goes straight to the level-1 draw with b = 0 -- no level-0 recompute, no
+// byte extraction.  Dense-region blocks (i < 256 k) carry y = 0 (all bytes zero is impossible for
+// a real block: probability 2^-128) and take the recomputing resolve.
+constexpr uint32_t kK1ZWin = 32;  // blocks per lane per window (W x U)
+
+// the 16-bit OR of a block's plane halves: bit e clear <=> b_e == 0 (one SDWA op for the fold)
+__device__ __forceinline__ uint32_t fold16(const u32x4& w) {
+    const uint32_t x = w.x | w.y | w.z | w.w;
+    uint32_t y;
+    asm("v_or_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
+        : "=v"(y)
+        : "v"(x));
+    return y;
+}
+
+// level-1 draw of a sparse-region candidate (b = 0): j = floor((L >> 8) (i + 1) / 2^64).
+// hi_uniform (wave-uniform): the counter's high word (i / 2^33) is the same for the whole launch.
+__device__ __forceinline__ uint64_t exact_j_b0(const DrawKey& dk, uint64_t i, bool hi_uniform, uint32_t c1u) {
+    const uint64_t g1 = i >> 1;
+    u32x4 w;
+    if (hi_uniform) w = philox4x32_10_uniform_hi((uint32_t)g1, c1u, dk.s0, dk.s1, dk.k0, dk.k1);
+    else w = philox4x32_10((uint32_t)g1, (uint32_t)(g1 >> 32) | kDomainLevel1, dk.s0, dk.s1, dk.k0, dk.k1);
+    const uint64_t L = (i & 1) ? (((uint64_t)w.z << 32) | w.w) : (((uint64_t)w.x << 32) | w.y);
+    return __umul64hi(L >> 8, i + 1);
+}
+
+template <int U>
+__device__ __forceinline__ void k1_body_z(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                          uint64_t n_groups, unsigned long long* __restrict__ win, uint64_t* q,
+                                          uint16_t* wy, uint64_t* cq) {
+    constexpr int W = kK1ZWin / U;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t qn = 0, cqn = 0;
+    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
+    const uint64_t dense_lim = 256ull * k;
+    const uint32_t ng = (uint32_t)n_groups;  // < 2^31 per launch (host splits)
+    const uint64_t g_sparse = (dense_lim + 14) >> 4;
+    const uint32_t off_sparse = g_sparse <= g_begin ? 0u : (uint32_t)std::min<uint64_t>(g_sparse - g_begin, ng);
+    const uint32_t stride = gridDim.x * blockDim.x * U;
+    const uint32_t c1u = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(lo >> 33) | kDomainLevel1));
+    const bool hi_uniform = (lo >> 33) == ((hi - 1) >> 33);
+    uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
+    const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g_begin >> 32));
+    uint32_t gl = (uint32_t)g_begin + base + lane;
+    uint16_t* wyl = wy + lane;
+    // the steady branch holds blocks wholly inside [lo, hi) and the sparse region
+    const uint32_t off_steady = std::max<uint32_t>(off_sparse, (lo & 15) ? 1u : 0u);
+    const uint32_t ng_steady = ng - ((hi & 15) ? 1u : 0u);
+
+    // all lanes take a queue entry (valid lanes only): its first zero byte gets the level-1 draw
+    // here; a block with more (~3 % of blocks) goes back on the block queue with that byte masked
+    // (y |= its bit), to be met again.  Clipped indices (outside [lo, hi)) were folded into y by
+    // the main loop, so no entry needs a clip.
+    auto resolve = [&](bool valid, uint64_t ent) {
+        const uint32_t off = (uint32_t)ent, y = (uint32_t)(ent >> 32);
+        const uint64_t g = g_begin + off, i0 = g << 4;
+        const bool dense = valid && y == 0;
+        if (__builtin_amdgcn_ballot_w64(dense)) resolve_block(dk, dense, g, lo, hi, dense_lim, k, cq, cqn, lane, hit);
+        const uint32_t zm = (valid && !dense) ? (~y & 0xFFFFu) : 0u;
+        uint32_t rest = 0;
+        if (zm) {
+            const uint32_t e = __builtin_ctz(zm);
+            rest = zm & (zm - 1);
+            const uint64_t i = i0 + e;
+            const uint64_t j = exact_j_b0(dk, i, hi_uniform, c1u);
+            if (j < k) hit((uint32_t)j, i);
+        }
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(rest != 0);
+        if (bal) {
+            if (rest) {
+                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, qn));
+                q[pos] = (uint64_t)off | ((uint64_t)(~rest & 0xFFFFu) << 32);
+            }
+            qn += (uint32_t)__popcll(bal);
+        }
+    };
+
+    while (base < ng) {  // wave-uniform
+        const uint32_t base0 = base;
+        uint32_t bits = 0, nb = 0;
+        for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride, nb += U) {
+            u32x4 w[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                w[u] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
+            if (base >= off_steady && base + U * 64 <= ng_steady) {  // steady state: zero-byte test only
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t y = fold16(w[u]);
+                    bits = bits + bits + (uint32_t)((uint16_t)y != 0xFFFFu);
+                    wyl[(t * U + u) * 64] = (uint16_t)y;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t off = base + u * 64 + lane;
+                    const uint64_t i0 = (g_begin + off) << 4;
+                    const bool dense = i0 + 1 < dense_lim;
+                    // indices outside [lo, hi) count as nonzero bytes (never candidates)
+                    const uint32_t y = dense ? 0u : (fold16(w[u]) | (~clip_mask16(i0, lo, hi) & 0xFFFFu));
+                    const bool has = (off < ng) & (dense | ((uint16_t)y != 0xFFFFu));
+                    bits = bits + bits + (uint32_t)has;
+                    wyl[(t * U + u) * 64] = (uint16_t)y;
+                }
+            }
+        }
+        // push the window's marked blocks: each round every lane with bits left pushes its lowest
+        // (prefix by mbcnt, offsets by 24-bit multiplies: stride < 2^24 -- full-rate VALU ops)
+        const uint32_t lbase = base0 + lane;
+        __builtin_amdgcn_wave_barrier();
+        for (;;) {
+            const bool has = bits != 0;
+            const unsigned long long bal = __builtin_amdgcn_ballot_w64(has);
+            if (!bal) break;
+            if (has) {
+                const uint32_t idx = nb - 1 - __builtin_ctz(bits);
+                bits &= bits - 1;
+                const uint32_t off = lbase + __umul24(idx / U, stride) + (idx % U) * 64u;
+                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, qn));
+                q[pos] = (uint64_t)off | ((uint64_t)wyl[idx * 64] << 32);
+            }
+            qn += (uint32_t)__popcll(bal);
+            while (qn >= 64) {  // a resolve may append (blocks with more zero bytes)
+                qn -= 64;
+                __builtin_amdgcn_wave_barrier();
+                const uint64_t ent = q[qn + lane];
+                __builtin_amdgcn_wave_barrier();
+                resolve(true, ent);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+    while (qn > 0) {  // the last partial rounds (appends shrink geometrically)
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t nv = std::min<uint32_t>(qn, 64u);
+        qn -= nv;
+        const bool valid = lane < nv;
+        const uint64_t ent = valid ? q[qn + lane] : 0ull;
+        __builtin_amdgcn_wave_barrier();
+        resolve(valid, ent);
+    }
+    __builtin_amdgcn_wave_barrier();
+    drain_queue(dk, cq, cqn, lane, k, hit);
 }
 
 }  // namespace rsv

@@ -73,6 +73,30 @@ __global__ __launch_bounds__(256) void philox_only(DrawKey dk, uint64_t n_groups
     if (c == 0x12345u) atomicAdd(cnt, c);
 }
 
+// V2: the product's level-0 loop (uniform-hi Philox, U blocks per lane, the bit-window test) with
+// the pushes removed: the cost of everything but the candidate handling
+template <int U>
+__global__ __launch_bounds__(256) void k1_l0_bits_only(DrawKey dk, uint64_t n_groups, unsigned long long* cnt) {
+    const uint32_t ng = (uint32_t)n_groups;
+    const uint32_t stride = gridDim.x * blockDim.x * U;
+    uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
+    uint32_t gl = base + (threadIdx.x & 63);
+    uint32_t acc = 0;
+    while (base < ng) {
+        uint32_t bits = 0;
+        for (int t = 0; t < 32 / U && base < ng; ++t, base += stride, gl += stride) {
+            u32x4 w[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                w[u] = philox4x32_10_uniform_hi(gl, 0u, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
+#pragma unroll
+            for (int u = 0; u < U; ++u) bits = (bits << 1) | (uint32_t)any_zero_byte(w[u]);
+        }
+        acc ^= bits;
+    }
+    if (acc == 0x12345u) atomicAdd(cnt, acc);
+}
+
 template <int U>
 __global__ __launch_bounds__(256) void k1_var(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
                                               uint64_t n_groups, unsigned long long* win) {
@@ -87,6 +111,16 @@ __global__ __launch_bounds__(256) void k1_var_bits(DrawKey dk, uint32_t k, uint6
     __shared__ uint32_t qs[4][63 + 64 + 1];
     __shared__ uint64_t cqs[4][kQueue];
     k1_body_bits<U>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k1_var_z(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                                uint64_t n_groups, unsigned long long* win) {
+    __shared__ uint64_t qs[4][128];
+    __shared__ uint16_t wys[4][kK1ZWin * 64];
+    __shared__ uint64_t cqs[4][kQueue];
+    k1_body_z<U>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], wys[threadIdx.x >> 6],
+                       cqs[threadIdx.x >> 6]);
 }
 
 int main(int argc, char** argv) {
@@ -167,6 +201,9 @@ int main(int argc, char** argv) {
                            n_groups, win);
         hipLaunchKernelGGL(k1_var_bits<2>, dim3(4096), dim3(256), 0, 0, dk, 1024u, 1024ull, 1000000000ull, 0ull,
                            n_groups, win);
+        hipLaunchKernelGGL(k1_l0_bits_only<2>, dim3(4096), dim3(256), 0, 0, dk, n_groups, cnt);
+        hipLaunchKernelGGL(k1_var_z<2>, dim3(4096), dim3(256), 0, 0, dk, 1024u, 1024ull, 1000000000ull, 0ull,
+                           n_groups, win);
         CK(hipDeviceSynchronize());
         return 0;
     }
@@ -185,7 +222,10 @@ int main(int argc, char** argv) {
                 time_v(k1_var_bits<2>, "k1 bit-mask push", g, 2);
             return 0;
         }
-        for (int grid : {2048, 4096, 8192, 16384}) {
+        for (int grid : {4096, 8192}) {
+            time_v(k1_var_z<2>, "k1 zero-mask queue", grid / 2, 2);
+            if (run_once(k1_var_z<2>, grid / 2, got)) return 1;
+            printf("  winners identical (z): %s\n", ref == got ? "yes" : "NO");
             time_v(k1_var<2>, "k1 per-iteration push", grid / 2, 2);
             time_v(k1_var_bits<1>, "k1 bit-mask push", grid, 1);
             time_v(k1_var_bits<2>, "k1 bit-mask push", grid / 2, 2);
