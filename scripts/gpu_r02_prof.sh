@@ -2,7 +2,7 @@
 # Round-2 profile set (one gpurun call): VALU issue costs + clock (PMC on tools/micro_valu), the
 # default bench line, rocprofv3 kernel stats and PMC passes for K1 (C2 bench) and K2 (C3).
 # Output: gpurun_out/$OUT/ (summaries get copied into profiles/r02/).
-OUT=${OUT:-r02h}
+OUT=${OUT:-r02z}
 P="rocprofv3 --output-format csv"
 SQ="GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES"
 B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary"
