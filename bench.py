@@ -310,8 +310,12 @@ def main() -> None:
     if rank == 0:
         total = n * world * args.steps
         l0, l1 = R.k1_calls(n, k, offset)
+        # the runtime fuses K1 with the slot resolve only up to 2^27 draws (rsv_runtime.hip rsv_sample_all)
+        fused = os.environ.get("RSV_K1_FUSE") == "1" or (os.environ.get("RSV_K1_FUSE") != "0" and n <= 1 << 27)
+        kname = ("k1_resolve_publish (K1 + the last workgroup's resolve/publish tail)" if fused else
+                 "k1_last_writer (K1 alone; the slot resolve/publish is a separate one-workgroup dispatch)")
         roof = R.valu_roofline(
-            l0, l1, k1_s, "k1_resolve_publish (K1 + the last workgroup's resolve/publish tail)",
+            l0, l1, k1_s, kname,
             note="bound = integer VALU (Philox): K1 reads only the k winning keys (draws depend on the index "
                  "alone, like the reference's sampleAll(IndexedSeq) skip, Sampler.scala:261-273), so the "
                  "SURVEY 8(d) 8 B/elem HBM convention would read " +

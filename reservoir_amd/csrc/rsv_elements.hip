@@ -28,11 +28,14 @@ constexpr int kBlock = 256;
 // global atomicMax on the k-slot winner table: 14k atomics per 1e9 indices at k = 1024.
 constexpr int kK1Unroll = 2;  // level-0 blocks per lane per iteration (two Philox chains in flight)
 
+constexpr unsigned kK1Grid = 256 * 12;
+
 // per-wave LDS of k1_body_z: block queue (< 64 waiting + one round of 64), the window's folds,
 // the per-candidate queue
 struct K1Lds {
     uint64_t q[kBlock / 64][128];
     uint16_t wy[kBlock / 64][kK1ZWin * 64];
+    uint32_t tab[kBlock / 64][kK1ZWin];
     uint64_t cq[kBlock / 64][kQueue];
 };
 
@@ -42,7 +45,7 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
                                                          unsigned long long* __restrict__ win) {
     __shared__ K1Lds L;
     const int w = threadIdx.x >> 6;
-    k1_body_z<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wy[w], L.cq[w]);
+    k1_body_z<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wy[w], L.tab[w], L.cq[w]);
 }
 
 // K1 + resolve_publish in one dispatch (single-launch batches, k <= kK1FusedMaxK): every
@@ -62,8 +65,8 @@ __global__ __launch_bounds__(kBlock) void k1_resolve_publish(DrawKey dk, uint32_
                                                              KeyT* dst, uint32_t* flag, uint32_t gen) {
     __shared__ K1Lds L;
     __shared__ uint32_t last;
-    k1_body_z<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, L.q[threadIdx.x >> 6], L.wy[threadIdx.x >> 6],
-                         L.cq[threadIdx.x >> 6]);
+    const int w = threadIdx.x >> 6;
+    k1_body_z<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wy[w], L.tab[w], L.cq[w]);
     // This wave's winner atomics are performed once vmcnt drains: on gfx942/gfx950 a global atomic
     // without return still counts in vmcnt until the memory system acknowledges it (there is no
     // separate vscnt), and an agent-scope atomic is performed at the agent's coherence point (the
@@ -465,8 +468,9 @@ hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, 
         // and no launch crosses a multiple of 2^32 blocks: the counter's high word is a scalar
         const uint64_t g_wrap = ((g_begin >> 32) + 1) << 32;
         n_groups = std::min<uint64_t>(std::min<uint64_t>(g_end, g_wrap) - g_begin, kMaxGroups);
-        // two resident rounds of 4-wave workgroups (8 waves per SIMD): measured best (tools/micro_k1)
-        const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 16);
+        // 12 four-wave workgroups per CU (with the 20-block window's 18.5 KB of LDS, 8 resident):
+        // measured best of 2560..4096 (tools/micro_k1 zf, r02ad)
+        const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, kK1Grid);
         hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
                            g_begin, n_groups, batch_win);
         hipError_t e = hipGetLastError();
@@ -489,7 +493,7 @@ hipError_t launch_k1_resolve_publish(const DrawParams& dp, uint32_t k, uint64_t 
                                      hipStream_t st) {
     if (!k1_fused_ok(lo, hi, k, key_width)) return hipErrorInvalidValue;
     const uint64_t g_begin = lo >> 4, n_groups = ((hi + 15) >> 4) - g_begin;
-    const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, 256 * 16);
+    const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, kK1Grid);
     if (key_width == 8)
         hipLaunchKernelGGL(k1_resolve_publish<int64_t>, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
                            g_begin, n_groups, batch_win, ticket, (const int64_t*)keys, base, n, (int64_t*)slot_key,

@@ -287,7 +287,7 @@ __device__ __forceinline__ void k1_body_bits(const DrawKey& dk, uint32_t k, uint
 // entry, and the resolve goes straight to the level-1 draw with b = 0 -- no level-0 recompute, no
 // byte extraction.  Dense-region blocks (i < 256 k) carry y = 0 (all bytes zero is impossible for
 // a real block: probability 2^-128) and take the recomputing resolve.
-constexpr uint32_t kK1ZWin = 32;  // blocks per lane per window (W x U)
+constexpr uint32_t kK1ZWin = 20;  // blocks per lane per window (W x U); 16..32 within 2 us, 20 best (r02ad)
 
 // the 16-bit OR of a block's plane halves: bit e clear <=> b_e == 0 (one SDWA op for the fold)
 __device__ __forceinline__ uint32_t fold16(const u32x4& w) {
@@ -300,21 +300,20 @@ __device__ __forceinline__ uint32_t fold16(const u32x4& w) {
 }
 
 // level-1 draw of a sparse-region candidate (b = 0): j = floor((L >> 8) (i + 1) / 2^64).
-// hi_uniform (wave-uniform): the counter's high word (i / 2^33) is the same for the whole launch.
-__device__ __forceinline__ uint64_t exact_j_b0(const DrawKey& dk, uint64_t i, bool hi_uniform, uint32_t c1u) {
+// The level-1 Philox words of index i (L = words x:y for even i, z:w for odd).  hi_uniform (wave-
+// uniform): the counter's high word (i / 2^33) is the same for the whole launch.
+__device__ __forceinline__ u32x4 level1_b0_words(const DrawKey& dk, uint64_t i, bool hi_uniform, uint32_t c1u) {
     const uint64_t g1 = i >> 1;
-    u32x4 w;
-    if (hi_uniform) w = philox4x32_10_uniform_hi((uint32_t)g1, c1u, dk.s0, dk.s1, dk.k0, dk.k1);
-    else w = philox4x32_10((uint32_t)g1, (uint32_t)(g1 >> 32) | kDomainLevel1, dk.s0, dk.s1, dk.k0, dk.k1);
-    const uint64_t L = (i & 1) ? (((uint64_t)w.z << 32) | w.w) : (((uint64_t)w.x << 32) | w.y);
-    return __umul64hi(L >> 8, i + 1);
+    if (hi_uniform) return philox4x32_10_uniform_hi((uint32_t)g1, c1u, dk.s0, dk.s1, dk.k0, dk.k1);
+    return philox4x32_10((uint32_t)g1, (uint32_t)(g1 >> 32) | kDomainLevel1, dk.s0, dk.s1, dk.k0, dk.k1);
 }
 
-template <int U>
+template <int U, int WIN = kK1ZWin>
 __device__ __forceinline__ void k1_body_z(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
                                           uint64_t n_groups, unsigned long long* __restrict__ win, uint64_t* q,
-                                          uint16_t* wy, uint64_t* cq) {
-    constexpr int W = kK1ZWin / U;
+                                          uint16_t* wy, uint32_t* tab, uint64_t* cq) {
+    static_assert(WIN % U == 0 && WIN <= 32, "the window's bits fit one 32-bit mask");
+    constexpr int W = WIN / U;
     const uint32_t lane = threadIdx.x & 63;
     uint32_t qn = 0, cqn = 0;
     auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
@@ -325,13 +324,19 @@ __device__ __forceinline__ void k1_body_z(const DrawKey& dk, uint32_t k, uint64_
     const uint32_t stride = gridDim.x * blockDim.x * U;
     const uint32_t c1u = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(lo >> 33) | kDomainLevel1));
     const bool hi_uniform = (lo >> 33) == ((hi - 1) >> 33);
+    const bool pre_ok = hi <= (1ull << 40);
+    const uint64_t k_hi = (uint64_t)k << 32;
     uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
     const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g_begin >> 32));
     uint32_t gl = (uint32_t)g_begin + base + lane;
     uint16_t* wyl = wy + lane;
+    // window row b holds slot s = WIN-1-b: block base0 + (s / U) stride + (s % U) 64 + lane
+    if (lane < WIN) tab[lane] = ((WIN - 1 - lane) / U) * stride + ((WIN - 1 - lane) % U) * 64u;
+    __builtin_amdgcn_wave_barrier();
     // the steady branch holds blocks wholly inside [lo, hi) and the sparse region
-    const uint32_t off_steady = std::max<uint32_t>(off_sparse, (lo & 15) ? 1u : 0u);
-    const uint32_t ng_steady = ng - ((hi & 15) ? 1u : 0u);
+    const uint32_t off_steady =
+        __builtin_amdgcn_readfirstlane((int)std::max<uint32_t>(off_sparse, (lo & 15) ? 1u : 0u));
+    const uint32_t ng_steady = __builtin_amdgcn_readfirstlane((int)(ng - ((hi & 15) ? 1u : 0u)));
 
     // all lanes take a queue entry (valid lanes only): its first zero byte gets the level-1 draw
     // here; a block with more (~3 % of blocks) goes back on the block queue with that byte masked
@@ -348,14 +353,23 @@ __device__ __forceinline__ void k1_body_z(const DrawKey& dk, uint32_t k, uint64_
             const uint32_t e = __builtin_ctz(zm);
             rest = zm & (zm - 1);
             const uint64_t i = i0 + e;
-            const uint64_t j = exact_j_b0(dk, i, hi_uniform, c1u);
-            if (j < k) hit((uint32_t)j, i);
+            const u32x4 w = level1_b0_words(dk, i, hi_uniform, c1u);
+            const uint32_t Lh = (i & 1) ? w.z : w.x;
+            // j >= floor((Lh >> 8) (i + 1) / 2^32) (the top 24 of L >> 8's 56 bits): when that
+            // already reaches k the candidate loses (all but ~256 k / i of them); exact otherwise.
+            // Needs (Lh >> 8) (i + 1) < 2^64: i < 2^40 for the whole launch (pre_ok, uniform).
+            const bool maybe = !pre_ok || (uint64_t)(Lh >> 8) * (i + 1) < k_hi;
+            if (maybe) {
+                const uint64_t L = ((uint64_t)Lh << 32) | ((i & 1) ? w.w : w.y);
+                const uint64_t j = __umul64hi(L >> 8, i + 1);
+                if (j < k) hit((uint32_t)j, i);
+            }
         }
         const unsigned long long bal = __builtin_amdgcn_ballot_w64(rest != 0);
         if (bal) {
             if (rest) {
-                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, qn));
-                q[pos] = (uint64_t)off | ((uint64_t)(~rest & 0xFFFFu) << 32);
+                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                q[qn + pos] = (uint64_t)off | ((uint64_t)(~rest & 0xFFFFu) << 32);
             }
             qn += (uint32_t)__popcll(bal);
         }
@@ -364,46 +378,74 @@ __device__ __forceinline__ void k1_body_z(const DrawKey& dk, uint32_t k, uint64_
     while (base < ng) {  // wave-uniform
         const uint32_t base0 = base;
         uint32_t bits = 0, nb = 0;
-        for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride, nb += U) {
-            u32x4 w[U];
+        if (base0 >= off_steady && (uint64_t)base0 + (uint64_t)(W - 1) * stride + U * 64 <= ng_steady) {
+            // a whole window of steady iterations, unrolled: the window slot is an immediate LDS
+            // offset, and the bit is shifted in by the compare's carry (v_cmp + v_addc: bits = 2 bits
+            // + has) -- 5 VALU per block beside the Philox and one counter add per iteration
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                w[u] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
-            if (base >= off_steady && base + U * 64 <= ng_steady) {  // steady state: zero-byte test only
+            for (int t = 0; t < W; ++t) {
+                u32x4 w[U];
+                const uint32_t gt = gl + t * stride;
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    w[u] = philox4x32_10_uniform_hi(gt, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t y = fold16(w[u]);
-                    bits = bits + bits + (uint32_t)((uint16_t)y != 0xFFFFu);
-                    wyl[(t * U + u) * 64] = (uint16_t)y;
+                    asm("v_cmp_ne_u32_e32 vcc, 0xffff, %1\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+                        : "+v"(bits)
+                        : "v"(y)
+                        : "vcc");
+                    wyl[(WIN - 1 - (t * U + u)) * 64] = (uint16_t)y;
                 }
-            } else {
+            }
+            base += W * stride;
+            gl += W * stride;
+            nb = W * U;
+        } else {  // a partial window (first, last, or where the dense / clipped blocks lie)
+            for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride, nb += U) {
+                u32x4 w[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t off = base + u * 64 + lane;
-                    const uint64_t i0 = (g_begin + off) << 4;
-                    const bool dense = i0 + 1 < dense_lim;
-                    // indices outside [lo, hi) count as nonzero bytes (never candidates)
-                    const uint32_t y = dense ? 0u : (fold16(w[u]) | (~clip_mask16(i0, lo, hi) & 0xFFFFu));
-                    const bool has = (off < ng) & (dense | ((uint16_t)y != 0xFFFFu));
-                    bits = bits + bits + (uint32_t)has;
-                    wyl[(t * U + u) * 64] = (uint16_t)y;
+                for (int u = 0; u < U; ++u)
+                    w[u] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
+                if (base >= off_steady && base + U * 64 <= ng_steady) {  // steady state: zero-byte test only
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t y = fold16(w[u]);
+                        bits = bits + bits + (uint32_t)((uint16_t)y != 0xFFFFu);
+                        wyl[(WIN - 1 - (t * U + u)) * 64] = (uint16_t)y;
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t off = base + u * 64 + lane;
+                        const uint64_t i0 = (g_begin + off) << 4;
+                        const bool dense = i0 + 1 < dense_lim;
+                        // indices outside [lo, hi) count as nonzero bytes (never candidates)
+                        const uint32_t y = dense ? 0u : (fold16(w[u]) | (~clip_mask16(i0, lo, hi) & 0xFFFFu));
+                        const bool has = (off < ng) & (dense | ((uint16_t)y != 0xFFFFu));
+                        bits = bits + bits + (uint32_t)has;
+                        wyl[(WIN - 1 - (t * U + u)) * 64] = (uint16_t)y;
+                    }
                 }
             }
         }
-        // push the window's marked blocks: each round every lane with bits left pushes its lowest
-        // (prefix by mbcnt, offsets by 24-bit multiplies: stride < 2^24 -- full-rate VALU ops)
+        // push the window's marked blocks: each round every lane with bits left pushes its lowest.
+        // Left-aligned, bit b is slot WIN-1-b: its fold is wy row b, its offset lbase + tab[b].
+        bits <<= WIN - nb;
         const uint32_t lbase = base0 + lane;
         __builtin_amdgcn_wave_barrier();
         for (;;) {
             const bool has = bits != 0;
             const unsigned long long bal = __builtin_amdgcn_ballot_w64(has);
             if (!bal) break;
+            const uint32_t b = __builtin_ctz(bits | (1u << (WIN - 1)));  // (any row for a lane with none)
+            bits &= bits - 1;
+            const uint32_t off = lbase + tab[b];
+            const uint32_t y = wyl[b * 64];
             if (has) {
-                const uint32_t idx = nb - 1 - __builtin_ctz(bits);
-                bits &= bits - 1;
-                const uint32_t off = lbase + __umul24(idx / U, stride) + (idx % U) * 64u;
-                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, qn));
-                q[pos] = (uint64_t)off | ((uint64_t)wyl[idx * 64] << 32);
+                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                q[qn + pos] = (uint64_t)off | ((uint64_t)y << 32);
             }
             qn += (uint32_t)__popcll(bal);
             while (qn >= 64) {  // a resolve may append (blocks with more zero bytes)

@@ -1,7 +1,7 @@
 #!/bin/bash
-# development (round 2): K1 zero-mask queue v2 -- A/B, PMC, element tests, bench
-D=gpurun_out/r02y
-scripts/gpu_run.sh r02y k1ab 120 tools/micro_k1 a :: \
-  k1pmc 120 rocprofv3 --output-format csv --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d $D/k1 -o pmc -- tools/micro_k1 p :: \
-  tests 600 python -u -m pytest tests/test_gpu_elements.py tests/test_gpu_configs.py tests/test_gpu_cpp.py -m gpu -x -q -rfE --timeout 200 --timeout-method thread :: \
-  bench 300 python3 bench.py --steps 50 --warmup 5 --no-secondary --no-cpu-baseline
+# development (round 2): K1 window 20 / grid 3072 / level-1 pre-test
+B="python3 bench.py --steps 200 --warmup 10 --no-secondary --no-cpu-baseline"
+scripts/gpu_run.sh r02ae micro 120 tools/micro_k1 z :: \
+  pytest 300 python -u -m pytest tests/test_gpu_elements.py tests/test_gpu_configs.py tests/test_gpu_stream.py -x -q --timeout 120 --timeout-method thread :: \
+  b1 120 $B :: b2 120 $B :: \
+  tr 200 rocprofv3 --output-format csv --kernel-trace --stats -d gpurun_out/r02ae/tr -o tr -- python3 bench.py --steps 30 --warmup 3 --no-secondary --no-cpu-baseline

@@ -21,7 +21,7 @@ import shutil
 import statistics
 import sys
 
-KERNELS = {"k1": "k1_resolve_publish", "c3": "k2_segmented"}
+KERNELS = {"k1": "k1_last_writer", "c3": "k2_segmented"}  # C2 runs K1 unfused (rsv_runtime.hip)
 
 
 def pmc(dirpath: str, kernel: str) -> dict:

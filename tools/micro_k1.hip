@@ -118,9 +118,21 @@ __global__ __launch_bounds__(256) void k1_var_z(DrawKey dk, uint32_t k, uint64_t
                                                 uint64_t n_groups, unsigned long long* win) {
     __shared__ uint64_t qs[4][128];
     __shared__ uint16_t wys[4][kK1ZWin * 64];
+    __shared__ uint32_t tabs[4][kK1ZWin];
     __shared__ uint64_t cqs[4][kQueue];
     k1_body_z<U>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], wys[threadIdx.x >> 6],
-                       cqs[threadIdx.x >> 6]);
+                 tabs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
+}
+
+template <int U, int WIN>
+__global__ __launch_bounds__(256) void k1_var_zw(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                                 uint64_t n_groups, unsigned long long* win) {
+    __shared__ uint64_t qs[4][128];
+    __shared__ uint16_t wys[4][WIN * 64];
+    __shared__ uint32_t tabs[4][WIN];
+    __shared__ uint64_t cqs[4][kQueue];
+    k1_body_z<U, WIN>(dk, k, lo, hi, g_begin, n_groups, win, qs[threadIdx.x >> 6], wys[threadIdx.x >> 6],
+                      tabs[threadIdx.x >> 6], cqs[threadIdx.x >> 6]);
 }
 
 int main(int argc, char** argv) {
@@ -217,6 +229,22 @@ int main(int argc, char** argv) {
             return 0;
         };
         if (run_once(k1_var<2>, 8192, ref)) return 1;
+        if (argv[1][0] == 'z') {  // window x grid sweep of the zero-mask body (LDS sets the occupancy)
+            const bool fine = argv[1][1] == 'f';  // 'zf': finer grid steps, two passes
+            for (int pass = 0; pass < (fine ? 2 : 1); ++pass)
+                for (int g : fine ? std::vector<int>{2560, 2816, 3072, 3328, 3584, 4096}
+                                  : std::vector<int>{1536, 2048, 2560, 3072, 4096}) {
+                    time_v(k1_var_zw<2, 32>, "k1 z win32", g, 2);
+                    time_v(k1_var_zw<2, 16>, "k1 z win16", g, 2);
+                    time_v(k1_var_zw<2, 24>, "k1 z win24", g, 2);
+                    time_v(k1_var_zw<2, 20>, "k1 z win20", g, 2);
+                }
+            for (auto* kern : {k1_var_zw<2, 16>, k1_var_zw<2, 24>}) {
+                if (run_once(kern, 2048, got)) return 1;
+                printf("  winners identical: %s\n", ref == got ? "yes" : "NO");
+            }
+            return 0;
+        }
         if (argv[1][0] == 'g') {  // grid sweep of the product body
             for (int g : {1536, 2048, 2560, 3072, 3584, 4096, 5120, 6144, 8192, 12288})
                 time_v(k1_var_bits<2>, "k1 bit-mask push", g, 2);
