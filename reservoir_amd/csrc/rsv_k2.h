@@ -69,16 +69,14 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     return x;
 }
 
-// b_i * (i+1) / 2^8 .. with the level-1 word: j = floor(((b << 56) | (L >> 8)) (i + 1) / 2^64)
-__device__ __forceinline__ uint64_t draw_j(uint32_t b, uint64_t L, uint64_t i1, bool small) {
-    const uint64_t U = ((uint64_t)b << 56) | (L >> 8);
-    if (small) {  // i + 1 < 2^32: a 64 x 32 product
+// j = floor(((b << 56) | (L >> 8)) (i + 1) / 2^64), L = Lh:Ll
+__device__ __forceinline__ uint64_t draw_j(uint32_t b, uint32_t Lh, uint32_t Ll, uint64_t i1, bool small) {
+    const uint32_t Uh = __builtin_amdgcn_alignbit(b, Lh, 8), Ul = __builtin_amdgcn_alignbit(Lh, Ll, 8);
+    if (small) {  // i + 1 < 2^32: a 64 x 32 product, the high word of its high half
         const uint32_t x = (uint32_t)i1;
-        const uint64_t lo = (uint64_t)(uint32_t)U * x;
-        const uint64_t hi = (uint64_t)(uint32_t)(U >> 32) * x + (lo >> 32);
-        return hi >> 32;
+        return (uint32_t)(((uint64_t)Uh * x + __umulhi(Ul, x)) >> 32);
     }
-    return __umul64hi(U, i1);
+    return __umul64hi(((uint64_t)Uh << 32) | Ul, i1);
 }
 
 struct Wave {
@@ -105,19 +103,21 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
     const DrawKey dk{W.k0, W.k1, s0, s1};
     const IdxT n_groups = (IdxT)(((uint64_t)len + 15) >> 4);
     uint32_t head = 0, tail = 0;  // FIFO positions (wave-uniform, wrap mod 2^32)
-    uint32_t ring = 0;
-    IdxT gb = (IdxT)(k >> 4);
+    // iterations start at a multiple of 64 blocks (the blocks below k >> 4 are clipped: fill), so
+    // block g sits in stash slot g mod 256 (ring = (g / 64) mod 4) and a FIFO entry is i mod 4096
+    IdxT gb = (IdxT)((k >> 4) & ~63u);
+    uint32_t ring = (k >> 10) & (kRing - 1);
 
-    // resolve FIFO entries [head, head + nvalid) (nvalid <= 64), one per lane; (last_gb, last_ring)
-    // = the most recently stashed iteration, so an entry's age is (last_ring - r) & 3
-    auto resolve_round = [&](uint32_t nvalid, IdxT last_gb, uint32_t last_ring) {
+    // resolve FIFO entries [head, head + nvalid) (nvalid <= 64), one per lane; last_gb = the most
+    // recently stashed iteration: every pending index lies in [16 (last_gb - 192), + 4096)
+    auto resolve_round = [&](uint32_t nvalid, IdxT last_gb) {
         __builtin_amdgcn_wave_barrier();
         const bool valid = lane < nvalid;
         const uint32_t ent = valid ? W.q[(head + lane) & (kQCap - 1)] : 0u;
-        const uint32_t r = ent >> 10, e = ent & 15u;
-        const u32x4 w = W.stash[ent >> 4];  // ring slot * 64 + lane
-        const IdxT gbr = last_gb - (IdxT)64 * ((last_ring - r) & (kRing - 1));
-        const IdxT i = (gbr << 4) + (ent & 0x3FFu);  // ((gbr + ln) << 4) + e
+        const uint32_t e = ent & 15u;
+        const u32x4 w = W.stash[ent >> 4];  // block g mod 256
+        const IdxT wlo = (last_gb << 4) - (IdxT)3072;
+        const IdxT i = wlo + (IdxT)((ent - (uint32_t)wlo) & 4095u);
         const uint32_t b = level0_byte(w, e);
         const IdxT g1 = i >> 1;
         u32x4 w1;
@@ -128,8 +128,11 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
         } else {
             w1 = philox4x32_10((uint32_t)g1, (uint32_t)((uint64_t)g1 >> 32) | kDomainLevel1, s0, s1, W.k0, W.k1);
         }
-        const uint64_t L = (i & 1) ? (((uint64_t)w1.z << 32) | w1.w) : (((uint64_t)w1.x << 32) | w1.y);
-        const uint64_t j = draw_j(b, L, (uint64_t)i + 1, SMALL);
+        // all four words, then one select per half (else the compiler selects the last round's
+        // operands instead: 7 v_cndmask for the one saved product)
+        asm volatile("" : "+v"(w1.x), "+v"(w1.y), "+v"(w1.z), "+v"(w1.w));
+        const bool odd = (i & 1) != 0;
+        const uint64_t j = draw_j(b, odd ? w1.z : w1.x, odd ? w1.w : w1.y, (uint64_t)i + 1, SMALL);
         if (valid && j < k) atomicMax(&tab[(uint32_t)j], i);
         head += nvalid;
         __builtin_amdgcn_wave_barrier();
@@ -138,7 +141,7 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
     for (; gb < n_groups; gb += 64, ring = (ring + 1) & (kRing - 1)) {
         // the oldest pending candidate still refers to the ring slot about to be overwritten
         if (tail != head && ((uint32_t)__builtin_amdgcn_readfirstlane((int)W.q[head & (kQCap - 1)]) >> 10) == ring) {
-            while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head), gb - 64, ring - 1);
+            while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head), gb - 64);
         }
         const IdxT g = gb + lane;
         const bool valid = g < n_groups;
@@ -148,15 +151,17 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
         const uint64_t i0 = (uint64_t)g << 4;
         const uint32_t T = g < kLut ? (uint32_t)W.lut[(uint32_t)g] : block_threshold(i0, W.dense_lim);
         uint32_t mask = valid ? mask_for(w, T) : 0u;
-        if (__builtin_amdgcn_readfirstlane((int)(((uint64_t)gb << 4) < k || (((uint64_t)gb + 64) << 4) > (uint64_t)len)))
-            mask &= clip16(i0, k, (uint64_t)len);
+        bool clip;  // wave-uniform; 32-bit compares for SMALL (scalar: no 64-bit s_cmp_lt)
+        if constexpr (SMALL) clip = ((uint32_t)gb << 4) < k || (((uint32_t)gb + 64) << 4) > (uint32_t)len;
+        else clip = ((uint64_t)gb << 4) < k || (((uint64_t)gb + 64) << 4) > (uint64_t)len;
+        if (clip) mask &= clip16(i0, k, (uint64_t)len);
         W.stash[ring * 64 + lane] = w;
         // FIFO offsets: one wave prefix sum of the per-lane candidate counts
         const uint32_t cnt = (uint32_t)__popc(mask);
         const uint32_t incl = wave_incl_scan(cnt);
         const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         uint32_t pos = tail + incl - cnt;
-        const uint32_t tag = (ring << 10) | (lane << 4);
+        const uint32_t tag = (ring << 10) | (lane << 4);  // = (g mod 256) << 4
         while (mask) {
             const uint32_t e = __builtin_ctz(mask);
             mask &= mask - 1;
@@ -165,9 +170,9 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
         }
         tail += tot;
         if constexpr ((V & 8) != 0) head = tail;  // variant: candidates dropped (cost probe)
-        while (tail - head >= 64) resolve_round(64u, gb, ring);
+        while (tail - head >= 64) resolve_round(64u, gb);
     }
-    while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head), gb - 64, ring - 1);
+    while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head), gb - 64);
     __builtin_amdgcn_wave_barrier();
     if constexpr (DEFER) {
         KeyT v = 0;

@@ -1,7 +1,5 @@
 #!/bin/bash
-# development (round 2): K1 window 20 / grid 3072 / level-1 pre-test
-B="python3 bench.py --steps 200 --warmup 10 --no-secondary --no-cpu-baseline"
-scripts/gpu_run.sh r02ae micro 120 tools/micro_k1 z :: \
-  pytest 300 python -u -m pytest tests/test_gpu_elements.py tests/test_gpu_configs.py tests/test_gpu_stream.py -x -q --timeout 120 --timeout-method thread :: \
-  b1 120 $B :: b2 120 $B :: \
-  tr 200 rocprofv3 --output-format csv --kernel-trace --stats -d gpurun_out/r02ae/tr -o tr -- python3 bench.py --steps 30 --warmup 3 --no-secondary --no-cpu-baseline
+# development (round 2): K2 compact FIFO entries / select / draw_j
+scripts/gpu_run.sh r02ag pytest 300 python -u -m pytest tests/test_gpu_segmented.py tests/test_gpu_configs.py -x -q --timeout 120 --timeout-method thread :: \
+  c3a 200 python3 tools/bench_paths.py --only c3 :: c3b 200 python3 tools/bench_paths.py --only c3 :: \
+  tr 200 rocprofv3 --output-format csv --kernel-trace --stats -d gpurun_out/r02ag/tr -o tr -- python3 tools/bench_paths.py --only c3

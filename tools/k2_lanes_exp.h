@@ -233,7 +233,7 @@ __device__ __forceinline__ void k2_lanes(unsigned char* wl, const KeyT* __restri
         if (live) {
             const u32x4 w1 = level1_lane(li >> 1, s1, c, k0, k1);
             const uint64_t L = (li & 1) ? (((uint64_t)w1.z << 32) | w1.w) : (((uint64_t)w1.x << 32) | w1.y);
-            const uint32_t j = (uint32_t)draw_j(lb, L, (uint64_t)li + 1, true);
+            const uint32_t j = (uint32_t)draw_j(lb, (uint32_t)(L >> 32), (uint32_t)L, (uint64_t)li + 1, true);
             if (j < k && !((filled >> j) & 1ull)) {  // the first hit of the backward scan wins
                 filled |= 1ull << j;
                 orow[j] = (KeyT)li;

@@ -50,11 +50,12 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     std::vector<int64_t> ref(S * k), got(S * k);
+    size_t lds_run = lds;
     auto run = [&](auto kern, const char* name, bool check) -> int {
         std::vector<float> ts;
         for (int rep = 0; rep < 7; ++rep) {
             CK(hipEventRecord(e0));
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * k2::kWaves), lds, 0, (const int64_t*)keys,
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * k2::kWaves), lds_run, 0, (const int64_t*)keys,
                                (const int64_t*)offs, S, k, 1u, 0u, 0ull, out, cnt);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
@@ -72,6 +73,17 @@ int main(int argc, char** argv) {
     };
     if (run(k2::k2_segmented<int64_t, 0>, "0 wave-per-stream", false)) return 1;
     CK(hipMemcpy(ref.data(), out, S * k * 8, hipMemcpyDeviceToHost));
+    if (argc > 1 && argv[1][0] == 'o') {  // occupancy sensitivity: the product with its LDS padded
+        CK(hipFuncSetAttribute((const void*)k2::k2_segmented<int64_t, 0>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        for (size_t pad : {lds, (size_t)(160 * 1024 / 3), (size_t)(160 * 1024 / 2)}) {
+            lds_run = pad;
+            char name[64];
+            snprintf(name, sizeof name, "0 product, %zu B LDS per workgroup", pad);
+            if (run(k2::k2_segmented<int64_t, 0>, name, true)) return 1;
+        }
+        return 0;
+    }
     {  // the lane-per-stream form (k2_segmented2)
         const size_t lds2 = k2::lds_bytes2(k);
         const unsigned grid2 = (unsigned)((S + 64 * k2::kWaves2 - 1) / (64 * k2::kWaves2));
