@@ -11,16 +11,20 @@ namespace k2 {
 
 constexpr int kWaves = 4;          // waves per workgroup
 constexpr uint32_t kRing = 4;      // level-0 iterations whose block words stay addressable
-constexpr uint32_t kQCap = 2048;   // FIFO entries: < 64 pending + <= 64 x 16 appended per iteration
+constexpr uint32_t kQCap = 512;    // FIFO entries (an iteration that would overflow takes ballot rounds)
 constexpr uint32_t kStashBytes = kRing * 64 * 16;
 constexpr uint32_t kQueueBytes = kQCap * 2;
 constexpr uint32_t kLut = 1024;    // blocks (16 indices each) whose threshold T is tabulated per workgroup
 constexpr uint32_t kLutBytes = kLut * 2;
 constexpr int64_t kSmallLen = 1ll << 27;  // streams shorter than this use 32-bit index arithmetic
 
+// FIFO entries of variant V (tools/micro_k2: V & 128 = the 2048-entry FIFO of r02 up to 696f99e,
+// which held any iteration: 4 workgroups per CU by LDS instead of 6)
+__host__ __device__ constexpr uint32_t qcap_of(int V) { return (V & 128) ? 2048u : kQCap; }
+
 // bytes of dynamic LDS per workgroup: T table + per wave (stash | FIFO | k-slot table)
-__host__ __device__ inline size_t lds_bytes(uint32_t k) {
-    return kLutBytes + (size_t)kWaves * (kStashBytes + kQueueBytes + (size_t)k * 8);
+__host__ __device__ inline size_t lds_bytes(uint32_t k, int V = 0) {
+    return kLutBytes + (size_t)kWaves * (kStashBytes + qcap_of(V) * 2 + (size_t)k * 8);
 }
 
 // T = ceil(256 k / (i0 + 1)), the block threshold of the dense region (T > 255: every byte is a
@@ -45,6 +49,15 @@ __device__ __forceinline__ uint32_t lt_mask16_borrow(const u32x4& w, uint32_t T)
         br = __builtin_amdgcn_bitop3_b32(plane, br, mm, 0xD4);
     }
     return ~br & 0xFFFFu;
+}
+
+// the level-0 bytes of indices e and e + 1 of a block (e even), as level0_byte twice
+__device__ __forceinline__ void level0_byte_pair(const u32x4& w, uint32_t e, uint32_t& b0, uint32_t& b1) {
+    // bits e, e+1 of the planes 2q (low half) and 2q+1 (high half) of word q, at 2q, 2q+1 / 16+2q, 17+2q
+    const uint32_t u = ((w.x >> e) & 0x30003u) | (((w.y >> e) & 0x30003u) << 2) |
+                       (((w.z >> e) & 0x30003u) << 4) | (((w.w >> e) & 0x30003u) << 6);
+    b0 = (u & 0x55u) | ((u >> 15) & 0xAAu);
+    b1 = ((u >> 1) & 0x55u) | ((u >> 16) & 0xAAu);
 }
 
 __device__ __forceinline__ uint32_t mask_for(const u32x4& w, uint32_t T) {
@@ -86,6 +99,7 @@ struct Wave {
     const uint16_t* lut;
     uint32_t lane, k, k0, k1;
     uint64_t dense_lim;
+    uint32_t fifo_cap;  // bulk appends while pending + new <= fifo_cap (<= the FIFO size; tests lower it)
 };
 
 // One stream on one wave.  SMALL: n < 2^27 -- 32-bit indices, u32 winner table, and Philox counters
@@ -96,6 +110,7 @@ template <typename KeyT, int V, bool SMALL, bool DEFER>
 __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict__ keys, int64_t off, int64_t len,
                                           uint64_t stream, KeyT* __restrict__ o) {
     using IdxT = typename std::conditional<SMALL, uint32_t, uint64_t>::type;
+    constexpr uint32_t QC = qcap_of(V);
     const uint32_t lane = W.lane, k = W.k;
     IdxT* tab = (IdxT*)W.tab;
     for (uint32_t j = lane; j < k; j += 64) tab[j] = 0;
@@ -113,7 +128,7 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
     auto resolve_round = [&](uint32_t nvalid, IdxT last_gb) {
         __builtin_amdgcn_wave_barrier();
         const bool valid = lane < nvalid;
-        const uint32_t ent = valid ? W.q[(head + lane) & (kQCap - 1)] : 0u;
+        const uint32_t ent = valid ? W.q[(head + lane) & (QC - 1)] : 0u;
         const uint32_t e = ent & 15u;
         const u32x4 w = W.stash[ent >> 4];  // block g mod 256
         const IdxT wlo = (last_gb << 4) - (IdxT)3072;
@@ -138,9 +153,15 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
         __builtin_amdgcn_wave_barrier();
     };
 
+    // The dense head [k, hend), hend = min(len, HM k): candidate density >= 256 / HM %, so it skips
+    // the FIFO -- each lane takes a PAIR of indices (one level-1 Philox serves both) straight from
+    // the stashed level-0 block; the FIFO path covers [hend, len).
+    constexpr uint32_t HM = (V & 32) ? 2u : (V & 64) ? 1u : 4u;
+    const IdxT hend = (IdxT)std::min<uint64_t>((uint64_t)len, (uint64_t)HM * k);
+    const IdxT flo = std::max<IdxT>((IdxT)k, hend);
     for (; gb < n_groups; gb += 64, ring = (ring + 1) & (kRing - 1)) {
         // the oldest pending candidate still refers to the ring slot about to be overwritten
-        if (tail != head && ((uint32_t)__builtin_amdgcn_readfirstlane((int)W.q[head & (kQCap - 1)]) >> 10) == ring) {
+        if (tail != head && ((uint32_t)__builtin_amdgcn_readfirstlane((int)W.q[head & (QC - 1)]) >> 10) == ring) {
             while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head), gb - 64);
         }
         const IdxT g = gb + lane;
@@ -152,23 +173,63 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
         const uint32_t T = g < kLut ? (uint32_t)W.lut[(uint32_t)g] : block_threshold(i0, W.dense_lim);
         uint32_t mask = valid ? mask_for(w, T) : 0u;
         bool clip;  // wave-uniform; 32-bit compares for SMALL (scalar: no 64-bit s_cmp_lt)
-        if constexpr (SMALL) clip = ((uint32_t)gb << 4) < k || (((uint32_t)gb + 64) << 4) > (uint32_t)len;
-        else clip = ((uint64_t)gb << 4) < k || (((uint64_t)gb + 64) << 4) > (uint64_t)len;
-        if (clip) mask &= clip16(i0, k, (uint64_t)len);
+        if constexpr (SMALL) clip = ((uint32_t)gb << 4) < (uint32_t)flo || (((uint32_t)gb + 64) << 4) > (uint32_t)len;
+        else clip = ((uint64_t)gb << 4) < (uint64_t)flo || (((uint64_t)gb + 64) << 4) > (uint64_t)len;
+        if (clip) mask &= clip16(i0, (uint64_t)flo, (uint64_t)len);
         W.stash[ring * 64 + lane] = w;
+        if (((uint64_t)gb << 4) < (uint64_t)hend) {  // this iteration holds head indices (uniform)
+            __builtin_amdgcn_wave_barrier();
+            const IdxT ia = std::max<IdxT>((IdxT)k & ~(IdxT)1, gb << 4);
+            const IdxT ib = std::min<IdxT>(hend, (gb + 64) << 4);
+            for (IdxT p0 = ia; p0 < ib; p0 += 128) {
+                const IdxT i = p0 + 2 * lane;  // even
+                const u32x4 wl = W.stash[(uint32_t)(i >> 4) & 255u];
+                uint32_t b0, b1;
+                level0_byte_pair(wl, (uint32_t)i & 15u, b0, b1);
+                const IdxT g1 = i >> 1;
+                u32x4 w1;
+                if constexpr (SMALL) w1 = philox4x32_10_uniform_hi((uint32_t)g1, kDomainLevel1, s0, s1, W.k0, W.k1);
+                else w1 = philox4x32_10((uint32_t)g1, (uint32_t)((uint64_t)g1 >> 32) | kDomainLevel1, s0, s1, W.k0, W.k1);
+                asm volatile("" : "+v"(w1.x), "+v"(w1.y), "+v"(w1.z), "+v"(w1.w));
+                const uint64_t j0 = draw_j(b0, w1.x, w1.y, (uint64_t)i + 1, SMALL);
+                const uint64_t j1 = draw_j(b1, w1.z, w1.w, (uint64_t)i + 2, SMALL);
+                if (i < ib && i >= (IdxT)k && j0 < k) atomicMax(&tab[(uint32_t)j0], i);
+                if (i + 1 < ib && i + 1 >= (IdxT)k && j1 < k) atomicMax(&tab[(uint32_t)j1], i + 1);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
         // FIFO offsets: one wave prefix sum of the per-lane candidate counts
         const uint32_t cnt = (uint32_t)__popc(mask);
         const uint32_t incl = wave_incl_scan(cnt);
         const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        uint32_t pos = tail + incl - cnt;
         const uint32_t tag = (ring << 10) | (lane << 4);  // = (g mod 256) << 4
-        while (mask) {
-            const uint32_t e = __builtin_ctz(mask);
-            mask &= mask - 1;
-            W.q[pos & (kQCap - 1)] = (uint16_t)(tag | e);
-            ++pos;
+        if (tail - head + tot <= W.fifo_cap) {  // uniform: the whole iteration fits
+            uint32_t pos = tail + incl - cnt;
+            while (mask) {
+                const uint32_t e = __builtin_ctz(mask);
+                mask &= mask - 1;
+                W.q[pos & (QC - 1)] = (uint16_t)(tag | e);
+                ++pos;
+            }
+            tail += tot;
+        } else {  // an iteration denser than the FIFO (never at random draws beyond the dense
+                  // head: ~4 candidates per block): one candidate per lane per round, resolved
+                  // as 64 wait, so at most 127 are ever pending
+            for (;;) {
+                const bool has = mask != 0;
+                const unsigned long long bal = __builtin_amdgcn_ballot_w64(has);
+                if (!bal) break;
+                if (has) {
+                    const uint32_t e = __builtin_ctz(mask);
+                    mask &= mask - 1;
+                    const uint32_t pos = tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    W.q[pos & (QC - 1)] = (uint16_t)(tag | e);
+                }
+                tail += (uint32_t)__popcll(bal);
+                if (tail - head >= 64) resolve_round(64u, gb);
+            }
         }
-        tail += tot;
         if constexpr ((V & 8) != 0) head = tail;  // variant: candidates dropped (cost probe)
         while (tail - head >= 64) resolve_round(64u, gb);
     }
@@ -199,7 +260,8 @@ template <typename KeyT, int V = 0>
 __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restrict__ keys,
                                                             const int64_t* __restrict__ offsets, int64_t S,
                                                             uint32_t k, uint32_t k0, uint32_t k1, uint64_t stream_base,
-                                                            KeyT* __restrict__ out, int64_t* __restrict__ counts) {
+                                                            KeyT* __restrict__ out, int64_t* __restrict__ counts,
+                                                            uint32_t fifo_cap = qcap_of(V)) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     uint16_t* lut = (uint16_t*)lds;
     const uint64_t dense_lim = 256ull * k;
@@ -207,9 +269,10 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // per wave: stash [kRing][64] x 16 B | FIFO kQCap x u16 | last-writer table k x (u32 | u64)
-    unsigned char* base = lds + kLutBytes + (size_t)wave * (kStashBytes + kQueueBytes + (size_t)k * 8);
-    const Wave W{(u32x4*)base, (uint16_t*)(base + kStashBytes), base + kStashBytes + kQueueBytes, lut, lane, k,
-                 k0, k1, dense_lim};
+    constexpr size_t qbytes = qcap_of(V) * 2;
+    unsigned char* base = lds + kLutBytes + (size_t)wave * (kStashBytes + qbytes + (size_t)k * 8);
+    const Wave W{(u32x4*)base, (uint16_t*)(base + kStashBytes), base + kStashBytes + qbytes, lut, lane, k,
+                 k0, k1, dense_lim, std::min<uint32_t>(std::max<uint32_t>(fifo_cap, 128u), qcap_of(V))};
     const int64_t wave_stride = (int64_t)gridDim.x * kWaves;
     int64_t s = (int64_t)blockIdx.x * kWaves + wave;
     int64_t off = 0, end = 0;

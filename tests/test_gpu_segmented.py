@@ -27,6 +27,28 @@ def test_ragged_parity(cuda, oracle, k):
     assert np.array_equal(out.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("k", [64, 256, 1000])
+def test_fifo_overflow_rounds(cuda, oracle, monkeypatch, k):
+    """An iteration with more candidates than the FIFO takes (RSV_K2_FIFO_CAP lowers the bulk-append
+    limit to 128; at k = 256 an iteration past the dense head holds ~177) goes through the ballot-
+    round path of rsv_k2.h: same reservoirs as the oracle."""
+    import torch
+
+    from reservoir_amd import batch
+
+    monkeypatch.setenv("RSV_K2_FIFO_CAP", "128")
+    rng = np.random.default_rng(500 + k)
+    lens = rng.integers(0, 20_000, size=200)
+    lens[:4] = [k, k + 1, 4096, 19_999]
+    offs = np.r_[0, np.cumsum(lens)].astype(np.int64)
+    keys = oracle.splitmix_keys(11 * k, int(offs[-1]))
+    want, wcnt = oracle.algo_r_segmented(31, 77, k, keys, offs)
+    out, cnt = batch.sample_segmented(torch.from_numpy(keys).to(cuda), torch.from_numpy(offs).to(cuda), k,
+                                      seed=31, stream_base=77)
+    assert np.array_equal(cnt.cpu().numpy(), wcnt)
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("k", [2, 7, 64])
 def test_long_streams_sparse_region(cuda, oracle, k):
     """Streams far longer than 256k: the dense head and the sparse tail (zero level-0 bytes only)."""

@@ -356,7 +356,7 @@ __global__ __launch_bounds__(64 * kWaves2) void k2_segmented2(const KeyT* __rest
                            (uint32_t)(st_first >> 32), k, k0, k1, n_st, out + s_first * (int64_t)k);
         } else {
             const Wave W{(u32x4*)wl, (uint16_t*)(wl + kStashBytes), wl + kStashBytes + kQueueBytes, lut, lane, k,
-                         k0, k1, dense_lim};
+                         k0, k1, dense_lim, kQCap};
             for (int64_t t = 0; t < n_st; ++t) {
                 const int64_t ot = offsets[s_first + t];
                 const int64_t lt = offsets[s_first + t + 1] - ot;

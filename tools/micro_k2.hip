@@ -56,7 +56,7 @@ int main(int argc, char** argv) {
         for (int rep = 0; rep < 7; ++rep) {
             CK(hipEventRecord(e0));
             hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * k2::kWaves), lds_run, 0, (const int64_t*)keys,
-                               (const int64_t*)offs, S, k, 1u, 0u, 0ull, out, cnt);
+                               (const int64_t*)offs, S, k, 1u, 0u, 0ull, out, cnt, 0xFFFFFFFFu);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms;
@@ -110,6 +110,19 @@ int main(int argc, char** argv) {
     }
     if (argc > 1 && argv[1][0] == 'l') return 0;  // the two product forms only
     if (argc > 1 && argv[1][0] == 'p') return 0;  // one variant only (rocprofv3 --pmc passes)
+    if (argc > 1 && argv[1][0] == 'q') {  // occupancy: the 2048-entry FIFO (4 workgroups per CU)
+        lds_run = k2::lds_bytes(k, 128);
+        if (run(k2::k2_segmented<int64_t, 128>, "128 FIFO 2048 entries", true)) return 1;
+        lds_run = lds;
+        if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'h') {  // dense-head multiplier: 4 (product), 2, none
+        if (run(k2::k2_segmented<int64_t, 32>, "32 head [k, 2k)", true)) return 1;
+        if (run(k2::k2_segmented<int64_t, 64>, "64 no head (all through the FIFO)", true)) return 1;
+        if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+        return 0;
+    }
     if (run(k2::k2_segmented<int64_t, 1>, "1 no gather", false)) return 1;
     if (run(k2::k2_segmented<int64_t, 2>, "2 no level-1 philox", false)) return 1;
     if (run(k2::k2_segmented<int64_t, 16>, "16 gather stored at once (no deferral)", true)) return 1;
