@@ -22,9 +22,12 @@ constexpr int64_t kSmallLen = 1ll << 27;  // streams shorter than this use 32-bi
 // which held any iteration: 4 workgroups per CU by LDS instead of 6)
 __host__ __device__ constexpr uint32_t qcap_of(int V) { return (V & 128) ? 2048u : kQCap; }
 
+// stash ring of variant V (V & 256: 2 iterations, occupancy probe)
+__host__ __device__ constexpr uint32_t ring_of(int V) { return (V & 256) ? 2u : kRing; }
+
 // bytes of dynamic LDS per workgroup: T table + per wave (stash | FIFO | k-slot table)
 __host__ __device__ inline size_t lds_bytes(uint32_t k, int V = 0) {
-    return kLutBytes + (size_t)kWaves * (kStashBytes + qcap_of(V) * 2 + (size_t)k * 8);
+    return kLutBytes + (size_t)kWaves * (ring_of(V) * 64 * 16 + qcap_of(V) * 2 + (size_t)k * 8);
 }
 
 // T = ceil(256 k / (i0 + 1)), the block threshold of the dense region (T > 255: every byte is a
@@ -110,7 +113,7 @@ template <typename KeyT, int V, bool SMALL, bool DEFER>
 __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict__ keys, int64_t off, int64_t len,
                                           uint64_t stream, KeyT* __restrict__ o) {
     using IdxT = typename std::conditional<SMALL, uint32_t, uint64_t>::type;
-    constexpr uint32_t QC = qcap_of(V);
+    constexpr uint32_t QC = qcap_of(V), RG = ring_of(V), WIN = RG * 1024;  // WIN: indices in the ring
     const uint32_t lane = W.lane, k = W.k;
     IdxT* tab = (IdxT*)W.tab;
     for (uint32_t j = lane; j < k; j += 64) tab[j] = 0;
@@ -121,7 +124,7 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
     // iterations start at a multiple of 64 blocks (the blocks below k >> 4 are clipped: fill), so
     // block g sits in stash slot g mod 256 (ring = (g / 64) mod 4) and a FIFO entry is i mod 4096
     IdxT gb = (IdxT)((k >> 4) & ~63u);
-    uint32_t ring = (k >> 10) & (kRing - 1);
+    uint32_t ring = (k >> 10) & (RG - 1);
 
     // resolve FIFO entries [head, head + nvalid) (nvalid <= 64), one per lane; last_gb = the most
     // recently stashed iteration: every pending index lies in [16 (last_gb - 192), + 4096)
@@ -131,8 +134,8 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
         const uint32_t ent = valid ? W.q[(head + lane) & (QC - 1)] : 0u;
         const uint32_t e = ent & 15u;
         const u32x4 w = W.stash[ent >> 4];  // block g mod 256
-        const IdxT wlo = (last_gb << 4) - (IdxT)3072;
-        const IdxT i = wlo + (IdxT)((ent - (uint32_t)wlo) & 4095u);
+        const IdxT wlo = (last_gb << 4) - (IdxT)(WIN - 1024);
+        const IdxT i = wlo + (IdxT)((ent - (uint32_t)wlo) & (WIN - 1));
         const uint32_t b = level0_byte(w, e);
         const IdxT g1 = i >> 1;
         u32x4 w1;
@@ -159,7 +162,7 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
     constexpr uint32_t HM = (V & 32) ? 2u : (V & 64) ? 1u : 4u;
     const IdxT hend = (IdxT)std::min<uint64_t>((uint64_t)len, (uint64_t)HM * k);
     const IdxT flo = std::max<IdxT>((IdxT)k, hend);
-    for (; gb < n_groups; gb += 64, ring = (ring + 1) & (kRing - 1)) {
+    for (; gb < n_groups; gb += 64, ring = (ring + 1) & (RG - 1)) {
         // the oldest pending candidate still refers to the ring slot about to be overwritten
         if (tail != head && ((uint32_t)__builtin_amdgcn_readfirstlane((int)W.q[head & (QC - 1)]) >> 10) == ring) {
             while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head), gb - 64);
@@ -183,7 +186,7 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
             const IdxT ib = std::min<IdxT>(hend, (gb + 64) << 4);
             for (IdxT p0 = ia; p0 < ib; p0 += 128) {
                 const IdxT i = p0 + 2 * lane;  // even
-                const u32x4 wl = W.stash[(uint32_t)(i >> 4) & 255u];
+                const u32x4 wl = W.stash[(uint32_t)(i >> 4) & (RG * 64 - 1)];
                 uint32_t b0, b1;
                 level0_byte_pair(wl, (uint32_t)i & 15u, b0, b1);
                 const IdxT g1 = i >> 1;
@@ -269,9 +272,9 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // per wave: stash [kRing][64] x 16 B | FIFO kQCap x u16 | last-writer table k x (u32 | u64)
-    constexpr size_t qbytes = qcap_of(V) * 2;
-    unsigned char* base = lds + kLutBytes + (size_t)wave * (kStashBytes + qbytes + (size_t)k * 8);
-    const Wave W{(u32x4*)base, (uint16_t*)(base + kStashBytes), base + kStashBytes + qbytes, lut, lane, k,
+    constexpr size_t qbytes = qcap_of(V) * 2, sbytes = ring_of(V) * 64 * 16;
+    unsigned char* base = lds + kLutBytes + (size_t)wave * (sbytes + qbytes + (size_t)k * 8);
+    const Wave W{(u32x4*)base, (uint16_t*)(base + sbytes), base + sbytes + qbytes, lut, lane, k,
                  k0, k1, dense_lim, std::min<uint32_t>(std::max<uint32_t>(fifo_cap, 128u), qcap_of(V))};
     const int64_t wave_stride = (int64_t)gridDim.x * kWaves;
     int64_t s = (int64_t)blockIdx.x * kWaves + wave;

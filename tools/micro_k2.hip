@@ -113,6 +113,8 @@ int main(int argc, char** argv) {
     if (argc > 1 && argv[1][0] == 'q') {  // occupancy: the 2048-entry FIFO (4 workgroups per CU)
         lds_run = k2::lds_bytes(k, 128);
         if (run(k2::k2_segmented<int64_t, 128>, "128 FIFO 2048 entries", true)) return 1;
+        lds_run = k2::lds_bytes(k, 256);
+        if (run(k2::k2_segmented<int64_t, 256>, "256 stash ring of 2 iterations", true)) return 1;
         lds_run = lds;
         if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
         return 0;
