@@ -746,6 +746,8 @@ __global__ __launch_bounds__(kBlock) void sched_filter(const KeyT* __restrict__ 
                                                        int32_t log_bmax, int64_t* __restrict__ bak_h,
                                                        KeyT* __restrict__ bak_k) {
     __shared__ int64_t sb[kMaxRanges + 1], stt[kMaxRanges];
+    // (the plan is NOT a kernel argument: 8192 workgroups reading ~1.6 KB of kernarg memory each
+    // made the pass 709 -> 769 us; a device copy, read through L2, costs one small copy dispatch)
     if (blockIdx.x == 0) {  // the merge's tie word and group sums (bucket_sort adds, bucket_emit sets)
         if (threadIdx.x == 0) ctl[5] = 0;
         zero_bucket_groups(ctl, log_bmax);
@@ -1262,8 +1264,8 @@ void distinct_destroy(DistinctState* d) {
     pool_host_free(d->ph);
     pool_host_free(d->pk);
     pool_host_free(d->pp);
-    pool_host_free(d->sstage);
     pool_host_free(d->shc);
+    pool_host_free(d->sstage);
     delete d;
 }
 
@@ -1271,7 +1273,8 @@ int64_t distinct_size(const DistinctState* d) { return d->m; }
 const void* distinct_keys_dev(const DistinctState* d) { return d->set_k; }
 
 void distinct_spec_target(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t* gen_counter) {
-    if (d->ordered || d->log_bmax < 0) return;  // set mode with the bucketed merge only
+    // the bucketed merge only: set mode behind ctl_publish, ordered mode behind the scheduled pass
+    if (d->log_bmax < 0) return;
     d->spec_dst = dst_host_dev;
     d->spec_flag = flag_dev;
     d->spec_gen_ctr = gen_counter;
@@ -1610,7 +1613,10 @@ template <typename KeyT>
 static hipError_t launch_filter_idx(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
                                     int64_t tinc, int64_t* out_h, KeyT* out_k, uint32_t* out_i, int64_t cap,
                                     hipStream_t st) {
-    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 32 + 1), 1), 256 * 32);
+    // ~8 keys per thread (one 1024-key tile per two waves) up to 8192 workgroups: a short chunk
+    // where every key is a candidate (the heap filling) would otherwise run on a few waves
+    // (132k keys: 17 workgroups, 18 us)
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 8 + 1), 1), 256 * 32);
 #define RSV_FILTER_IDX(H)                                                                                       \
     hipLaunchKernelGGL((k3_filter<KeyT, H, true>), dim3(grid), dim3(kBlock), 0, st, keys, hashes, n, d->r0,     \
                        d->r1, tinc, out_h, out_k, d->counter, cap, out_i)
@@ -1745,15 +1751,17 @@ static hipError_t sched_ensure(DistinctState* d, int32_t lb, hipStream_t st) {
         if ((e = pool_device_alloc(&d->bak_k, (size_t)d->k * d->kw))) return e;
     }
     if (lb > d->log_bmax_s) {
+        // the old area may still be read by queued work: wait before it goes back to the pool
+        if (d->sctl && (e = hipStreamSynchronize(st))) return e;
         for (void* p : {(void*)d->sctl, (void*)d->sbh, d->sbk, (void*)d->sbi}) pool_device_free(p);
         d->sctl = nullptr;
         d->sbh = nullptr;
         d->sbk = nullptr;
         d->sbi = nullptr;
         d->log_bmax_s = -1;
-        if ((e = hipStreamSynchronize(st))) return e;  // the old area may still be read by queued work
         const size_t B = (size_t)1 << lb;
-        const size_t ctl_bytes = kCtlWords * 8 + (kCountStride + 1) * 4 * B + 4 * ((B >> 4) + 1);
+        // rounded to 256 B: one aligned fill dispatch (an unaligned tail costs a second one)
+        const size_t ctl_bytes = (kCtlWords * 8 + (kCountStride + 1) * 4 * B + 4 * ((B >> 4) + 1) + 255) & ~(size_t)255;
         if ((e = pool_device_alloc((void**)&d->sctl, ctl_bytes))) return e;
         if ((e = hipMemsetAsync(d->sctl, 0, ctl_bytes, st))) return e;  // counts, counter: re-armed after each pass
         if ((e = pool_device_alloc((void**)&d->sbh, B * kBucketCap * 8))) return e;
@@ -1762,6 +1770,21 @@ static hipError_t sched_ensure(DistinctState* d, int32_t lb, hipStream_t st) {
         d->log_bmax_s = lb;
     }
     return hipSuccess;
+}
+
+// The scheduled pass's buffers (and their zeroing) for a batch of n keys, queued ahead of the batch's
+// first chunk so that the pass itself starts without a host round trip for them.  Sized from an
+// estimate of the pass's candidates (sched_sample's c_pred with D0 = k and distinct elements arriving
+// at >= 3/4 of the positions); a pass that needs more reallocates in sched_ensure.
+template <typename KeyT>
+static hipError_t sched_prepare(DistinctState* d, int64_t n, hipStream_t st) {
+    const double k = (double)d->k;
+    const double c_est = d->sched_beta * k / 0.75 * std::log1p(0.75 * (double)n / k);
+    const int64_t cap = std::min<int64_t>((int64_t)(1.5 * c_est) + 4 * 4096, ((int64_t)1 << 31) - 1);
+    int32_t lb = 1;
+    while (((int64_t)1 << (lb + 6)) < d->k + cap) ++lb;
+    if (((int64_t)kBucketCap * 8 + 20) << lb > ((int64_t)1 << 30)) return hipSuccess;
+    return sched_ensure<KeyT>(d, lb, st);
 }
 
 // The scheduled pass over keys[0, n) of a batch, heap full (see SchedDev).  Bounds: with D
@@ -1861,7 +1884,6 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
     STRY(ensure_log(d, d->log_n + cap, st));
     STRY(sched_ensure<KeyT>(d, lb, st));
     std::memcpy(d->sstage, sp, sizeof(SchedDev));  // the previous pass has read its copy (we waited on it)
-
     const size_t kw = sizeof(KeyT);
     STRY(hipMemcpyAsync(d->sdev, d->sstage, sizeof(SchedDev), hipMemcpyHostToDevice, st));
     const unsigned B = sp->B;
@@ -1871,7 +1893,7 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
         const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 32 + 1), 1), 256 * 32);
         KeyT* lk = (KeyT*)d->log_k + d->log_n;
 #define RSV_SCHED_FILTER(H)                                                                                             \
-    hipLaunchKernelGGL((sched_filter<KeyT, H>), dim3(grid), dim3(kBlock), 0, st, keys, hashes, n, d->r0, d->r1,          \
+    hipLaunchKernelGGL((sched_filter<KeyT, H>), dim3(grid), dim3(kBlock), 0, st, keys, hashes, n, d->r0, d->r1,       \
                        (const SchedDev*)d->sdev, d->log_h + d->log_n, lk, d->log_i + d->log_n, d->sctl, cap, d->set_h,  \
                        (const KeyT*)d->set_k, k, d->sbh, bk, d->sbi, d->log_bmax_s, d->bak_h, (KeyT*)d->bak_k)
         switch (d->hash_kind) {
@@ -1894,6 +1916,21 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
     hipLaunchKernelGGL(sched_publish, dim3(1), dim3(kBlock), 0, st, d->sctl, d->vacc,
                        (const SchedDev*)d->sdev, k, d->shc_dev, (uint32_t*)(d->shc_dev + 12), gen);
     STRY(hipGetLastError());
+    // the merged set published speculatively behind the verdict (size from sctl[2] on the device): it
+    // runs while the host turns the verdict around, and result() takes it if the pass verified and
+    // left no tie for the replica to settle
+    bool spec = false;
+    if (d->spec_dst && n >= d->spec_min) {
+        const uint32_t g = ++*d->spec_gen_ctr;
+        const int64_t per = 32 * 1024;  // bytes per workgroup, as launch_publish_multi
+        const unsigned pgrid = (unsigned)std::min<int64_t>(32, std::max<int64_t>(1, (k * (int64_t)kw + per - 1) / per));
+        hipLaunchKernelGGL(publish_set_kernel, dim3(pgrid), dim3(1024), 0, st, (const uint32_t*)d->set_k,
+                           (uint32_t*)d->spec_dst, (const int64_t*)d->sctl, k, (int32_t)(kw / 4), d->spec_flag, g,
+                           (uint32_t*)(d->ctl + 4));
+        STRY(hipGetLastError());
+        d->spec_gen = g;
+        spec = true;
+    }
     {
         const auto t0w = std::chrono::steady_clock::now();
         bool seen = false;
@@ -1939,6 +1976,7 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
     d->segs.push_back(DistinctState::Seg{d->log_n, c, n});
     d->log_n += c;
     d->seen += n;
+    d->spec_ok = spec && d->m == k && !d->over;  // verified, and no replay will change the set
     *done = true;
     return RSV_OK;
 #undef STRY
@@ -1977,6 +2015,7 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
     int64_t pos = 0;
     int64_t m_next = 0;  // chunk length after an overflow retry
     bool sched_tried = !d->sched || d->log_bmax < 0;
+    if (!sched_tried && n >= 9 * ccap && n < ((int64_t)1 << 31)) OTRY(sched_prepare<KeyT>(d, n, st));
     while (pos < n) {
         const bool full = d->m == k;
         if (full && d->max_h == INT64_MIN) break;  // nothing is < Long.MinValue

@@ -107,11 +107,11 @@ struct Wave {
 
 // One stream on one wave.  SMALL: n < 2^27 -- 32-bit indices, u32 winner table, and Philox counters
 // whose high words are wave-uniform (level 0: g < 2^32; level 1: i/2 < 2^32).
-// DEFER (k <= 64): the lane's winner key is returned instead of stored -- the caller stores it
-// after the next stream's draws, so the random gather's latency overlaps them
+// DEFER (k <= 64): the lane's winner index is returned (-1: none) and the caller gathers its key
+// after storing the previous stream's, so the random gather's latency overlaps the next stream's draws
 template <typename KeyT, int V, bool SMALL, bool DEFER>
-__device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict__ keys, int64_t off, int64_t len,
-                                          uint64_t stream, KeyT* __restrict__ o) {
+__device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restrict__ keys, int64_t off, int64_t len,
+                                             uint64_t stream, KeyT* __restrict__ o) {
     using IdxT = typename std::conditional<SMALL, uint32_t, uint64_t>::type;
     constexpr uint32_t QC = qcap_of(V), RG = ring_of(V), WIN = RG * 1024;  // WIN: indices in the ring
     const uint32_t lane = W.lane, k = W.k;
@@ -175,12 +175,13 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
         const uint64_t i0 = (uint64_t)g << 4;
         const uint32_t T = g < kLut ? (uint32_t)W.lut[(uint32_t)g] : block_threshold(i0, W.dense_lim);
         uint32_t mask = valid ? mask_for(w, T) : 0u;
+        if constexpr ((V & 4096) != 0) mask = (mask == 0x12345u) ? 1u : 0u;  // variant: no candidates (cost probe)
         bool clip;  // wave-uniform; 32-bit compares for SMALL (scalar: no 64-bit s_cmp_lt)
         if constexpr (SMALL) clip = ((uint32_t)gb << 4) < (uint32_t)flo || (((uint32_t)gb + 64) << 4) > (uint32_t)len;
         else clip = ((uint64_t)gb << 4) < (uint64_t)flo || (((uint64_t)gb + 64) << 4) > (uint64_t)len;
         if (clip) mask &= clip16(i0, (uint64_t)flo, (uint64_t)len);
         W.stash[ring * 64 + lane] = w;
-        if (((uint64_t)gb << 4) < (uint64_t)hend) {  // this iteration holds head indices (uniform)
+        if ((V & 1024) == 0 && ((uint64_t)gb << 4) < (uint64_t)hend) {  // this iteration holds head indices (uniform)
             __builtin_amdgcn_wave_barrier();
             const IdxT ia = std::max<IdxT>((IdxT)k & ~(IdxT)1, gb << 4);
             const IdxT ib = std::min<IdxT>(hend, (gb + 64) << 4);
@@ -206,7 +207,9 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
         const uint32_t incl = wave_incl_scan(cnt);
         const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint32_t tag = (ring << 10) | (lane << 4);  // = (g mod 256) << 4
-        if (tail - head + tot <= W.fifo_cap) {  // uniform: the whole iteration fits
+        if constexpr ((V & 2048) != 0) {  // variant: no FIFO append (cost probe)
+            if (tot == 0x7FFFFFFFu) W.q[0] = (uint16_t)mask;
+        } else if (tail - head + tot <= W.fifo_cap) {  // uniform: the whole iteration fits
             uint32_t pos = tail + incl - cnt;
             while (mask) {
                 const uint32_t e = __builtin_ctz(mask);
@@ -238,14 +241,14 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
     }
     while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head), gb - 64);
     __builtin_amdgcn_wave_barrier();
-    if constexpr (DEFER) {
-        KeyT v = 0;
+    if constexpr (DEFER) {  // the caller gathers (one load site, see k2_segmented)
+        int64_t at = -1;
         if (lane < k) {
             const IdxT wi = tab[lane];
-            v = wi ? keys[off + (int64_t)wi] : ((int64_t)lane < len ? keys[off + lane] : (KeyT)0);
+            at = wi ? (int64_t)wi : ((int64_t)lane < len ? (int64_t)lane : -1);
         }
         __builtin_amdgcn_wave_barrier();
-        return v;
+        return at;
     }
     for (uint32_t j = lane; j < k; j += 64) {
         const IdxT wi = tab[j];
@@ -255,7 +258,7 @@ __device__ __forceinline__ KeyT k2_stream(const Wave& W, const KeyT* __restrict_
             o[j] = wi ? keys[off + (int64_t)wi] : ((int64_t)j < len ? keys[off + j] : (KeyT)0);
     }
     __builtin_amdgcn_wave_barrier();
-    return (KeyT)0;
+    return -1;
 }
 
 // V: development variants for tools/micro_k2.hip (0 = the product kernel)
@@ -270,7 +273,9 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
     const uint64_t dense_lim = 256ull * k;
     for (uint32_t g = threadIdx.x; g < kLut; g += blockDim.x) lut[g] = (uint16_t)block_threshold((uint64_t)g << 4, dense_lim);
     __syncthreads();
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // wave index in a scalar register: stream numbers and offsets[] loads below are wave-uniform
+    // (scalar loads, counted by lgkmcnt -- never waited for together with the deferred key gather)
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     // per wave: stash [kRing][64] x 16 B | FIFO kQCap x u16 | last-writer table k x (u32 | u64)
     constexpr size_t qbytes = qcap_of(V) * 2, sbytes = ring_of(V) * 64 * 16;
     unsigned char* base = lds + kLutBytes + (size_t)wave * (sbytes + qbytes + (size_t)k * 8);
@@ -286,6 +291,7 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
     const bool defer = k <= 64 && (V & 16) == 0 && (V & 1) == 0;
     KeyT* pend_o = nullptr;
     KeyT pend_v = 0;
+    bool pend_ok = false;
     for (; s < S; s += wave_stride) {
         // wave-uniform stream bounds (scalar registers: uniform control flow below)
         off = ((int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)off)) |
@@ -294,19 +300,21 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
               ((int64_t)__builtin_amdgcn_readfirstlane((int)(end >> 32)) << 32);
         const int64_t len = end - off;
         const int64_t s_next = s + wave_stride;
-        int64_t off_next = 0, end_next = 0;
-        if (s_next < S) {  // prefetch: in flight during this stream's work
-            off_next = offsets[s_next];
-            end_next = offsets[s_next + 1];
-        }
+        // prefetch, in flight during this stream's work; unconditional (clamped index), so the
+        // loop-top wait for it is vmcnt(1) -- it does not also wait for the deferred gather below
+        const int64_t s_pf = std::min<int64_t>(s_next, S - 1);
+        const int64_t off_next = offsets[s_pf], end_next = offsets[s_pf + 1];
         const uint64_t stream = stream_base + (uint64_t)s;
         KeyT* o = out + s * (int64_t)k;
         if (defer) {  // k <= 64: this stream's key is stored after the next stream's draws
-            const KeyT v = len < kSmallLen ? k2_stream<KeyT, V, true, true>(W, keys, off, len, stream, o)
-                                           : k2_stream<KeyT, V, false, true>(W, keys, off, len, stream, o);
-            if (pend_o && lane < k) pend_o[lane] = pend_v;
+            const int64_t at = len < kSmallLen ? k2_stream<KeyT, V, true, true>(W, keys, off, len, stream, o)
+                                               : k2_stream<KeyT, V, false, true>(W, keys, off, len, stream, o);
+            // the previous stream's key (loaded a whole stream ago) leaves its register before this
+            // stream's load lands in it: no copy of a load in flight, so no s_waitcnt at the stream end
+            if (pend_o && lane < k) pend_o[lane] = pend_ok ? pend_v : (KeyT)0;
             pend_o = o;
-            pend_v = v;
+            pend_ok = at >= 0;  // else an empty slot: the load below reads a valid dummy word
+            pend_v = *(pend_ok ? keys + off + at : (const KeyT*)offsets);
         } else if (len < kSmallLen) {
             k2_stream<KeyT, V, true, false>(W, keys, off, len, stream, o);
         } else {
@@ -316,7 +324,7 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
         off = off_next;
         end = end_next;
     }
-    if (pend_o && lane < k) pend_o[lane] = pend_v;
+    if (pend_o && lane < k) pend_o[lane] = pend_ok ? pend_v : (KeyT)0;
 }
 
 }  // namespace k2

@@ -358,11 +358,11 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
         s->win_zero = false;  // until this batch's resolve is enqueued
     }
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
-        // set mode: large batches publish the merged set speculatively (distinct_spec_target) --
-        // only where a publication can happen at all (a coherent result buffer of k keys); other
-        // samplers (huge k, ordered mode, device-only consumers) keep the result buffer lazy
-        if ((int64_t)s->k * s->kw <= kPublishMaxBytes && !distinct_is_ordered(s->distinct) &&
-            n >= distinct_spec_min(s->distinct)) {
+        // large batches publish the merged set speculatively (distinct_spec_target: set mode behind
+        // its last merge, ordered mode behind the scheduled pass) -- only where a publication can
+        // happen at all (a coherent result buffer of k keys); other samplers (huge k, device-only
+        // consumers) keep the result buffer lazy
+        if ((int64_t)s->k * s->kw <= kPublishMaxBytes && n >= distinct_spec_min(s->distinct)) {
             if (rsv_status st = ensure_result_buffer(s)) return st;
             if (s->result_publish) distinct_spec_target(s->distinct, s->result_dev, s->result_flag_dev, &s->result_gen);
         }

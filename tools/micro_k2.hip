@@ -119,6 +119,14 @@ int main(int argc, char** argv) {
         if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
         return 0;
     }
+    if (argc > 1 && argv[1][0] == 'c') {  // cost split of the level-0 side (no gather, no resolve)
+        if (run(k2::k2_segmented<int64_t, 9>, "9 dropped + no gather", false)) return 1;
+        if (run(k2::k2_segmented<int64_t, 9 | 1024>, "9 + no head", false)) return 1;
+        if (run(k2::k2_segmented<int64_t, 9 | 1024 | 2048>, "9 + no head + no append", false)) return 1;
+        if (run(k2::k2_segmented<int64_t, 9 | 1024 | 2048 | 4096>, "9 + no head + no append + no candidates", false)) return 1;
+        if (run(k2::k2_segmented<int64_t, 1 | 1024>, "1 + no head (resolve kept)", false)) return 1;
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 'h') {  // dense-head multiplier: 4 (product), 2, none
         if (run(k2::k2_segmented<int64_t, 32>, "32 head [k, 2k)", true)) return 1;
         if (run(k2::k2_segmented<int64_t, 64>, "64 no head (all through the FIFO)", true)) return 1;
