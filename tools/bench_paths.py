@@ -55,11 +55,25 @@ def c3(dev):
     offs = torch.arange(0, n + 1, L, dtype=torch.int64, device=dev)
     t = timed(lambda: batch.sample_segmented(keys, offs, k, seed=1), reps=5)
     l0, l1 = R.k2_calls(S, L, k)
+    # the memory floor: K2 must fetch each stream's 64 winning keys, ~57 distinct random 128-B lines
+    # of its 32 KB segment (7.5 GB per launch by FETCH_SIZE, profiles/r02).  Timed here as a plain
+    # gather of 64 uniform random positions per 4096-key row (the last writer of a slot is uniform on
+    # [0, n)); tools/micro_gather.hip times the same access as a hand-written kernel (1.40-1.47 ms)
+    g = torch.Generator(device=dev)
+    g.manual_seed(12345)
+    idx = torch.randint(0, L, (S, k), device=dev, generator=g)
+    rows = keys.view(S, L)
+    t_g = timed(lambda: torch.gather(rows, 1, idx), reps=5)
+    del idx
     return {"config": "C3 segmented 2^20 x 4096, k=64", "elements": n, "seconds": t,
             "Gelem_s": n / t / 1e9,
             "roofline": R.valu_roofline(l0, l1, t, "k2_segmented",
-                                        note="launch time = median of 5 (HIP events); K2 reads only the "
-                                             "64 winning keys per stream (gather), so its bound is VALU"),
+                                        note="launch time = median of 5 (HIP events); VALU: the Philox draws "
+                                             "alone; the binding floor is the winner gather below"),
+            "gather_floor": {"seconds": t_g, "frac": t_g / t,
+                             "what": "torch.gather of 64 random positions per 4096-key row (2^26 random "
+                                     "8-B loads, ~57 distinct 128-B lines per row): the memory work K2 "
+                                     "cannot avoid; frac = floor / K2 launch"},
             "winner_gather_bytes": S * k * 8}
 
 
@@ -73,21 +87,26 @@ def c4(dev, hash_kind="identity", order="auto", twins=False, seed=7):
     torch.cuda.synchronize()
     L = _native.load()
     times, kern = [], []
-    for rep in range(4):
+    # reps 1..4 timed end to end with the filter timer off (its events add marker packets and host
+    # calls to the batch); one more rep with it on, for the filter launches and their time
+    for rep in range(6):
+        prof = rep == 5
         mk = Sampler.distinct(k, seed=seed, order=order)
         d = mk(hash=hash_kind) if hash_kind != "default" else mk()
         d.set_stream(torch.cuda.current_stream().cuda_stream)
-        _native.check(L.rsv_profile_enable(d.handle, 1))
+        if prof:
+            _native.check(L.rsv_profile_enable(d.handle, 1))
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         d.sample_all(vals)
         r = d.result()
         t1 = time.perf_counter()
-        ms, cnt = C.c_double(), C.c_int64()
-        _native.check(L.rsv_profile_read(d.handle, C.byref(ms), C.byref(cnt)))
-        if rep:
-            times.append(t1 - t0)
+        if prof:
+            ms, cnt = C.c_double(), C.c_int64()
+            _native.check(L.rsv_profile_read(d.handle, C.byref(ms), C.byref(cnt)))
             kern.append((ms.value / 1e3, cnt.value))
+        elif rep:
+            times.append(t1 - t0)
         assert r.size == k
         d.close()
     t = sorted(times)[len(times) // 2]
