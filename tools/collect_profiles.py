@@ -21,7 +21,9 @@ import shutil
 import statistics
 import sys
 
-KERNELS = {"k1": "k1_last_writer", "c3": "k2_segmented"}  # C2 runs K1 unfused (rsv_runtime.hip)
+# C2 runs K1 unfused (rsv_runtime.hip); "gather" = tools/micro_gather's plain winner-key gather (the
+# C3 memory floor); "c4" = the ordered-distinct scheduled pass (kernel stats only)
+KERNELS = {"k1": "k1_last_writer", "c3": "k2_segmented", "gather": "gather<0>", "c4": "sched_filter"}
 
 
 def pmc(dirpath: str, kernel: str) -> dict:
