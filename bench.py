@@ -205,8 +205,9 @@ def main() -> None:
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--seed", type=int, default=0xC0FFEE)
     ap.add_argument("--stream-id", type=int, default=0x5A5A)
-    ap.add_argument("--time-every", type=int, default=4,
-                    help="HIP events around every N-th K1 launch of the timed steps (1 = every launch)")
+    ap.add_argument("--time-every", type=int, default=8,
+                    help="HIP events around every N-th K1 launch of the timed steps (1 = every launch); "
+                         "each timed launch carries ~10 us of marker packets and host calls")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the other hot-path configs (C3 segmented, C4 distinct, C2 on java_l)")
@@ -286,7 +287,7 @@ def main() -> None:
     torch.cuda.synchronize()
     # K1 timing: HIP events around every N-th K1 launch of the timed steps (process-wide list,
     # drained after the timed region; rsv_profile_global in include/reservoir_hip.h).  Each event
-    # pair adds ~5 us of marker packets to its step, so by default one step in four carries them.
+    # pair adds ~5 us of marker packets to its step, so by default one step in eight carries them.
     _native.check(L.rsv_profile_global(max(1, args.time_every)))
     t0 = time.perf_counter()
     res = None

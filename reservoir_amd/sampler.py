@@ -204,9 +204,11 @@ class GpuSampler:
 
     def sample_all(self, elements: Iterable) -> None:
         """Sampler.sampleAll (Sampler.scala:49-50): same result as sample() on each element."""
-        if not self._L.rsv_is_open(self._h):
-            raise IllegalStateException("use of sampler after calling `result()`")
         if _is_torch_cuda(elements) and self._map is identity and not self._precomputed:
+            # device fast path: rsv_sample_batch itself raises IllegalStateException on a closed
+            # sampler (check_open, same message) before it touches the stream or the keys
+            if self._h is None:  # closed: the handle is gone
+                raise IllegalStateException("use of sampler after calling `result()`")
             torch = _torch()
             t = elements if elements.is_contiguous() else elements.contiguous()
             cur = _current_raw_stream(torch, t)
@@ -226,6 +228,8 @@ class GpuSampler:
             N.check(self._L.rsv_sample_batch(self._h, C.c_void_p(t.data_ptr()), n_keys,
                                              N.MEM_DEVICE, None))
             return
+        if not self._L.rsv_is_open(self._h):
+            raise IllegalStateException("use of sampler after calling `result()`")
         if self._width > 8:
             keys = self._wide_keys(elements)
         elif isinstance(elements, np.ndarray) and self._map is identity:

@@ -501,3 +501,42 @@ def test_ordered_scheduled_pass_ties(cuda, oracle):
     d = Sampler.distinct(1500, seed=23)()
     d.sample_all(torch.from_numpy(vals).to(cuda))
     assert d.result().tolist() == ref.result()[0].tolist()
+
+
+@pytest.mark.gpu
+def test_ordered_speculative_publication(cuda, oracle, monkeypatch):
+    """Ordered mode (default Long.hashCode): a batch that takes the scheduled pass publishes the
+    merged set right behind the pass's verdict (RSV_SPEC_MIN_BATCH=1 forces it on every such batch),
+    and result() takes that publication only when the pass verified and left no tie for the host
+    replica.  Several batches of a reusable sampler with results read in between, host and device
+    batches, colliding hashes (tied boundary buckets: the replay path must not use the stale
+    publication), and a fresh single-use sampler: every result equals the oracle's sequential
+    RandomValues."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    monkeypatch.setenv("RSV_SPEC_MIN_BATCH", "1")
+    rng = np.random.default_rng(31)
+    for k, n, buckets in [(300, 600_000, None), (300, 600_000, 400), (2000, 900_000, None)]:
+        if buckets is None:
+            base = rng.integers(-2**62, 2**62, size=int(n * 0.7), dtype=np.int64)
+            vals = np.concatenate([base, base[rng.integers(0, base.size, size=n - base.size)]])
+            rng.shuffle(vals)
+        else:
+            vals = _colliding(rng, n, buckets)
+        d = Sampler.distinct(k, seed=17, reusable=True)()  # default hash -> ordered
+        ref = oracle.Distinct(k, 17, oracle.HASH_JAVA_LONG)
+        vd = torch.from_numpy(vals).to(cuda)
+        for part_i, (a, b) in enumerate([(0, n // 3), (n // 3, 2 * n // 3), (2 * n // 3, n)]):
+            if part_i == 1:
+                d.sample_all(vals[a:b])  # host batch
+            else:
+                d.sample_all(vd[a:b])
+            ref.sample_all(vals[a:b])
+            assert np.array_equal(np.sort(d.result()), np.sort(ref.result()[0])), (k, n, buckets, part_i)
+    d = Sampler.distinct(500, seed=3)()
+    d.sample_all(torch.from_numpy(vals).to(cuda))
+    ref = oracle.Distinct(500, 3, oracle.HASH_JAVA_LONG)
+    ref.sample_all(vals)
+    assert np.array_equal(np.sort(d.result()), np.sort(ref.result()[0]))
