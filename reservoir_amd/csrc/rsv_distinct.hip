@@ -794,7 +794,7 @@ __device__ __forceinline__ bool ent_less3(int64_t ha, KeyT ka, uint32_t ia, int6
 // one wave per bucket: sort by (h, key, tag), keep the first of each (h, key) run (its earliest
 // arrival), write them back compacted; each kept element adds +1 / -1 at ranges r_a / r_h + 1 of
 // the block's difference array (sdiff, LDS)
-template <typename KeyT, int R>
+template <typename KeyT, int R, int AGG>
 __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(int64_t* gh, KeyT* gk, uint32_t* gi, uint32_t n,
                                                             const int64_t* sb, const int64_t* stt, int nr,
                                                             int* sdiff) {
@@ -875,6 +875,7 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(int64_t* gh, KeyT* g
         }
         const bool first = i < n && (i == 0 || ph != h[r] || pk != k[r]);
         const unsigned long long bal = __ballot(first);
+        int ra = 1, rh = -1;
         if (first) {
             const uint32_t o = base + (uint32_t)__popcll(bal & lanemask_lt());
             gh[o] = h[r];
@@ -889,17 +890,45 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(int64_t* gh, KeyT* g
                     if (sb[mid] >= (int64_t)g[r]) hi = mid;
                     else lo = mid;
                 }
-            const int ra = std::max(1, hi);
+            ra = std::max(1, hi);
             int a = 0, z = nr;  // t[a] >= h > t[z] (t[nr] treated as -inf)
             while (z - a > 1) {
                 const int mid = (a + z) >> 1;
                 if (stt[mid] >= h[r]) a = mid;
                 else z = mid;
             }
-            const int rh = stt[0] >= h[r] ? a : -1;
-            if (ra <= rh) {
+            rh = stt[0] >= h[r] ? a : -1;
+        }
+        // +1 at r_a, -1 at r_h + 1 of the difference array.  The bucket map is monotone in h, so a
+        // bucket's elements share r_h almost always: one atomic for the wave's -1s then, instead of
+        // up to 64 on one LDS word
+        const bool part = ra <= rh;
+        if constexpr (AGG == 0) {  // one atomic per element and end (RSV_SCHED_AGG=0, A/B)
+            if (part) {
                 atomicAdd(&sdiff[ra], 1);
                 atomicAdd(&sdiff[rh + 1], -1);
+            }
+        } else {
+            const unsigned long long pm = __ballot(part);
+            if (pm) {
+                const int lead = __builtin_ctzll(pm);
+                const int rh0 = __shfl(rh, lead);
+                if (__ballot(part && rh != rh0) == 0) {
+                    if ((int)(threadIdx.x & 63) == lead) atomicAdd(&sdiff[rh0 + 1], -(int)__popcll(pm));
+                } else if (part) {
+                    atomicAdd(&sdiff[rh + 1], -1);
+                }
+                if constexpr (AGG == 2) {  // +1s too: one atomic per distinct r_a of the wave
+                    unsigned long long left = pm;
+                    while (left) {
+                        const int ra0 = __shfl(ra, __builtin_ctzll(left));
+                        const unsigned long long same = __ballot(part && ra == ra0);
+                        if ((int)(threadIdx.x & 63) == __builtin_ctzll(same)) atomicAdd(&sdiff[ra0], (int)__popcll(same));
+                        left &= ~same;
+                    }
+                } else if (part) {
+                    atomicAdd(&sdiff[ra], 1);
+                }
             }
         }
         base += (uint32_t)__popcll(bal);
@@ -909,7 +938,7 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(int64_t* gh, KeyT* g
     return base;
 }
 
-template <typename KeyT>
+template <typename KeyT, int AGG>
 __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap, int64_t* __restrict__ ctl,
                                                      int32_t log_bmax, int64_t* __restrict__ bh, KeyT* __restrict__ bk,
                                                      uint32_t* __restrict__ bi, const SchedDev* __restrict__ sd,
@@ -935,9 +964,9 @@ __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap
         uint32_t* gi = bi + (size_t)b * kBucketCap;
         uint32_t nd = 0;
         if (n > 0)
-            nd = n <= 64    ? wave_sort_bucket_tagged<KeyT, 1>(gh, gk, gi, n, sb, stt, nr, sdiff)
-                 : n <= 128 ? wave_sort_bucket_tagged<KeyT, 2>(gh, gk, gi, n, sb, stt, nr, sdiff)
-                            : wave_sort_bucket_tagged<KeyT, 4>(gh, gk, gi, n, sb, stt, nr, sdiff);
+            nd = n <= 64    ? wave_sort_bucket_tagged<KeyT, 1, AGG>(gh, gk, gi, n, sb, stt, nr, sdiff)
+                 : n <= 128 ? wave_sort_bucket_tagged<KeyT, 2, AGG>(gh, gk, gi, n, sb, stt, nr, sdiff)
+                            : wave_sort_bucket_tagged<KeyT, 4, AGG>(gh, gk, gi, n, sb, stt, nr, sdiff);
         if ((threadIdx.x & 63) == 0) {
             *bdist = nd;
             if (nd) atomicAdd(bucket_group(ctl, log_bmax) + (b >> 4), nd);
@@ -1912,8 +1941,17 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
         STRY(hipGetLastError());
     }
     if (d->timer) d->timer->mark(st);
-    hipLaunchKernelGGL(sched_sort<KeyT>, dim3((B + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, k, cap,
-                       d->sctl, d->log_bmax_s, d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
+    {
+        // the difference array's LDS atomics aggregated per wave (RSV_SCHED_AGG: 0 none, 1 the -1s,
+        // 2 both; read once, for A/B runs)
+        static const int agg = [] {
+            const char* e = std::getenv("RSV_SCHED_AGG");
+            return e ? std::atoi(e) : 1;
+        }();
+        auto kern = agg == 0 ? sched_sort<KeyT, 0> : agg == 2 ? sched_sort<KeyT, 2> : sched_sort<KeyT, 1>;
+        hipLaunchKernelGGL(kern, dim3((B + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, k, cap, d->sctl,
+                           d->log_bmax_s, d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
+    }
     hipLaunchKernelGGL(bucket_emit<KeyT>, dim3((B + kEmitBuckets - 1) / kEmitBuckets), dim3(kBlock), 0, st, k, cap,
                        d->sctl, d->log_bmax_s, (const int64_t*)d->sbh, (const KeyT*)bk, k, d->set_h, (KeyT*)d->set_k,
                        (int32_t)sp->lb);
