@@ -176,7 +176,10 @@ rsv_status rsv_export_state(rsv_sampler* s, int64_t* idx_dev, void* keys_dev, in
                             int64_t* out_n);
 /* Merge `parts` exported states (laid out back to back, `part_len` entries each, e.g. gathered
  * from every rank) into this sampler.  ELEMENTS: per slot the largest global index wins (last
- * writer).  DISTINCT: bottom-k of the union.  total_count sets the merged element count. */
+ * writer).  DISTINCT: bottom-k of the union by (hash, key).  total_count sets the merged element
+ * count.  An RSV_DISTINCT_ORDERED sampler merges the same way: a stream split across ranks has no
+ * single arrival order, so the reference's PriorityQueue tie choice at the boundary hash (S:394-409)
+ * is replaced by the (hash, key) order there; with an injective hash the result is identical. */
 rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* keys_dev,
                            const int64_t* hash_dev, const int64_t* part_n_host, int32_t parts,
                            int64_t part_len, int64_t total_count);
