@@ -1054,6 +1054,19 @@ __global__ __launch_bounds__(1024) void publish_set_kernel(const uint32_t* __res
     }
 }
 
+// one logged segment gathered into arrival order (perm from the radix sort of its arrival indices)
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void permute_log(const uint32_t* __restrict__ perm, const int64_t* __restrict__ h,
+                                                      const KeyT* __restrict__ k, int64_t c, int64_t* __restrict__ oh,
+                                                      KeyT* __restrict__ ok) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < c; t += stride) {
+        const uint32_t p = perm[t];
+        oh[t] = h[p];
+        ok[t] = k[p];
+    }
+}
+
 inline unsigned grid_1d(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 }  // namespace
@@ -1137,10 +1150,12 @@ struct DistinctState {
     double sched_beta = 1.6;        // RSV_SCHED_BETA (test hook: a small beta forces the fallback)
     uint32_t* perm = nullptr;       // [ord_cap] one segment's candidates in arrival order
     uint32_t* sorted_i = nullptr;   // [ord_cap] radix-sort key output
+    int64_t* ord_h = nullptr;       // [ord_cap] one segment's hashes and keys permuted into arrival order
+    void* ord_k = nullptr;
     int64_t ord_cap = 0;            // capacity of the two buffers above and of the pinned copies
-    int64_t* ph = nullptr;          // pinned: hashes, keys (as KeyT), perm of one segment
+    int64_t* ph = nullptr;          // pinned: hashes, keys (as KeyT) of one segment in arrival order
     void* pk = nullptr;
-    uint32_t* pp = nullptr;
+    uint32_t* pp = nullptr;         // (unused since the device-side permutation; freed if set)
 };
 
 void distinct_set_timer(DistinctState* d, KernelTimer* t) { d->timer = t; }
@@ -1295,7 +1310,8 @@ void distinct_destroy(DistinctState* d) {
     if (!d) return;
     void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->ctl, d->bh, d->bk, d->mh0, d->mh1, d->mk0,
                   d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp, d->log_h, d->log_k, d->log_i,
-                  d->perm, d->sorted_i, d->sdev, d->sctl, d->sbh, d->sbk, d->sbi, d->vacc, d->bak_h, d->bak_k};
+                  d->perm, d->sorted_i, d->ord_h, d->ord_k, d->sdev, d->sctl, d->sbh, d->sbk, d->sbi, d->vacc,
+                  d->bak_h, d->bak_k};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
     pool_host_free(d->h_pinned);
     pool_host_free(d->hc);
@@ -1674,6 +1690,8 @@ static hipError_t ensure_ordered(DistinctState* d, int64_t cap, hipStream_t st) 
     hipError_t e;
     if ((e = grow((void**)&d->perm, 0, (size_t)cap * 4, false, st))) return e;
     if ((e = grow((void**)&d->sorted_i, 0, (size_t)cap * 4, false, st))) return e;
+    if ((e = grow((void**)&d->ord_h, 0, (size_t)cap * 8, false, st))) return e;
+    if ((e = grow(&d->ord_k, 0, (size_t)cap * d->kw, false, st))) return e;
     pool_host_free(d->ph);
     pool_host_free(d->pk);
     pool_host_free(d->pp);
@@ -1682,7 +1700,6 @@ static hipError_t ensure_ordered(DistinctState* d, int64_t cap, hipStream_t st) 
     d->pp = nullptr;
     if ((e = pool_host_alloc((void**)&d->ph, (size_t)cap * 8, hipHostMallocDefault))) return e;
     if ((e = pool_host_alloc(&d->pk, (size_t)cap * d->kw, hipHostMallocDefault))) return e;
-    if ((e = pool_host_alloc((void**)&d->pp, (size_t)cap * 4, hipHostMallocDefault))) return e;
     size_t tb = 0;
     if ((e = rocprim::radix_sort_pairs(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                        rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (size_t)cap)))
@@ -1755,17 +1772,18 @@ static hipError_t replay_log(DistinctState* d, hipStream_t st) {
                                            rocprim::counting_iterator<uint32_t>(0), d->perm, (size_t)g.c, 0, bits,
                                            st)))
             return e;
-        if ((e = hipMemcpyAsync(d->pp, d->perm, (size_t)g.c * 4, hipMemcpyDeviceToHost, st))) return e;
-        if ((e = hipMemcpyAsync(d->ph, d->log_h + g.off, (size_t)g.c * 8, hipMemcpyDeviceToHost, st))) return e;
-        if ((e = hipMemcpyAsync(d->pk, (const KeyT*)d->log_k + g.off, (size_t)g.c * sizeof(KeyT),
-                                hipMemcpyDeviceToHost, st)))
-            return e;
+        // the permutation applied on the device, so the host replica reads the segment in arrival
+        // order sequentially (two random reads per element from a ~20 MB log cost more than its heap)
+        hipLaunchKernelGGL(permute_log<KeyT>, dim3((unsigned)std::min<int64_t>((g.c + kBlock - 1) / kBlock, 8192)),
+                           dim3(kBlock), 0, st, d->perm, d->log_h + g.off, (const KeyT*)d->log_k + g.off, g.c,
+                           d->ord_h, (KeyT*)d->ord_k);
+        if ((e = hipGetLastError())) return e;
+        if ((e = hipMemcpyAsync(d->ph, d->ord_h, (size_t)g.c * 8, hipMemcpyDeviceToHost, st))) return e;
+        if ((e = hipMemcpyAsync(d->pk, d->ord_k, (size_t)g.c * sizeof(KeyT), hipMemcpyDeviceToHost, st))) return e;
         if ((e = hipStreamSynchronize(st))) return e;
         const KeyT* pk = (const KeyT*)d->pk;
-        const uint32_t* pp = d->pp;
         const int64_t* ph = d->ph;
-        d->rep.sample_run(
-            g.c, [&](int64_t t) { return (int64_t)pk[pp[t]]; }, [&](int64_t t) { return ph[pp[t]]; });
+        d->rep.sample_run(g.c, [&](int64_t t) { return (int64_t)pk[t]; }, [&](int64_t t) { return ph[t]; });
     }
     d->segs.clear();
     d->log_n = 0;
