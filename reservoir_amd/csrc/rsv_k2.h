@@ -67,6 +67,22 @@ __device__ __forceinline__ uint32_t mask_for(const u32x4& w, uint32_t T) {
     return T == 0 ? zero_byte_mask16(w) : T > 255 ? 0xFFFFu : lt_mask16_borrow(w, T);
 }
 
+// mask_for for T <= 16 (T = 0, the sparse region's b == 0, is T = 1): b < T needs planes 4..7 zero
+// (the high words' OR) and the low four planes below T -- 4 borrow steps instead of 8
+__device__ __forceinline__ uint32_t mask_for_small(const u32x4& w, uint32_t T) {
+    const uint32_t M = (T ? T : 1u) - 1u;
+    const uint32_t words[2] = {w.x, w.y};
+    uint32_t br = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const uint32_t plane = (p & 1) ? (words[p >> 1] >> 16) : words[p >> 1];
+        const uint32_t mm = (uint32_t)((int32_t)(M << (31 - p)) >> 31);
+        br = __builtin_amdgcn_bitop3_b32(plane, br, mm, 0xD4);
+    }
+    const uint32_t hi = w.z | w.w;
+    return ~(br | hi | (hi >> 16)) & 0xFFFFu;
+}
+
 __device__ __forceinline__ uint32_t clip16(uint64_t i0, uint64_t lo, uint64_t hi) {
     uint32_t m = 0xFFFFu;
     if (i0 < lo) m = (lo - i0 >= 16) ? 0u : ((0xFFFFu << (uint32_t)(lo - i0)) & 0xFFFFu);
@@ -174,7 +190,10 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
         else w = level0(dk, (uint64_t)g);
         const uint64_t i0 = (uint64_t)g << 4;
         const uint32_t T = g < kLut ? (uint32_t)W.lut[(uint32_t)g] : block_threshold(i0, W.dense_lim);
-        uint32_t mask = valid ? mask_for(w, T) : 0u;
+        // T falls with the block index, so lane 0's (block gb) bounds the iteration's: past the first
+        // blocks of a stream every lane has T <= 16 (C3: iterations 1..3) and takes the short compare
+        const uint32_t Tmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)T);
+        uint32_t mask = valid ? ((Tmax <= 16u && (V & 8192) == 0) ? mask_for_small(w, T) : mask_for(w, T)) : 0u;
         if constexpr ((V & 4096) != 0) mask = (mask == 0x12345u) ? 1u : 0u;  // variant: no candidates (cost probe)
         bool clip;  // wave-uniform; 32-bit compares for SMALL (scalar: no 64-bit s_cmp_lt)
         if constexpr (SMALL) clip = ((uint32_t)gb << 4) < (uint32_t)flo || (((uint32_t)gb + 64) << 4) > (uint32_t)len;

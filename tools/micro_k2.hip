@@ -1,7 +1,8 @@
 // micro_k2.hip -- K2 (segmented, rsv_k2.h) variant timing at C3's shape: 2^20 streams x 4096 keys,
 // k = 64 (development tool, not product).  Variants: 0 = product kernel, 1 = no winner-key gather,
 // 2 = no level-1 Philox, 8 = candidates dropped after the FIFO append, 9 = 8 + 1, 16 = the
-// winner keys stored right after their gather (the product defers the store by one stream).
+// winner keys stored right after their gather (the product defers the store by one stream),
+// 8192 = the 8-plane candidate mask for every block (the product takes 4 planes once T <= 16).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/micro_k2.hip -o tools/micro_k2
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -53,7 +54,7 @@ int main(int argc, char** argv) {
     size_t lds_run = lds;
     auto run = [&](auto kern, const char* name, bool check) -> int {
         std::vector<float> ts;
-        for (int rep = 0; rep < 7; ++rep) {
+        for (int rep = 0; rep < 15; ++rep) {
             CK(hipEventRecord(e0));
             hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * k2::kWaves), lds_run, 0, (const int64_t*)keys,
                                (const int64_t*)offs, S, k, 1u, 0u, 0ull, out, cnt, 0xFFFFFFFFu);
@@ -84,7 +85,7 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
-    {  // the lane-per-stream form (k2_segmented2)
+    if (!(argc > 1 && argv[1][0] == 'g')) {  // the lane-per-stream form (k2_segmented2)
         const size_t lds2 = k2::lds_bytes2(k);
         const unsigned grid2 = (unsigned)((S + 64 * k2::kWaves2 - 1) / (64 * k2::kWaves2));
         std::vector<float> ts;
@@ -117,6 +118,14 @@ int main(int argc, char** argv) {
         if (run(k2::k2_segmented<int64_t, 256>, "256 stash ring of 2 iterations", true)) return 1;
         lds_run = lds;
         if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'g') {  // A/B/A against the previous masks and the gather-free forms
+        if (run(k2::k2_segmented<int64_t, 8192>, "8192 8-plane masks everywhere (r02 up to here)", true)) return 1;
+        if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+        if (run(k2::k2_segmented<int64_t, 8193>, "8193 8-plane masks, no gather", false)) return 1;
+        if (run(k2::k2_segmented<int64_t, 1>, "1 no gather", false)) return 1;
+        if (run(k2::k2_segmented<int64_t, 8192>, "8192 (again)", true)) return 1;
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'c') {  // cost split of the level-0 side (no gather, no resolve)
