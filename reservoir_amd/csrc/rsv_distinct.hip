@@ -1155,7 +1155,6 @@ struct DistinctState {
     int64_t ord_cap = 0;            // capacity of the two buffers above and of the pinned copies
     int64_t* ph = nullptr;          // pinned: hashes, keys (as KeyT) of one segment in arrival order
     void* pk = nullptr;
-    uint32_t* pp = nullptr;         // (unused since the device-side permutation; freed if set)
 };
 
 void distinct_set_timer(DistinctState* d, KernelTimer* t) { d->timer = t; }
@@ -1317,7 +1316,6 @@ void distinct_destroy(DistinctState* d) {
     pool_host_free(d->hc);
     pool_host_free(d->ph);
     pool_host_free(d->pk);
-    pool_host_free(d->pp);
     pool_host_free(d->shc);
     delete d;
 }
@@ -1694,10 +1692,8 @@ static hipError_t ensure_ordered(DistinctState* d, int64_t cap, hipStream_t st) 
     if ((e = grow(&d->ord_k, 0, (size_t)cap * d->kw, false, st))) return e;
     pool_host_free(d->ph);
     pool_host_free(d->pk);
-    pool_host_free(d->pp);
     d->ph = nullptr;
     d->pk = nullptr;
-    d->pp = nullptr;
     if ((e = pool_host_alloc((void**)&d->ph, (size_t)cap * 8, hipHostMallocDefault))) return e;
     if ((e = pool_host_alloc(&d->pk, (size_t)cap * d->kw, hipHostMallocDefault))) return e;
     size_t tb = 0;
