@@ -21,7 +21,11 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
                    all cores, C4 prefix)
   secondary     -- (N = 1) the other configs of BASELINE.json: C3 segmented (with K2's VALU
                    roofline), C4 distinct (identity; Long.hashCode in set and ordered order; the
-                   ordered replay branch), C2 on engine java_l (tools/bench_paths.py)
+                   ordered replay branch), C2 on engine java_l (tools/bench_paths.py), C5
+                   sustained elem/s at k = 1 Mi (tools/bench_c5)
+  c4            -- (N > 1) C4 at its own definition: N x 5e8 keys split by rank (4e9 at N = 8),
+                   distinct sampling + distributed.combine inside the timed step, both hashes, the
+                   merged set checked against one sampler over the whole stream (c4_leg)
 """
 from __future__ import annotations
 
@@ -63,6 +67,15 @@ def host_cores() -> int:
         return os.cpu_count() or 1
 
 
+def cpu_quota():
+    """CPUs this job may use per the cgroup v2 cpu.max quota (None when unlimited / unreadable)."""
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(k: int, n_stream: int, seed: int, c4_host=None) -> dict:
     """The oracle (C restatement of Sampler.scala) on the host, median of 5 runs per leg.
 
@@ -73,7 +86,7 @@ def cpu_baseline(k: int, n_stream: int, seed: int, c4_host=None) -> dict:
     from oracle import oracle as O
 
     L = O.lib()
-    threads = min(16, host_cores())
+    quota = cpu_quota()
     out = np.zeros(max(k, 1 << 10), dtype=np.int64)
     op = out.ctypes.data_as(C.c_void_p)
     legs = []
@@ -110,22 +123,32 @@ def cpu_baseline(k: int, n_stream: int, seed: int, c4_host=None) -> dict:
         legs.append({"config": f"C1 Sampler.distinct(100), hash = {name}, per element", "cores": 1,
                      "Gelem_s": round(n1 / t / 1e9, 4), "sample": "1e7 keys"})
 
-    # C3: one reference sampler per stream (4096 Longs, k = 64) on every host core we may use
+    # C3: one reference sampler per stream (4096 Longs, k = 64) on every host core (nproc
+    # affinity cores), and on the CPU quota the box grants this job (cgroup cpu.max) when it is smaller
     S3, L3 = 1 << 16, 4096
     k3 = O.splitmix_keys(0, S3 * L3)
-    for mode, name in ((0, "per-element sample()"), (1, "sampleAll(IndexedSeq)")):
-        t = _median(lambda: L.or_time_segmented_algo_l(64, k3, S3, L3, mode, threads, None))
-        legs.append({"config": f"C3 one Sampler(64) per stream, {name}", "cores": threads,
-                     "Gelem_s": round(S3 * L3 / t / 1e9, 3), "sample": f"2^16 of the 2^20 streams x {L3} keys"})
+    counts = [host_cores()]
+    if quota and quota < host_cores():
+        counts.append(max(1, int(quota)))
+    for threads in counts:
+        for mode, name in ((0, "per-element sample()"), (1, "sampleAll(IndexedSeq)")):
+            t = _median(lambda: L.or_time_segmented_algo_l(64, k3, S3, L3, mode, threads, None), 3)
+            legs.append({"config": f"C3 one Sampler(64) per stream, {name}", "cores": threads,
+                         "Gelem_s": round(S3 * L3 / t / 1e9, 3),
+                         "sample": f"2^16 of the 2^20 streams x {L3} keys on {threads} threads"
+                                   + (" (all affinity cores)" if threads == host_cores() else
+                                      " (the job's cgroup CPU quota)")})
     del k3
 
-    # C4: Sampler.distinct(65536), default Long.hashCode, over a prefix of one GPU's C4 share
+    # C4: Sampler.distinct(65536) over a prefix of one GPU's C4 share, both hashes of BASELINE.md
     if c4_host is not None:
         n4 = c4_host.size
-        t = _median(lambda: L.or_time_distinct(65536, 7, O.HASH_JAVA_LONG, c4_host, n4))
-        legs.append({"config": "C4 Sampler.distinct(65536), hash = Long.hashCode, per element", "cores": 1,
-                     "Gelem_s": round(n4 / t / 1e9, 4),
-                     "sample": f"the first {n4:.1e} keys of C4's per-GPU share (30 % duplicates, Feistel order)"})
+        for hk, name in ((O.HASH_JAVA_LONG, "Long.hashCode (default)"), (O.HASH_IDENTITY, "identity")):
+            t = _median(lambda: L.or_time_distinct(65536, 7, hk, c4_host, n4), 3)
+            legs.append({"config": f"C4 Sampler.distinct(65536), hash = {name}, per element", "cores": 1,
+                         "Gelem_s": round(n4 / t / 1e9, 4),
+                         "sample": f"the first {n4:.1e} keys of C4's per-GPU share (30 % duplicates, Feistel order); "
+                                   "median of 3"})
     return {
         "value": round(per_elem, 4),
         "unit": "Gelem/s",
@@ -134,6 +157,7 @@ def cpu_baseline(k: int, n_stream: int, seed: int, c4_host=None) -> dict:
         "sample": f"per-element sample() (Algorithm L, Sampler.scala:248-259) over one stream of "
                   f"{reps * buf_n:.3g} keys (a {buf_n:.0e}-key C2 prefix replayed {reps}x), k={k}; median of 5",
         "host_cores": host_cores(),
+        "cpu_quota_cores": quota,
         "legs": legs,
     }
 
@@ -158,6 +182,95 @@ def secondary(dev) -> list:
             r = {"config": name, "error": f"{type(ex).__name__}: {ex}"}
         out.append({kk: (round(v, 6) if isinstance(v, float) else v) for kk, v in r.items()})
         torch.cuda.empty_cache()
+    return out
+
+
+def c5_legs(n: int = 200_000_000) -> list:
+    """C5 (BASELINE.json configs[4]): sustained elem/s of a per-element source feeding the sampler
+    through the C ABI at k = 1 Mi -- rsv_sample per element (what SampleImpl.onPush does,
+    SampleImpl.scala:27-31) and zero-copy pinned batches (rsv_stage_acquire/commit), both engines.
+    tools/bench_c5 (built by __graft_entry__.build) prints one JSON object per leg."""
+    exe = os.path.join(ROOT, "tools", "bench_c5")
+    if not os.path.exists(exe):
+        return [{"config": "C5", "error": f"{exe} not built (__graft_entry__.build)"}]
+    r = subprocess.run([exe, str(n), str(1 << 20)], capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        return [{"config": "C5", "error": f"bench_c5 rc={r.returncode}: {r.stderr[-400:]}"}]
+    return [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+
+
+def c4_leg(args, rank: int, world: int, dev, backend: str) -> dict:
+    """C4 (BASELINE.json configs[3]) at N ranks: a stream of N x 5e8 Long keys (30 % duplicates; at
+    N = 8 the 4e9-key workload) split by rank, k = 65536.  A step: every rank creates a distinct
+    sampler, samples its contiguous 5e8 piece (device-resident), distributed.combine merges the
+    ranks' sets (one all_gather; the exact replay for the default hash when its boundary bucket is
+    tied), result() to the host, close.  Timed like the headline (barrier + synchronize, max over
+    ranks); afterwards rank 0 checks the merged set against ONE sampler fed the whole stream."""
+    import torch
+    import torch.distributed as dist
+
+    import workloads
+    from reservoir_amd import Sampler
+    from reservoir_amd import distributed as D
+
+    piece, k = args.c4_keys, 65536
+    total = piece * world
+    keys = workloads.c4_slice(total, rank * piece, (rank + 1) * piece, dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    out = {"workload": f"C4: distinct over {total:.2e} Long keys (30% duplicates, Feistel order), k=65536, "
+                       f"{world} ranks x {piece:.1e} contiguous keys, merged by distributed.combine",
+           "ranks": world, "backend": backend, "legs": []}
+
+    def make(hash_kind):
+        mk = Sampler.distinct(k, seed=7)
+        return mk(hash="identity") if hash_kind == "identity" else mk()
+
+    for hash_kind in ("identity", "default"):
+        replays = 0
+
+        def step():
+            nonlocal replays
+            s = make(hash_kind)
+            s.set_stream(stream)
+            s.sample_all(keys)
+            replays += D.combine(s, device=dev, total_count=total)
+            r = s.result()
+            s.close()
+            return r
+
+        for _ in range(args.c4_warmup):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        replays = 0
+        t0 = time.perf_counter()
+        res = None
+        for _ in range(args.c4_steps):
+            res = step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                          device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        elapsed = float(el.item())
+        leg = {"hash": hash_kind + (" (Long.hashCode, ordered: exact sequential set)" if hash_kind == "default"
+                                    else " (set mode, bit-exact bottom-k)"),
+               "steps": args.c4_steps, "ms_per_step": round(elapsed / args.c4_steps * 1e3, 4),
+               "Gelem_s": round(total * args.c4_steps / elapsed / 1e9, 3), "exact_replays": replays}
+        if rank == 0:  # the merged set vs one sampler over the whole stream (same seed, same hash)
+            full = workloads.c4_slice(total, 0, total, dev)
+            one = make(hash_kind)
+            one.sample_all(full)
+            want = np.sort(one.result())
+            one.close()
+            del full
+            torch.cuda.empty_cache()
+            leg["matches_single_sampler"] = bool(np.array_equal(np.sort(res), want))
+        out["legs"].append(leg)
+    del keys
+    torch.cuda.empty_cache()
     return out
 
 
@@ -210,7 +323,11 @@ def main() -> None:
                          "each timed launch carries ~10 us of marker packets and host calls")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the other hot-path configs (C3 segmented, C4 distinct, C2 on java_l)")
+                    help="skip the other hot-path configs (C3 segmented, C4 distinct, C2 on java_l, C5)")
+    ap.add_argument("--c4-keys", type=int, default=500_000_000, help="C4 keys per rank (N > 1 leg)")
+    ap.add_argument("--c4-steps", type=int, default=10)
+    ap.add_argument("--c4-warmup", type=int, default=2)
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 leg at N > 1")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -308,6 +425,12 @@ def main() -> None:
     k1_s = k1_ms / max(k1_launches, 1) / 1e3  # K1 launch time (HIP events on the launch stream)
     assert res is not None and res.size == k
 
+    c4 = None
+    if world > 1 and not args.no_c4:
+        del keys
+        torch.cuda.empty_cache()
+        c4 = c4_leg(args, rank, world, dev, backend)
+
     if rank == 0:
         total = n * world * args.steps
         l0, l1 = R.k1_calls(n, k, offset)
@@ -346,12 +469,19 @@ def main() -> None:
                                if world > 1 else "single GPU",
             },
             "roofline": roof,
+            "ranks_seen": dist.get_world_size() if world > 1 else 1,
         }
+        if c4 is not None:
+            line["c4"] = c4
         c4_host = None
         if world == 1 and not args.no_secondary:
             del keys
             torch.cuda.empty_cache()
             line["secondary"] = secondary(dev)
+            try:
+                line["secondary"] += c5_legs()
+            except Exception as ex:  # noqa: BLE001 -- reported, not raised
+                line["secondary"].append({"config": "C5", "error": f"{type(ex).__name__}: {ex}"})
         if world == 1 and not args.no_cpu_baseline:
             import workloads
 

@@ -177,12 +177,46 @@ rsv_status rsv_export_state(rsv_sampler* s, int64_t* idx_dev, void* keys_dev, in
 /* Merge `parts` exported states (laid out back to back, `part_len` entries each, e.g. gathered
  * from every rank) into this sampler.  ELEMENTS: per slot the largest global index wins (last
  * writer).  DISTINCT: bottom-k of the union by (hash, key).  total_count sets the merged element
- * count.  An RSV_DISTINCT_ORDERED sampler merges the same way: a stream split across ranks has no
- * single arrival order, so the reference's PriorityQueue tie choice at the boundary hash (S:394-409)
- * is replaced by the (hash, key) order there; with an injective hash the result is identical. */
+ * count.  An RSV_DISTINCT_ORDERED sampler merges the same way, which is the reference's set
+ * unless the boundary hash bucket is oversubscribed (rsv_get_distinct_info `tied`); then the
+ * exact set comes from rsv_export_log / rsv_merge_log below (reservoir_amd/distributed.py does
+ * both).  With an injective hash the result is always identical. */
 rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* keys_dev,
                            const int64_t* hash_dev, const int64_t* part_n_host, int32_t parts,
                            int64_t part_len, int64_t total_count);
+
+/* ---- Exact multi-rank merge of ORDERED distinct samplers (the reference's default hash) ----- *
+ * A stream split across ranks in order (rank r holds the r-th contiguous piece) is, to the
+ * reference, one sequential RandomValues run (S:394-409): under a colliding hash the members of the
+ * boundary hash bucket depend on that run's arrival order and heap ties.  rsv_merge_state gives the
+ * (hash, key) bottom-k of the union; when rsv_get_distinct_info then reports `tied` (or a rank's own
+ * set was tied at the merged maximum), the exact set comes from replaying every rank's logged
+ * candidates in rank order: a rank's log is a superset of what the global run admits from its
+ * piece (its local maximum is never below the global one), and the global heap's maximum inside
+ * rank r's piece is below the k-th smallest hash of the pieces before it, so rank r exports only
+ * candidates under that bound (reservoir_amd/distributed.py computes the bounds). */
+typedef struct rsv_distinct_info {
+    uint32_t struct_size;  /* = sizeof(rsv_distinct_info) */
+    int32_t  ordered;      /* RSV_DISTINCT_ORDERED sampler */
+    int32_t  tied;         /* set full and more distinct elements share its maximum hash than it keeps
+                            * (ordered: of those the reference could admit; after rsv_merge_state: of
+                            * the merged union) -- the boundary bucket needs the arrival order */
+    int32_t  log_retained; /* ordered: rsv_export_log can return every candidate logged since creation */
+    int64_t  size;         /* set size */
+    int64_t  max_hash;     /* the set's largest scrambled hash (INT64_MIN when empty) */
+    int64_t  log_entries;  /* ordered: upper bound on rsv_export_log's count */
+} rsv_distinct_info;
+rsv_status rsv_get_distinct_info(rsv_sampler* s, rsv_distinct_info* out);
+/* Every logged candidate with scrambled hash < bound (all of them for bound = INT64_MAX), in
+ * arrival order, into host buffers of cap entries (keys as key_width values); *out_n = the count
+ * (RSV_E_ILLEGAL_ARGUMENT when it exceeds cap).  RSV_E_UNSUPPORTED if the log was not retained.
+ * Stays available after rsv_merge_state until the sampler samples again. */
+rsv_status rsv_export_log(rsv_sampler* s, int64_t bound, int64_t* hashes_host, void* keys_host, int64_t cap,
+                          int64_t* out_n);
+/* Replace the state by a fresh RandomValues replica run over n candidates (host, in global arrival
+ * order: rank 0's export, then rank 1's, ...), as if the sampler had seen the whole stream. */
+rsv_status rsv_merge_log(rsv_sampler* s, const int64_t* hashes_host, const void* keys_host, int64_t n,
+                         int64_t total_count);
 
 /* Packed form of the two calls above for ELEMENTS samplers, the one-collective combine of
  * reservoir_amd/distributed.py: row_dev[0..k) = global index per slot (-1 = empty),

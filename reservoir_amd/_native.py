@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
     "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
     "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read", "rsv_stage_acquire",
-    "rsv_stage_commit",
+    "rsv_stage_commit", "rsv_get_distinct_info", "rsv_export_log", "rsv_merge_log",
 )
 
 
@@ -47,6 +47,18 @@ class RsvConfig(C.Structure):
         ("distinct_order", C.c_int32),
         ("seed", C.c_uint64),
         ("stream_id", C.c_uint64),
+    ]
+
+
+class RsvDistinctInfo(C.Structure):
+    _fields_ = [
+        ("struct_size", C.c_uint32),
+        ("ordered", C.c_int32),
+        ("tied", C.c_int32),
+        ("log_retained", C.c_int32),
+        ("size", C.c_int64),
+        ("max_hash", C.c_int64),
+        ("log_entries", C.c_int64),
     ]
 
 
@@ -115,12 +127,15 @@ def load():
     L.rsv_profile_global_read.argtypes = [C.POINTER(C.c_double), C.POINTER(i64)]
     L.rsv_stage_acquire.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(i64)]
     L.rsv_stage_commit.argtypes = [vp, i64]
+    L.rsv_get_distinct_info.argtypes = [vp, C.POINTER(RsvDistinctInfo)]
+    L.rsv_export_log.argtypes = [vp, i64, vp, vp, i64, C.POINTER(i64)]
+    L.rsv_merge_log.argtypes = [vp, vp, vp, i64, i64]
     for name in ("rsv_config_init", "rsv_create", "rsv_sample", "rsv_sample_batch", "rsv_result",
                  "rsv_result_device", "rsv_set_stream", "rsv_synchronize", "rsv_seek",
                  "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
                  "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
                  "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read", "rsv_stage_acquire",
-                 "rsv_stage_commit"):
+                 "rsv_stage_commit", "rsv_get_distinct_info", "rsv_export_log", "rsv_merge_log"):
         getattr(L, name).restype = i32
     if L.rsv_abi_version() != 1:
         raise ImportError("libreservoir_hip.so ABI version mismatch")

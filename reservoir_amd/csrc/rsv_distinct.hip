@@ -1155,7 +1155,18 @@ struct DistinctState {
     int64_t ord_cap = 0;            // capacity of the two buffers above and of the pinned copies
     int64_t* ph = nullptr;          // pinned: hashes, keys (as KeyT) of one segment in arrival order
     void* pk = nullptr;
+    // Exact multi-rank merge of ordered samplers (rsv_export_log / rsv_merge_log): the candidates
+    // the replica consumed (arrival order, host) + the segments still in the log, and the segments
+    // logged before the last merge -- together every candidate logged since creation (`arch_ok`).
+    // Sampling again after a merge drops them (the merged state has no single arrival order).
+    std::vector<int64_t> arch_h, arch_k;
+    bool arch_ok = true;
+    std::vector<Seg> pre_segs;
+    bool merged = false;
 };
+
+// ~2 GB of host archive (16 B per candidate): beyond it rsv_export_log reports the log as not retained
+constexpr int64_t kArchMax = (int64_t)1 << 27;
 
 void distinct_set_timer(DistinctState* d, KernelTimer* t) { d->timer = t; }
 
@@ -1753,36 +1764,59 @@ static hipError_t upload_replica(DistinctState* d, hipStream_t st) {
     return hipSuccess;
 }
 
-// Every logged segment, in order, through the host replica: a radix sort by chunk index restores
-// arrival order, the replica runs RandomValues.sample on each candidate (Sampler.scala:394-409).
+// One logged segment in arrival order into the pinned host copies d->ph / d->pk: a radix sort by
+// the chunk-relative index restores the order, and the permutation is applied on the device, so
+// the host reads the segment sequentially (two random reads per element from a ~20 MB log cost
+// more than the replica's heap).
+template <typename KeyT>
+static hipError_t segment_to_host(DistinctState* d, const DistinctState::Seg& g, hipStream_t st) {
+    hipError_t e;
+    if ((e = ensure_ordered(d, g.c, st))) return e;
+    unsigned bits = 1;
+    while (bits < 32 && ((uint64_t)1 << bits) < (uint64_t)g.m) ++bits;
+    size_t tb = d->temp_bytes;
+    if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->log_i + g.off, d->sorted_i,
+                                       rocprim::counting_iterator<uint32_t>(0), d->perm, (size_t)g.c, 0, bits, st)))
+        return e;
+    hipLaunchKernelGGL(permute_log<KeyT>, dim3((unsigned)std::min<int64_t>((g.c + kBlock - 1) / kBlock, 8192)),
+                       dim3(kBlock), 0, st, d->perm, d->log_h + g.off, (const KeyT*)d->log_k + g.off, g.c, d->ord_h,
+                       (KeyT*)d->ord_k);
+    if ((e = hipGetLastError())) return e;
+    if ((e = hipMemcpyAsync(d->ph, d->ord_h, (size_t)g.c * 8, hipMemcpyDeviceToHost, st))) return e;
+    if ((e = hipMemcpyAsync(d->pk, d->ord_k, (size_t)g.c * sizeof(KeyT), hipMemcpyDeviceToHost, st))) return e;
+    return hipStreamSynchronize(st);
+}
+
+static void archive_drop(DistinctState* d) {
+    d->arch_ok = false;
+    std::vector<int64_t>().swap(d->arch_h);
+    std::vector<int64_t>().swap(d->arch_k);
+}
+
+// Every logged segment, in order, through the host replica (RandomValues.sample on each candidate,
+// Sampler.scala:394-409); the consumed candidates are kept in the host archive for rsv_export_log.
 template <typename KeyT>
 static hipError_t replay_log(DistinctState* d, hipStream_t st) {
     hipError_t e;
     for (const DistinctState::Seg& g : d->segs) {
         if (g.c == 0) continue;
-        if ((e = ensure_ordered(d, g.c, st))) return e;
-        unsigned bits = 1;
-        while (bits < 32 && ((uint64_t)1 << bits) < (uint64_t)g.m) ++bits;
-        size_t tb = d->temp_bytes;
-        if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->log_i + g.off, d->sorted_i,
-                                           rocprim::counting_iterator<uint32_t>(0), d->perm, (size_t)g.c, 0, bits,
-                                           st)))
-            return e;
-        // the permutation applied on the device, so the host replica reads the segment in arrival
-        // order sequentially (two random reads per element from a ~20 MB log cost more than its heap)
-        hipLaunchKernelGGL(permute_log<KeyT>, dim3((unsigned)std::min<int64_t>((g.c + kBlock - 1) / kBlock, 8192)),
-                           dim3(kBlock), 0, st, d->perm, d->log_h + g.off, (const KeyT*)d->log_k + g.off, g.c,
-                           d->ord_h, (KeyT*)d->ord_k);
-        if ((e = hipGetLastError())) return e;
-        if ((e = hipMemcpyAsync(d->ph, d->ord_h, (size_t)g.c * 8, hipMemcpyDeviceToHost, st))) return e;
-        if ((e = hipMemcpyAsync(d->pk, d->ord_k, (size_t)g.c * sizeof(KeyT), hipMemcpyDeviceToHost, st))) return e;
-        if ((e = hipStreamSynchronize(st))) return e;
+        if ((e = segment_to_host<KeyT>(d, g, st))) return e;
         const KeyT* pk = (const KeyT*)d->pk;
         const int64_t* ph = d->ph;
+        if (d->arch_ok) {
+            if ((int64_t)d->arch_h.size() + g.c > kArchMax) {
+                archive_drop(d);
+            } else {
+                d->arch_h.insert(d->arch_h.end(), ph, ph + g.c);
+                const size_t a = d->arch_k.size();
+                d->arch_k.resize(a + (size_t)g.c);
+                for (int64_t t = 0; t < g.c; ++t) d->arch_k[a + (size_t)t] = (int64_t)pk[t];
+            }
+        }
         d->rep.sample_run(g.c, [&](int64_t t) { return (int64_t)pk[t]; }, [&](int64_t t) { return ph[t]; });
     }
     d->segs.clear();
-    d->log_n = 0;
+    if (d->pre_segs.empty()) d->log_n = 0;  // else the log still holds the pre-merge segments
     return hipSuccess;
 }
 
@@ -2162,6 +2196,12 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
 
 int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* hashes, int64_t n,
                            hipStream_t st) {
+    if (d->merged && n > 0) {  // sampling on after a merge: the pre-merge candidates are history
+        d->merged = false;
+        d->pre_segs.clear();
+        if (d->segs.empty()) d->log_n = 0;
+        archive_drop(d);
+    }
     if (d->ordered)
         return d->kw == 8 ? ordered_sample_impl<int64_t>(d, (const int64_t*)keys, hashes, n, st)
                           : ordered_sample_impl<int32_t>(d, (const int32_t*)keys, hashes, n, st);
@@ -2188,26 +2228,55 @@ int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStre
     return RSV_OK;
 }
 
-int distinct_merge(DistinctState* d, const void* keys_dev, const int64_t* hash_dev, int64_t n,
-                   hipStream_t st) {
-    if (n > 0)
-        if (int rc = distinct_finalize(d, st)) return rc;
-    int64_t off = 0;
-    while (off < n) {  // chunks that fit the merge buffer
-        const int64_t c = std::min<int64_t>(n - off, d->cand_limit);
-        int64_t nd = 0;
-        hipError_t e = d->kw == 8
-                           ? merge_into_set<int64_t>(d, hash_dev + off, (const int64_t*)keys_dev + off, c, &nd, st)
-                           : merge_into_set<int32_t>(d, hash_dev + off, (const int32_t*)keys_dev + off, c, &nd, st);
-        if (e != hipSuccess) {
-            set_error(std::string("distinct_merge: ") + hipGetErrorString(e));
-            return RSV_E_DEVICE;
+void distinct_info(const DistinctState* d, int32_t* ordered, int32_t* tied, int32_t* retained, int64_t* size,
+                   int64_t* max_hash, int64_t* log_entries) {
+    *ordered = d->ordered;
+    *tied = d->m == d->k && d->over;
+    *retained = d->ordered && d->arch_ok;
+    *size = d->m;
+    *max_hash = d->m ? d->set_top : INT64_MIN;
+    int64_t c = (int64_t)d->arch_h.size();
+    for (const DistinctState::Seg& g : d->pre_segs) c += g.c;
+    for (const DistinctState::Seg& g : d->segs) c += g.c;
+    *log_entries = d->ordered ? c : 0;
+}
+
+// Merge `parts` external (key, hash) runs (device; run p at keys + p part_len, part_n[p] entries)
+// into the set: bottom-k of the union by (h, key).  `over` afterwards says whether more distinct
+// elements of the union share the boundary hash than the set keeps (sticky across the chunked
+// merges while the maximum stays).  An ordered sampler rebuilds its replica from the union in
+// (h, key) order (a merged set has no single arrival order; rsv_merge_log is the exact form) and
+// keeps its logged candidates for rsv_export_log until it samples again.
+int distinct_merge_parts(DistinctState* d, const void* keys_dev, const int64_t* hash_dev, const int64_t* part_n,
+                         int32_t parts, int64_t part_len, hipStream_t st) {
+    int64_t total = 0;
+    for (int32_t p = 0; p < parts; ++p) total += std::max<int64_t>(0, std::min(part_n[p], part_len));
+    if (total == 0) return RSV_OK;
+    if (int rc = distinct_finalize(d, st)) return rc;
+    bool tie = d->m == d->k && d->over;
+    for (int32_t p = 0; p < parts; ++p) {
+        const int64_t n = std::max<int64_t>(0, std::min(part_n[p], part_len));
+        const uint8_t* kp = (const uint8_t*)keys_dev + (size_t)p * part_len * d->kw;
+        const int64_t* hp = hash_dev + (size_t)p * part_len;
+        for (int64_t off = 0; off < n;) {  // chunks that fit the merge buffer
+            const int64_t c = std::min<int64_t>(n - off, d->cand_limit);
+            const int64_t old_max = d->max_h;
+            const bool was_full = d->m == d->k;
+            int64_t nd = 0;
+            hipError_t e = d->kw == 8
+                               ? merge_into_set<int64_t>(d, hp + off, (const int64_t*)kp + off, c, &nd, st)
+                               : merge_into_set<int32_t>(d, hp + off, (const int32_t*)kp + off, c, &nd, st);
+            if (e != hipSuccess) {
+                set_error(std::string("distinct_merge: ") + hipGetErrorString(e));
+                return RSV_E_DEVICE;
+            }
+            tie = d->m == d->k && (d->last_tie || (tie && was_full && d->max_h == old_max));
+            off += c;
         }
-        off += c;
     }
-    if (d->ordered && n > 0) {
-        // a merged (multi-GPU) set has no single arrival order: rebuild the replica from the
-        // bottom-k union, inserting in ascending (h, key) order
+    d->over = tie;
+    d->spec_ok = false;
+    if (d->ordered) {
         std::vector<int64_t> hh((size_t)d->m), kk((size_t)d->m);
         std::vector<int32_t> k4(d->kw == 4 ? (size_t)d->m : 0);
         hipError_t e = hipMemcpyAsync(hh.data(), d->set_h, (size_t)d->m * 8, hipMemcpyDeviceToHost, st);
@@ -2222,11 +2291,92 @@ int distinct_merge(DistinctState* d, const void* keys_dev, const int64_t* hash_d
         d->rep.reset(d->k);
         for (int64_t i = 0; i < d->m; ++i) d->rep.sample(d->kw == 8 ? kk[(size_t)i] : (int64_t)k4[(size_t)i], hh[(size_t)i]);
         d->max_h = d->rep.max_hash;
-        d->segs.clear();  // the replica starts over from the union: the set arrays are its set
-        d->log_n = 0;
-        d->over = false;
+        // the replica starts over from the union (the set arrays are its set); the logged segments
+        // stay readable for rsv_export_log until the next sample
+        d->pre_segs.insert(d->pre_segs.end(), d->segs.begin(), d->segs.end());
+        d->segs.clear();
         d->exact = true;
+        d->merged = true;
     }
+    return RSV_OK;
+}
+
+template <typename KeyT>
+static int log_export_impl(DistinctState* d, int64_t bound, int64_t* out_h, KeyT* out_k, int64_t cap, int64_t* out_n,
+                           hipStream_t st) {
+    const bool all = bound == INT64_MAX;
+    int64_t cnt = 0;
+    auto emit = [&](int64_t h, int64_t key) {
+        if (all || h < bound) {
+            if (cnt < cap) {
+                out_h[cnt] = h;
+                out_k[cnt] = (KeyT)key;
+            }
+            ++cnt;
+        }
+    };
+    for (size_t i = 0; i < d->arch_h.size(); ++i) emit(d->arch_h[i], d->arch_k[i]);
+    for (const std::vector<DistinctState::Seg>* v : {&d->pre_segs, &d->segs})
+        for (const DistinctState::Seg& g : *v) {
+            if (g.c == 0) continue;
+            if (hipError_t e = segment_to_host<KeyT>(d, g, st)) {
+                set_error(std::string("rsv_export_log: ") + hipGetErrorString(e));
+                return e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;
+            }
+            const KeyT* pk = (const KeyT*)d->pk;
+            for (int64_t t = 0; t < g.c; ++t) emit(d->ph[t], (int64_t)pk[t]);
+        }
+    *out_n = cnt;
+    if (cnt > cap) {
+        set_error("rsv_export_log: cap is smaller than the number of candidates (*out_n)");
+        return RSV_E_ILLEGAL_ARGUMENT;
+    }
+    return RSV_OK;
+}
+
+int distinct_log_export(DistinctState* d, int64_t bound, int64_t* out_h, void* out_k, int64_t cap, int64_t* out_n,
+                        hipStream_t st) {
+    if (!d->ordered || !d->arch_ok) {
+        set_error(!d->ordered ? "rsv_export_log needs an RSV_DISTINCT_ORDERED sampler"
+                              : "rsv_export_log: the candidate log was not retained (archive limit, or sampled "
+                                "after a merge)");
+        return RSV_E_UNSUPPORTED;
+    }
+    return d->kw == 8 ? log_export_impl<int64_t>(d, bound, out_h, (int64_t*)out_k, cap, out_n, st)
+                      : log_export_impl<int32_t>(d, bound, out_h, (int32_t*)out_k, cap, out_n, st);
+}
+
+// The exact multi-rank merge: a fresh replica runs RandomValues.sample over the concatenated
+// candidate run (every rank's rsv_export_log output, in rank = global arrival order) and becomes
+// the sampler's state, as if it had seen the whole stream.
+int distinct_log_merge(DistinctState* d, const int64_t* h, const void* keys, int64_t n, int64_t seen,
+                       hipStream_t st) {
+    if (!d->ordered) {
+        set_error("rsv_merge_log needs an RSV_DISTINCT_ORDERED sampler");
+        return RSV_E_UNSUPPORTED;
+    }
+    d->rep.reset(d->k);
+    if (d->kw == 8) {
+        const int64_t* kk = (const int64_t*)keys;
+        d->rep.sample_run(n, [&](int64_t t) { return kk[t]; }, [&](int64_t t) { return h[t]; });
+    } else {
+        const int32_t* kk = (const int32_t*)keys;
+        d->rep.sample_run(n, [&](int64_t t) { return (int64_t)kk[t]; }, [&](int64_t t) { return h[t]; });
+    }
+    d->segs.clear();
+    d->pre_segs.clear();
+    d->log_n = 0;
+    archive_drop(d);
+    hipError_t e = d->kw == 8 ? upload_replica<int64_t>(d, st) : upload_replica<int32_t>(d, st);
+    if (e != hipSuccess) {
+        set_error(std::string("rsv_merge_log: ") + hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;
+    }
+    d->over = false;
+    d->exact = true;
+    d->merged = true;
+    d->spec_ok = false;
+    d->seen = std::max(d->seen, seen);
     return RSV_OK;
 }
 

@@ -161,8 +161,16 @@ int64_t distinct_spec_min(const DistinctState* d);  // smallest batch that publi
 bool distinct_spec_take(DistinctState* d, uint32_t* gen);
 // copies the set (ascending hash) to device buffers; either may be null
 int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStream_t st);
-// merge external (key, hash) entries (device) into the set
-int distinct_merge(DistinctState* d, const void* keys_dev, const int64_t* hash_dev, int64_t n,
-                   hipStream_t st);
+// merge `parts` external (key, hash) runs (device; run p at p * part_len) into the set
+int distinct_merge_parts(DistinctState* d, const void* keys_dev, const int64_t* hash_dev, const int64_t* part_n,
+                         int32_t parts, int64_t part_len, hipStream_t st);
+void distinct_info(const DistinctState* d, int32_t* ordered, int32_t* tied, int32_t* retained, int64_t* size,
+                   int64_t* max_hash, int64_t* log_entries);
+// ordered samplers: every logged candidate with h < bound (all of them for bound = INT64_MAX) in
+// arrival order into host buffers; the exact replay of a concatenated candidate run
+int distinct_log_export(DistinctState* d, int64_t bound, int64_t* out_h, void* out_k, int64_t cap, int64_t* out_n,
+                        hipStream_t st);
+int distinct_log_merge(DistinctState* d, const int64_t* h, const void* keys, int64_t n, int64_t seen,
+                       hipStream_t st);
 
 }  // namespace rsv

@@ -920,12 +920,9 @@ rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* k
     if (rsv_status st = flush_stage(s)) return st;
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
         if (parts > 0 && (!hash_dev || !part_n_host)) return fail(RSV_E_NULL_POINTER, "hash_dev/part_n is NULL");
-        for (int32_t p = 0; p < parts; ++p) {
-            const int64_t n = std::min(part_n_host[p], part_len);
-            int rc = distinct_merge(s->distinct, (const uint8_t*)keys_dev + (size_t)p * part_len * s->kw,
-                                    hash_dev + (size_t)p * part_len, n, s->stream);
-            if (rc) return (rsv_status)rc;
-        }
+        if (parts > 0)
+            if (int rc = distinct_merge_parts(s->distinct, keys_dev, hash_dev, part_n_host, parts, part_len, s->stream))
+                return (rsv_status)rc;
     } else {
         if (part_len < (int64_t)s->k) return fail(RSV_E_ILLEGAL_ARGUMENT, "part_len < k");
         if (parts > 0 && !idx_dev) return fail(RSV_E_NULL_POINTER, "idx_dev is NULL");
@@ -935,6 +932,52 @@ rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* k
         s->pub_valid = false;
     }
     if (total_count > s->count) s->count = total_count;
+    if (s->own_stream) RSV_HIP_TRY(sync_stream(s));
+    return RSV_OK;
+}
+
+static rsv_status check_distinct(rsv_sampler* s, const char* what) {
+    if (rsv_status st = check_open(s)) return st;
+    if (s->cfg.kind != RSV_KIND_DISTINCT) return fail(RSV_E_UNSUPPORTED, std::string(what) + " needs a DISTINCT sampler");
+    return RSV_OK;
+}
+
+rsv_status rsv_get_distinct_info(rsv_sampler* s, rsv_distinct_info* out) {
+    if (rsv_status st = check_distinct(s, "rsv_get_distinct_info")) return st;
+    if (!out) return fail(RSV_E_NULL_POINTER, "out is NULL");
+    if (out->struct_size < sizeof(rsv_distinct_info)) return fail(RSV_E_ILLEGAL_ARGUMENT, "struct_size too small");
+    DeviceGuard g(s->device);
+    touch(s);
+    if (rsv_status st = flush_stage(s)) return st;
+    distinct_info(s->distinct, &out->ordered, &out->tied, &out->log_retained, &out->size, &out->max_hash,
+                  &out->log_entries);
+    return RSV_OK;
+}
+
+rsv_status rsv_export_log(rsv_sampler* s, int64_t bound, int64_t* hashes_host, void* keys_host, int64_t cap,
+                          int64_t* out_n) {
+    if (rsv_status st = check_distinct(s, "rsv_export_log")) return st;
+    if (!out_n) return fail(RSV_E_NULL_POINTER, "out_n is NULL");
+    if (cap < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative cap");
+    if (cap > 0 && (!hashes_host || !keys_host)) return fail(RSV_E_NULL_POINTER, "hashes_host/keys_host is NULL");
+    DeviceGuard g(s->device);
+    touch(s);
+    if (rsv_status st = flush_stage(s)) return st;
+    return (rsv_status)distinct_log_export(s->distinct, bound, hashes_host, keys_host, cap, out_n, s->stream);
+}
+
+rsv_status rsv_merge_log(rsv_sampler* s, const int64_t* hashes_host, const void* keys_host, int64_t n,
+                         int64_t total_count) {
+    if (rsv_status st = check_distinct(s, "rsv_merge_log")) return st;
+    if (n < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative n");
+    if (n > 0 && (!hashes_host || !keys_host)) return fail(RSV_E_NULL_POINTER, "hashes_host/keys_host is NULL");
+    DeviceGuard g(s->device);
+    touch(s);
+    if (rsv_status st = flush_stage(s)) return st;
+    if (int rc = distinct_log_merge(s->distinct, hashes_host, keys_host, n, total_count, s->stream))
+        return (rsv_status)rc;
+    if (total_count > s->count) s->count = total_count;
+    s->pub_valid = false;
     if (s->own_stream) RSV_HIP_TRY(sync_stream(s));
     return RSV_OK;
 }

@@ -332,6 +332,39 @@ class GpuSampler:
         N.check(self._L.rsv_merge_packed(self._h, C.c_void_p(rows.data_ptr()), int(rows.shape[0]),
                                          int(rows.shape[1]), int(total_count)))
 
+    def distinct_info(self) -> dict:
+        """Distinct samplers: set size, largest hash, whether the boundary hash bucket is
+        oversubscribed (``tied``), and the candidate log's status (include/reservoir_hip.h)."""
+        info = N.RsvDistinctInfo()
+        info.struct_size = C.sizeof(N.RsvDistinctInfo)
+        N.check(self._L.rsv_get_distinct_info(self._h, C.byref(info)))
+        return {f: int(getattr(info, f)) for f, _ in N.RsvDistinctInfo._fields_[1:]}
+
+    @property
+    def is_ordered(self) -> bool:
+        return self.is_distinct and bool(self.distinct_info()["ordered"])
+
+    def export_log(self, bound: int = 2**63 - 1):
+        """Ordered distinct samplers: every logged candidate with hash < ``bound`` in arrival order
+        as host arrays (hashes int64, keys of the key type)."""
+        n = C.c_int64(0)
+        cap = self.distinct_info()["log_entries"]
+        h = np.empty(max(cap, 1), dtype=np.int64)
+        k = np.empty(max(cap, 1), dtype=self._dtype)
+        N.check(self._L.rsv_export_log(self._h, int(bound), h.ctypes.data_as(C.c_void_p),
+                                       k.ctypes.data_as(C.c_void_p), cap, C.byref(n)))
+        return h[: n.value].copy(), k[: n.value].copy()
+
+    def merge_log(self, hashes, keys, total_count: int) -> None:
+        """Ordered distinct samplers: become a fresh RandomValues replica run over the candidate
+        run (host arrays, global arrival order)."""
+        h = np.ascontiguousarray(hashes, dtype=np.int64)
+        k = np.ascontiguousarray(keys, dtype=self._dtype)
+        if h.size != k.size:
+            raise IllegalArgumentException("hashes and keys differ in length")
+        N.check(self._L.rsv_merge_log(self._h, h.ctypes.data_as(C.c_void_p), k.ctypes.data_as(C.c_void_p),
+                                      h.size, int(total_count)))
+
     def merge_state(self, idx, keys, hashes, part_n, total_count: int) -> None:
         """Merge gathered partial states ([parts, k] device tensors) into this sampler."""
         parts = int(keys.shape[0])

@@ -1,6 +1,7 @@
 #!/bin/bash
 # gpurun helper: run named steps, each under its own time limit, stop at the first failure.
-#   scripts/gpu_run.sh <outdir> <name> <limit> <command...> [-- <name> <limit> <command...>]...
+#   scripts/gpu_run.sh <outdir> <name> <limit> <command...> [:: <name> <limit> <command...>]...
+# (steps are separated by "::" -- "--" is left alone for rocprofv3's program separator)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -73,6 +73,8 @@ class OracleElements:
 
 class OracleDistinct:
     is_distinct = True
+    key_width = 8
+    key_dtype = np.int64
 
     def __init__(self, k, seed):
         from oracle import oracle as O
@@ -85,6 +87,15 @@ class OracleDistinct:
     def sample_all(self, keys):
         self.d.sample_all(keys)
         self.count += len(keys)
+
+    @property
+    def max_sample_size(self):
+        return self.k
+
+    def distinct_info(self):  # set mode: the exact ordered replay never applies
+        keys, hs = self.d.result()
+        return {"ordered": 0, "tied": 0, "log_retained": 0, "size": keys.size,
+                "max_hash": int(hs.max()) if keys.size else -2**63, "log_entries": 0}
 
     def export_state(self, device):
         keys, hs = self.d.result()
@@ -101,6 +112,151 @@ class OracleDistinct:
 
     def result(self):
         return np.array([v for _, v in self.entries], dtype=np.int64)
+
+
+def _java_long_hashes(O, r0, r1, vals):
+    """RandomValues' scrambled hash of Long.hashCode (Sampler.scala:75, :396) per element."""
+    u = np.asarray(vals, dtype=np.int64).view(np.uint64)
+    hc = ((u ^ (u >> np.uint64(32))) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32).astype(np.int64)
+    return np.array([O.scramble(r0, r1, int(x)) for x in hc], dtype=np.int64)
+
+
+class OracleOrdered:
+    """Ordered (default-hash) distinct shard sampler on the oracle, with GpuSampler's exact-merge
+    protocol: distinct_info / export_log / merge_log.  Its "log" is every element of the piece, a
+    superset of what any sequential run admits from it (the engine logs fewer)."""
+
+    is_distinct = True
+    key_width = 8
+    key_dtype = np.int64
+
+    def __init__(self, k, seed):
+        from oracle import oracle as O
+
+        self.O, self.k, self.seed = O, k, seed
+        self.d = O.Distinct(k, seed, O.HASH_JAVA_LONG)
+        self.seen = np.empty(0, dtype=np.int64)
+        self.count = 0
+        self.merged = None  # (keys, hashes) ascending after merge_state
+        self.tied_merge = False
+
+    @property
+    def max_sample_size(self):
+        return self.k
+
+    def sample_all(self, keys):
+        self.d.sample_all(keys)
+        self.seen = np.concatenate([self.seen, np.asarray(keys, dtype=np.int64)])
+        self.count += len(keys)
+
+    def _state(self):
+        if self.merged is not None:
+            return self.merged
+        keys, hs = self.d.result()
+        o = np.lexsort((keys, hs))
+        return keys[o], hs[o]
+
+    def distinct_info(self):
+        keys, hs = self._state()
+        m = keys.size
+        mx = int(hs[-1]) if m else -2**63
+        if self.merged is not None:
+            tied = self.tied_merge
+        else:  # more distinct elements of the piece with h <= max than the set keeps
+            u = np.unique(self.seen)
+            tied = m == self.k and int((_java_long_hashes(self.O, self.d.r0, self.d.r1, u) <= mx).sum()) > m
+        return {"ordered": 1, "tied": int(tied), "log_retained": 1, "size": m, "max_hash": mx,
+                "log_entries": self.seen.size}
+
+    def export_state(self, device):
+        keys, hs = self._state()
+        n = keys.size
+        pad = lambda a: torch.from_numpy(np.concatenate([a, np.zeros(self.k - n, dtype=np.int64)]))
+        return torch.full((self.k,), -1, dtype=torch.int64), pad(keys), pad(hs), n
+
+    def merge_state(self, idx, keys, hashes, part_n, total):
+        ents = set()
+        for p, n in enumerate(part_n):
+            ents |= set(zip(hashes[p, :n].tolist(), keys[p, :n].tolist()))
+        ents = sorted(ents)
+        top = ents[: self.k]
+        self.tied_merge = len(top) == self.k and sum(1 for h, _ in ents if h <= top[-1][0]) > self.k
+        self.merged = (np.array([v for _, v in top], dtype=np.int64), np.array([h for h, _ in top], dtype=np.int64))
+        self.count = total
+
+    def export_log(self, bound):
+        h = _java_long_hashes(self.O, self.d.r0, self.d.r1, self.seen)
+        keep = h < bound if bound != 2**63 - 1 else np.ones(h.size, dtype=bool)
+        return h[keep], self.seen[keep]
+
+    def merge_log(self, hashes, keys, total):
+        self.d = self.O.Distinct(self.k, self.seed, self.O.HASH_JAVA_LONG)
+        self.d.sample_all(keys)
+        self.merged = None
+        self.seen = np.empty(0, dtype=np.int64)
+        self.count = total
+
+    def result(self):
+        return self._state()[0]
+
+
+def _colliding(rng, n, buckets):
+    """Long keys whose Long.hashCode takes `buckets` values (many distinct keys per hash)."""
+    hi = rng.integers(0, 2**31, size=n, dtype=np.int64)
+    lo = (hi ^ rng.integers(0, buckets, size=n, dtype=np.int64)) & 0xFFFFFFFF
+    return (hi << 32) | lo
+
+
+def _ordered_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from reservoir_amd import distributed as D
+
+        outs = []
+        for seed in range(6):
+            rng = np.random.default_rng(50 + seed)
+            vals = _colliding(rng, 6000, 150)
+            vals = np.concatenate([vals, vals[rng.integers(0, vals.size, 1500)]])
+            lo, hi = D.shard_range(vals.size, rank, world)
+            s = OracleOrdered(40, seed)
+            s.sample_all(vals[lo:hi])
+            replayed = D.combine(s, device="cpu")
+            outs.append((sorted(s.result().tolist()), s.count, replayed))
+        q.put((rank, outs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ordered_exact_combine(oracle, world):
+    """Default-hash distinct split in rank order: combine's exact replay (bounds from the gathered
+    sets, per-rank candidate export, one more all-gather, replica merge) equals the reference's
+    sequential RandomValues over the whole stream -- tie bucket included."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ordered_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    replays = 0
+    for seed in range(6):
+        rng = np.random.default_rng(50 + seed)
+        vals = _colliding(rng, 6000, 150)
+        vals = np.concatenate([vals, vals[rng.integers(0, vals.size, 1500)]])
+        ref = oracle.Distinct(40, seed, oracle.HASH_JAVA_LONG)
+        ref.sample_all(vals)
+        want = sorted(ref.result()[0].tolist())
+        for rank, res in outs:
+            got, cnt, replayed = res[seed]
+            assert got == want and cnt == vals.size, (rank, seed)
+            replays += bool(replayed)
+    assert replays > 0  # the boundary bucket was oversubscribed (40 slots, ~40 keys per hash value)
 
 
 def _free_port():

@@ -10,7 +10,9 @@
       vs or_algo_r_segmented, every count == 64
   C4  one GPU's share of C4 (5e8 keys, 30 % duplicates, k = 65536) under the default
       Long.hashCode (ordered mode): the set equals the oracle's sequential RandomValues; and a
-      hash-twin variant whose boundary hash bucket is oversubscribed, so the host replay runs
+      hash-twin variant whose boundary hash bucket is oversubscribed, so the host replay runs;
+      the share in set mode (hash = identity); and the FULL C4 (4e9 keys) as 8 one-GPU shards
+      merged like the 8-GPU run, plus one sampler over >= 2^31-key batches, both hashes
   C5  akka path at k = 1 Mi: zero-copy pinned batches (rsv_stage_acquire/commit) over 3e7 keys and
       the Sample operator (SampleImpl.scala:27-31) vs the oracle; the per-element rsv_sample path
       at k = 1 Mi runs in tests/cpp/test_ffm_sequence.cpp (test_gpu_ffm.py)
@@ -160,6 +162,76 @@ def test_c4_share_ordered(cuda, oracle, variant, seed):
         tied = torch.unique(vals[h == top]).numel()
         assert tied > int((wh == top).sum()), (tied, int((wh == top).sum()))
     del vals
+    torch.cuda.empty_cache()
+
+
+def test_c4_share_set_mode_identity(cuda, oracle):
+    """C4's per-GPU share (5e8 keys, k = 65536) with hash = identity (set mode: analytic threshold,
+    bucketed merge, speculative publication): the set equals the oracle's RandomValues."""
+    from reservoir_amd import Sampler
+
+    n, k = 500_000_000, 65536
+    vals = _w().c4_data(n, cuda)
+    d = Sampler.distinct(k, seed=7)(hash="identity")
+    d.sample_all(vals)
+    got = d.result()
+    ref = oracle.Distinct(k, 7, oracle.HASH_IDENTITY)
+    ref.sample_all(vals.cpu().numpy())
+    assert got.size == k
+    assert np.array_equal(np.sort(got), np.sort(ref.result()[0]))
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+def test_c4_full_workload_8way(cuda, oracle):
+    """C4 at its own workload (BASELINE.json configs[3]): 4e9 Long keys, 30 % duplicates,
+    k = 65536, split 8 ways -- 8 distinct samplers on one GPU, each fed one contiguous 5e8 piece
+    (= one rank of the 8-GPU run), merged with distributed.merge_local (export_state -> merge_state,
+    plus the exact ordered replay for the default hash).  Also one sampler fed the whole stream in
+    two batches of >= 2^31 keys (the chunk loop).  Both hashes vs the oracle's sequential
+    RandomValues over all 4e9 keys (Sampler.scala:383-412)."""
+    import threading
+
+    import torch
+
+    from reservoir_amd import Sampler
+    from reservoir_amd import distributed as D
+
+    n, k, parts, seed = 4_000_000_000, 65536, 8, 7
+    keys = torch.empty(n, dtype=torch.int64, device=cuda)
+    _w().c4_slice(n, 0, n, cuda, out=keys)
+    torch.cuda.synchronize()
+    refs = {"identity": oracle.Distinct(k, seed, oracle.HASH_IDENTITY),
+            "default": oracle.Distinct(k, seed, oracle.HASH_JAVA_LONG)}
+    step = 250_000_000
+    for a in range(0, n, step):  # the oracle over the whole sequence, both hashes side by side
+        host = keys[a:a + step].cpu().numpy()
+        ts = [threading.Thread(target=r.sample_all, args=(host,)) for r in refs.values()]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    piece = n // parts
+    cut = (1 << 31) + 12_345
+    for name, ref in refs.items():
+        want = np.sort(ref.result()[0])
+        mk = Sampler.distinct(k, seed=seed)
+        make = (lambda: mk(hash="identity")) if name == "identity" else (lambda: mk())
+        shards = []
+        for r in range(parts):
+            s = make()
+            s.sample_all(keys[r * piece:(r + 1) * piece])
+            shards.append(s)
+        target = make()
+        D.merge_local(target, shards)
+        assert target.count == n
+        assert np.array_equal(np.sort(target.result()), want), name
+        single = make()
+        single.sample_all(keys[:cut])
+        single.sample_all(keys[cut:])
+        assert np.array_equal(np.sort(single.result()), want), name
+        del shards, target, single
+    del keys
     torch.cuda.empty_cache()
 
 

@@ -540,3 +540,90 @@ def test_ordered_speculative_publication(cuda, oracle, monkeypatch):
     ref = oracle.Distinct(500, 3, oracle.HASH_JAVA_LONG)
     ref.sample_all(vals)
     assert np.array_equal(np.sort(d.result()), np.sort(ref.result()[0]))
+
+
+@pytest.mark.parametrize("shards,k,n,buckets,int_keys", [(2, 64, 60_000, 200_000, False),
+                                                         (2, 64, 60_000, 2000, False),
+                                                         (3, 300, 400_000, 4000, False),
+                                                         (8, 1000, 1_500_000, 30_000, False),
+                                                         (4, 200, 200_000, 3000, True)])
+def test_ordered_exact_shard_merge(cuda, oracle, shards, k, n, buckets, int_keys):
+    """Default hash, stream split into contiguous pieces (piece r = rank r): distributed.merge_local
+    (the rows, merge and exact replay of distributed.combine, without a process group) equals the
+    reference's sequential RandomValues over the whole stream, tie bucket included -- into a fresh
+    sampler and into shard 0 itself."""
+    import torch
+
+    from reservoir_amd import Sampler
+    from reservoir_amd import distributed as D
+
+    replays = 0
+    for seed in range(4):
+        rng = np.random.default_rng(700 + 10 * shards + seed)
+        if int_keys:
+            vals = rng.integers(-2**31, 2**31 - 1, size=n).astype(np.int64)
+            vals = np.concatenate([vals, vals[rng.integers(0, n, n // 4)]])
+            ref = oracle.Distinct(k, seed, oracle.HASH_JAVA_INT)
+        else:
+            vals = _colliding(rng, n, buckets)
+            vals = np.concatenate([vals, vals[rng.integers(0, n, n // 4)]])
+            ref = oracle.Distinct(k, seed, oracle.HASH_JAVA_LONG)
+        ref.sample_all(vals)
+        want = ref.result()[0].tolist()
+        kt = "int" if int_keys else "long"
+        dt = torch.int32 if int_keys else torch.int64
+        for into_shard in (False, True):
+            ss = []
+            for piece in np.array_split(vals, shards):
+                s = Sampler.distinct(k, seed=seed, key_type=kt, order="ordered")()
+                s.sample_all(torch.from_numpy(piece).to(dt).to(cuda))
+                ss.append(s)
+            target = ss[0] if into_shard else Sampler.distinct(k, seed=seed, key_type=kt, order="ordered")()
+            replays += D.merge_local(target, ss)
+            assert target.count == vals.size
+            assert target.result().astype(np.int64).tolist() == want, (seed, into_shard)
+    if not int_keys and buckets <= 30_000:
+        assert replays > 0  # dense collisions oversubscribe the boundary bucket: the exact replay ran
+
+
+def test_ordered_exact_merge_archived_log(cuda, oracle, monkeypatch):
+    """Shards whose logs were replayed eagerly (RSV_ORDERED_LOG_LIMIT) or finalized by result-like
+    calls keep every candidate in the host archive: the exact merge is unchanged.  Sampling after a
+    merge drops the pre-merge log (rsv_export_log then reports it as not retained)."""
+    import torch
+
+    from reservoir_amd import Sampler, _native as N
+    from reservoir_amd import distributed as D
+
+    monkeypatch.setenv("RSV_ORDERED_LOG_LIMIT", "1")
+    rng = np.random.default_rng(77)
+    vals = _colliding(rng, 300_000, 2500)
+    want = {}
+    for seed in range(3):
+        ref = oracle.Distinct(250, seed, oracle.HASH_JAVA_LONG)
+        ref.sample_all(vals)
+        want[seed] = ref.result()[0].tolist()
+        ss = []
+        for piece in np.array_split(vals, 3):
+            s = Sampler.distinct(250, seed=seed)()
+            for sub in np.array_split(piece, 4):
+                s.sample_all(torch.from_numpy(sub).to(cuda))
+            ss.append(s)
+        info = ss[1].distinct_info()
+        assert info["ordered"] == 1 and info["log_retained"] == 1
+        t = Sampler.distinct(250, seed=seed)()
+        D.merge_local(t, ss)
+        assert t.result().tolist() == want[seed], seed
+    assert t.distinct_info()["log_retained"] == 0  # rsv_merge_log: the replica is the history now
+    # rsv_merge_state keeps the merged sampler's own log readable until it samples again
+    s = ss[1]
+    before = s.export_log()
+    parts = [p.export_state(cuda) for p in ss]
+    s.merge_state(torch.zeros((3, 250), dtype=torch.int64, device=cuda), torch.stack([p[1] for p in parts]),
+                  torch.stack([p[2] for p in parts]), [p[3] for p in parts], vals.size)
+    after = s.export_log()
+    assert np.array_equal(before[0], after[0]) and np.array_equal(before[1], after[1])
+    s.sample_all(torch.from_numpy(vals[:1000]).to(cuda))
+    assert s.distinct_info()["log_retained"] == 0
+    with pytest.raises(N.ReservoirError):
+        s.export_log()

@@ -1,9 +1,11 @@
-"""reservoir_amd.distributed with the REAL engine: 2 gloo ranks sharing one GPU.
+"""reservoir_amd.distributed with the REAL engine: 2 and 3 gloo ranks sharing one GPU.
 
 Each rank samples its index range of one stream with a GpuSampler (seek + sample_all on device
 keys), then distributed.combine runs the one-collective exchange: export_packed -> all_gather ->
 merge_packed for element samplers, export_state -> all_gather -> merge_state for distinct ones.
-Every rank must end with the oracle's single-stream result (oracle.algo_r, oracle.Distinct).
+Every rank must end with the oracle's single-stream result (oracle.algo_r, oracle.Distinct) --
+including default-hash (ordered) distinct samplers whose boundary hash bucket is oversubscribed,
+which take combine's exact replay (export_log -> all_gather -> merge_log).
 RCCL cannot put two ranks on one device, so this rehearsal uses gloo (CUDA tensors through host
 copies); bench.py at N GPUs uses RCCL with one rank per GPU and the same calls.
 """
@@ -25,6 +27,14 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def _colliding_vals(seed):
+    rng = np.random.default_rng(300 + seed)
+    hi = rng.integers(0, 2**31, size=400_000, dtype=np.int64)
+    lo = (hi ^ rng.integers(0, 3000, size=hi.size, dtype=np.int64)) & 0xFFFFFFFF
+    v = (hi << 32) | lo
+    return np.concatenate([v, v[rng.integers(0, v.size, 100_000)]])
 
 
 def _worker(rank, world, port, q):
@@ -63,6 +73,14 @@ def _worker(rank, world, port, q):
         D.sample_shard(d, torch.from_numpy(vals[dlo:dhi]).to(dev), dlo)
         D.combine(d, device=dev)
         out["distinct"] = (sorted(d.result().tolist()), d.count)
+        # default hash (ordered): the exact combine, boundary bucket included
+        for seed in range(3):
+            cv = _colliding_vals(seed)
+            clo, chi = D.shard_range(cv.size, rank, world)
+            o = Sampler.distinct(300, seed=seed)()
+            o.sample_all(torch.from_numpy(cv[clo:chi]).to(dev))
+            replayed = D.combine(o, device=dev)
+            out[f"ordered{seed}"] = (o.result().tolist(), o.count, bool(replayed))
         q.put((rank, out))
     except BaseException as ex:  # noqa: BLE001 -- reported to the parent
         q.put((rank, repr(ex)))
@@ -71,10 +89,10 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_gloo_ranks_real_engine(cuda, oracle):
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_ranks_real_engine(cuda, oracle, world):
     import torch.multiprocessing as mp
 
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -102,3 +120,13 @@ def test_two_gloo_ranks_real_engine(cuda, oracle):
         for key in ("elements_int", "elements_int_total"):
             assert out[key] == (want32.tolist(), n), (rank, key)
         assert out["distinct"] == (sorted(ref.result()[0].tolist()), vals.size), rank
+    replays = 0
+    for seed in range(3):
+        cv = _colliding_vals(seed)
+        ref = oracle.Distinct(300, seed, oracle.HASH_JAVA_LONG)
+        ref.sample_all(cv)
+        for rank, out in outs:
+            got, cnt, replayed = out[f"ordered{seed}"]
+            assert got == ref.result()[0].tolist() and cnt == cv.size, (rank, seed)
+            replays += replayed
+    assert replays > 0

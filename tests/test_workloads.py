@@ -3,6 +3,7 @@ import os
 import sys
 
 import numpy as np
+import pytest
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
@@ -35,3 +36,14 @@ def test_hash_twins_fold_hashcode(oracle):
     hc = np.array([oracle.lib().or_java_long_hashcode(int(v)) for v in tw[:2000]])
     assert hc.min() >= 0 and hc.max() < 4096
     assert np.unique(tw).size == tw.size
+
+
+@pytest.mark.parametrize("n", [1000, 100_003, 2**16, 2**16 + 1])
+def test_c4_slice_equals_scatter_construction(n):
+    """c4_slice (inverse Feistel, any piece on its own) == the defining scatter construction, and
+    the pieces of an 8-way split concatenate to the whole sequence."""
+    want = W.c4_data_scatter(n, "cpu", chunk=1 << 12)
+    assert torch.equal(W.c4_data(n, "cpu", chunk=1 << 12), want)
+    bounds = [n * r // 8 for r in range(9)]
+    pieces = [W.c4_slice(n, a, b, "cpu", chunk=1 << 12) for a, b in zip(bounds[:-1], bounds[1:])]
+    assert torch.equal(torch.cat(pieces), want)

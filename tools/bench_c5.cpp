@@ -3,7 +3,7 @@
 // k = 1M.  Measures the sustained element rate of rsv_sample (pinned double-buffered staging,
 // asynchronous flushes) and the end-to-end time including result().
 // Build: g++ -O3 -std=c++17 -I include tools/bench_c5.cpp -L reservoir_amd -lreservoir_hip \
-//            -Wl,-rpath,$PWD/reservoir_amd -o tools/bench_c5
+//            -Wl,-rpath,'$ORIGIN/../reservoir_amd' -o tools/bench_c5   (__graft_entry__.build does this)
 #include <algorithm>
 #include <chrono>
 #include <cstdio>

@@ -9,6 +9,8 @@ torch int64 arithmetic wraps like Java Long; logical right shifts are emulated w
                                 duplicates), hash(i) = splitmix64(i ^ 0xD0B) >>> 1; positions
                                 shuffled by a 4-round Feistel permutation of [0, n) (seed 7,
                                 cycle-walking)
+  c4_slice(n, lo, hi, dev)      positions [lo, hi) of c4_data(n), generated directly (inverse
+                                permutation): one rank's piece of C4's 8-way split
   hash_twins(keys, bits)        keys whose java.lang.Long.hashCode takes only 2^bits values (many
                                 distinct keys per hash bucket: the ordered distinct path's replay)
 """
@@ -68,15 +70,65 @@ def feistel_perm(n: int, seed: int, device, chunk: int = 1 << 26) -> torch.Tenso
         y[bad] = enc(y[bad])
 
 
+def _feistel_params(n: int):
+    bits = max(2, (n - 1).bit_length())
+    bits += bits & 1
+    h = bits // 2
+    return h, (1 << h) - 1
+
+
+def feistel_inverse(y: torch.Tensor, n: int, seed: int) -> torch.Tensor:
+    """feistel_perm(n, seed)^-1 at the positions y: the rounds run backwards, and cycle-walking
+    inverts by walking the inverse permutation until it lands inside [0, n)."""
+    h, mask = _feistel_params(n)
+
+    def dec(x):
+        lo, hi = x & mask, x >> h
+        for r in reversed(range(4)):  # enc round: (lo, hi) -> (hi ^ f(lo), lo)
+            lo, hi = hi, lo ^ (smix(hi + ((seed * 4 + r) << 40)) & mask)
+        return (hi << h) | lo
+
+    x = dec(y)
+    while True:
+        bad = torch.nonzero(x >= n).flatten()
+        if bad.numel() == 0:
+            return x
+        x[bad] = dec(x[bad])
+
+
+def _c4_value(i: torch.Tensor, D: int) -> torch.Tensor:
+    vi = torch.where(i < D, i, _srl(smix(i ^ 0xD0B), 1) % max(D, 1))
+    return smix(vi ^ 0xD15C)
+
+
+def c4_slice(n: int, lo: int, hi: int, device, dup: float = 0.3, seed: int = 7, chunk: int = 1 << 26,
+             out: torch.Tensor | None = None) -> torch.Tensor:
+    """Positions [lo, hi) of the C4 sequence of n keys (= c4_data(n)[lo:hi]) without building the
+    whole sequence: position p holds value v_{perm^-1(p)}.  A rank of C4's 8-way split generates
+    its own piece this way; the full 4e9 sequence is 8 such pieces."""
+    D = int(round(n * (1.0 - dup)))
+    if out is None:
+        out = torch.empty(hi - lo, dtype=torch.int64, device=device)
+    for a in range(lo, hi, chunk):
+        b = min(hi, a + chunk)
+        src = feistel_inverse(torch.arange(a, b, dtype=torch.int64, device=device), n, seed)
+        out[a - lo:b - lo] = _c4_value(src, D)
+    return out
+
+
 def c4_data(n: int, device, dup: float = 0.3, seed: int = 7, chunk: int = 1 << 26) -> torch.Tensor:
     """C4: n Long keys, D = (1 - dup) n distinct values, Feistel-shuffled."""
+    return c4_slice(n, 0, n, device, dup, seed, chunk)
+
+
+def c4_data_scatter(n: int, device, dup: float = 0.3, seed: int = 7, chunk: int = 1 << 26) -> torch.Tensor:
+    """The defining construction of c4_data (values scattered through the forward permutation);
+    kept to check c4_slice against (tests/test_workloads.py)."""
     D = int(round(n * (1.0 - dup)))
     vals = torch.empty(n, dtype=torch.int64, device=device)
     for a in range(0, n, chunk):
         b = min(n, a + chunk)
-        i = torch.arange(a, b, dtype=torch.int64, device=device)
-        vi = torch.where(i < D, i, _srl(smix(i ^ 0xD0B), 1) % max(D, 1))
-        vals[a:b] = smix(vi ^ 0xD15C)
+        vals[a:b] = _c4_value(torch.arange(a, b, dtype=torch.int64, device=device), D)
     perm = feistel_perm(n, seed, device)
     out = torch.empty_like(vals)
     out[perm] = vals
