@@ -1,5 +1,6 @@
 /*
- * reservoir_jni.c -- JNI shim of lgbt.princess.reservoir.gpu.Jni (bindings/scala/.../Jni.scala)
+ * reservoir_jni.c -- JNI shim of lgbt.princess.reservoir.gpu.Jni
+ * (bindings/scala/core/lgbt/princess/reservoir/gpu/JniSampler.scala)
  * for the reference's CI JDKs 8/11/15 (build.sbt:37-42), where Panama FFM does not exist.
  *
  * Every native method is a few lines over bindings/jvm/rsv_jvm.{h,c} -- the JVM-side session logic
@@ -69,51 +70,62 @@ JNIEXPORT void JNICALL JNI_FN(sampleInt)(JNIEnv* env, jobject self, jlong s, jin
 }
 
 /* Sampler.sampleAll (Sampler.scala:49-50) over the first n keys of a primitive array (+ hashes when
- * the sampler takes precomputed hashes, else null): copied straight from the pinned-down array
- * into the engine's staging buffer */
-JNIEXPORT void JNICALL JNI_FN(sampleLongs)(JNIEnv* env, jobject self, jlong s, jlongArray keys, jlongArray hashes,
-                                            jint n) {
-    (void)self;
-    jlong* k = (jlong*)(*env)->GetPrimitiveArrayCritical(env, keys, NULL);
-    jlong* h = hashes ? (jlong*)(*env)->GetPrimitiveArrayCritical(env, hashes, NULL) : NULL;
-    rsv_status st = rsv_jvm_sample_array(session(s), k, (const int64_t*)h, n);
-    if (h) (*env)->ReleasePrimitiveArrayCritical(env, hashes, h, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, keys, k, JNI_ABORT);
-    if (st != RSV_OK) throw_status(env, st);
-}
+ * the sampler takes precomputed hashes, else null).  Copied with Get<Type>ArrayRegion straight into
+ * the engine's pinned staging: no array stays pinned (and GC blocked) while a full staging buffer's
+ * commit may wait for the GPU (rsv_jvm_stage_span). */
+#define SAMPLE_ARRAY(NAME, JARR, GET)                                                                   \
+    JNIEXPORT void JNICALL JNI_FN(NAME)(JNIEnv * env, jobject self, jlong s, JARR keys, jlongArray hashes, \
+                                        jint n) {                                                     \
+        (void)self;                                                                                   \
+        jint done = 0;                                                                                \
+        while (done < n) {                                                                            \
+            void* kb = NULL;                                                                          \
+            int64_t* hb = NULL;                                                                       \
+            int64_t room = 0;                                                                         \
+            rsv_status st = rsv_jvm_stage_span(session(s), &kb, &hb, &room);                          \
+            if (st != RSV_OK) {                                                                       \
+                throw_status(env, st);                                                                \
+                return;                                                                               \
+            }                                                                                         \
+            const jint c = room < (int64_t)(n - done) ? (jint)room : n - done;                        \
+            (*env)->GET(env, keys, done, c, kb);                                                      \
+            if (hb && hashes) (*env)->GetLongArrayRegion(env, hashes, done, c, (jlong*)hb);           \
+            if ((*env)->ExceptionCheck(env)) return; /* bounds: nothing committed for this span */    \
+            if (hb && !hashes) {                                                                      \
+                throw_status(env, RSV_E_NULL_POINTER);                                                \
+                return;                                                                               \
+            }                                                                                         \
+            rsv_jvm_stage_advance(session(s), c);                                                     \
+            done += c;                                                                                \
+        }                                                                                             \
+    }
 
-JNIEXPORT void JNICALL JNI_FN(sampleInts)(JNIEnv* env, jobject self, jlong s, jintArray keys, jlongArray hashes,
-                                           jint n) {
-    (void)self;
-    jint* k = (jint*)(*env)->GetPrimitiveArrayCritical(env, keys, NULL);
-    jlong* h = hashes ? (jlong*)(*env)->GetPrimitiveArrayCritical(env, hashes, NULL) : NULL;
-    rsv_status st = rsv_jvm_sample_array(session(s), k, (const int64_t*)h, n);
-    if (h) (*env)->ReleasePrimitiveArrayCritical(env, hashes, h, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, keys, k, JNI_ABORT);
-    if (st != RSV_OK) throw_status(env, st);
-}
+SAMPLE_ARRAY(sampleLongs, jlongArray, GetLongArrayRegion)
+SAMPLE_ARRAY(sampleInts, jintArray, GetIntArrayRegion)
 
 /* Sampler.result (Sampler.scala:59-60): fills `out` (length >= k) and returns the sample size;
- * a single-use sampler's handle is destroyed here (never touched again) */
-JNIEXPORT jint JNICALL JNI_FN(resultLongs)(JNIEnv* env, jobject self, jlong s, jlongArray out) {
-    (void)self;
-    int64_t n = 0;
-    jlong* o = (jlong*)(*env)->GetPrimitiveArrayCritical(env, out, NULL);
-    rsv_status st = rsv_jvm_result(session(s), o, (*env)->GetArrayLength(env, out), &n);
-    (*env)->ReleasePrimitiveArrayCritical(env, out, o, 0);
-    if (st != RSV_OK) throw_status(env, st);
-    return (jint)n;
-}
+ * a single-use sampler's handle is destroyed here (never touched again).  The engine writes into a
+ * native buffer (its result may wait on the GPU or run the ordered replay: no pinned array), then
+ * Set<Type>ArrayRegion copies it out. */
+#define RESULT_ARRAY(NAME, JARR, JT, SET)                                                 \
+    JNIEXPORT jint JNICALL JNI_FN(NAME)(JNIEnv * env, jobject self, jlong s, JARR out) {  \
+        (void)self;                                                                      \
+        const jsize len = (*env)->GetArrayLength(env, out);                              \
+        JT* buf = (JT*)malloc((size_t)(len > 0 ? len : 1) * sizeof(JT));                 \
+        if (!buf) {                                                                      \
+            throw_status(env, RSV_E_OUT_OF_MEMORY);                                      \
+            return 0;                                                                    \
+        }                                                                                \
+        int64_t n = 0;                                                                   \
+        rsv_status st = rsv_jvm_result(session(s), buf, len, &n);                        \
+        if (st == RSV_OK) (*env)->SET(env, out, 0, (jsize)n, buf);                       \
+        free(buf);                                                                       \
+        if (st != RSV_OK) throw_status(env, st);                                         \
+        return (jint)n;                                                                  \
+    }
 
-JNIEXPORT jint JNICALL JNI_FN(resultInts)(JNIEnv* env, jobject self, jlong s, jintArray out) {
-    (void)self;
-    int64_t n = 0;
-    jint* o = (jint*)(*env)->GetPrimitiveArrayCritical(env, out, NULL);
-    rsv_status st = rsv_jvm_result(session(s), o, (*env)->GetArrayLength(env, out), &n);
-    (*env)->ReleasePrimitiveArrayCritical(env, out, o, 0);
-    if (st != RSV_OK) throw_status(env, st);
-    return (jint)n;
-}
+RESULT_ARRAY(resultLongs, jlongArray, jlong, SetLongArrayRegion)
+RESULT_ARRAY(resultInts, jintArray, jint, SetIntArrayRegion)
 
 /* Sampler.isOpen (Sampler.scala:67): no downcall into the engine */
 JNIEXPORT jboolean JNICALL JNI_FN(isOpen)(JNIEnv* env, jobject self, jlong s) {
@@ -122,7 +134,8 @@ JNIEXPORT jboolean JNICALL JNI_FN(isOpen)(JNIEnv* env, jobject self, jlong s) {
     return rsv_jvm_is_open(session(s)) ? JNI_TRUE : JNI_FALSE;
 }
 
-/* release (the JVM Cleaner, exactly once): destroys a live handle, frees the session */
+/* release (JniSession.release, exactly once: a single-use result() or the phantom-reference cleaner):
+ * destroys a live handle, frees the session */
 JNIEXPORT void JNICALL JNI_FN(destroy)(JNIEnv* env, jobject self, jlong s) {
     (void)env;
     (void)self;

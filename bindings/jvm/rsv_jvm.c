@@ -69,6 +69,21 @@ rsv_status rsv_jvm_sample(rsv_jvm* s, const void* key, int64_t hash) {
     return RSV_OK;
 }
 
+rsv_status rsv_jvm_stage_span(rsv_jvm* s, void** keys_out, int64_t** hashes_out, int64_t* room) {
+    g_local_error = 0;
+    if (!s->open) return closed();
+    if (s->filled == s->cap) {
+        rsv_status st = next_stage(s);
+        if (st != RSV_OK) return st;
+    }
+    *keys_out = s->stage + s->filled * s->key_width;
+    *hashes_out = s->precomputed ? s->stage_hash + s->filled : 0;
+    *room = s->cap - s->filled;
+    return RSV_OK;
+}
+
+void rsv_jvm_stage_advance(rsv_jvm* s, int64_t n) { s->filled += n; }
+
 rsv_status rsv_jvm_sample_array(rsv_jvm* s, const void* keys, const int64_t* hashes, int64_t n) {
     g_local_error = 0;
     if (!s->open) return closed();
@@ -81,16 +96,16 @@ rsv_status rsv_jvm_sample_array(rsv_jvm* s, const void* keys, const int64_t* has
         return RSV_E_NULL_POINTER;
     }
     const uint8_t* src = (const uint8_t*)keys;
-    while (n > 0) {
-        if (s->filled == s->cap) {
-            rsv_status st = next_stage(s);
-            if (st != RSV_OK) return st;
-        }
-        int64_t c = s->cap - s->filled;
-        if (c > n) c = n;
-        memcpy(s->stage + s->filled * s->key_width, src, (size_t)(c * s->key_width));
-        if (s->precomputed) memcpy(s->stage_hash + s->filled, hashes, (size_t)c * 8);
-        s->filled += c;
+    while (n > 0) {  /* the JNI shim runs this same loop with Get<Type>ArrayRegion as the copy */
+        void* kb = 0;
+        int64_t* hb = 0;
+        int64_t room = 0;
+        rsv_status st = rsv_jvm_stage_span(s, &kb, &hb, &room);
+        if (st != RSV_OK) return st;
+        const int64_t c = room < n ? room : n;
+        memcpy(kb, src, (size_t)(c * s->key_width));
+        if (hb) memcpy(hb, hashes, (size_t)c * 8);
+        rsv_jvm_stage_advance(s, c);
         src += c * s->key_width;
         if (hashes) hashes += c;
         n -= c;

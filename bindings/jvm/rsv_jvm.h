@@ -3,7 +3,7 @@
  *
  * This is the per-call logic of the JNI shim (bindings/jni/reservoir_jni.c calls these functions
  * and nothing else) and, statement for statement, of the Panama FFM binding
- * (bindings/scala/lgbt/princess/reservoir/gpu/GpuSampler.scala).  It has no JNI types, so the
+ * (bindings/scala/ffm/lgbt/princess/reservoir/gpu/ffm/FfmSampler.scala).  It has no JNI types, so the
  * exact call sequence a JVM drives is compiled and run on the GPU without a JDK
  * (tests/cpp/test_ffm_sequence.cpp, tests/test_gpu_ffm.py).
  *
@@ -43,6 +43,11 @@ rsv_status rsv_jvm_create(rsv_jvm* s, const rsv_config* cfg);
 rsv_status rsv_jvm_sample(rsv_jvm* s, const void* key, int64_t hash);
 /* Sampler.sampleAll over a primitive array (S:49-50): n keys (+ n hashes when precomputed) */
 rsv_status rsv_jvm_sample_array(rsv_jvm* s, const void* keys, const int64_t* hashes, int64_t n);
+/* the free tail of the pinned staging (the next buffer once this one is full: that commit may wait
+ * for the GPU, so a JNI caller must hold no array pinned here): room for *room keys (+ hashes for
+ * RSV_HASH_PRECOMPUTED, else *hashes_out = NULL); rsv_jvm_stage_advance(n) records n keys written */
+rsv_status rsv_jvm_stage_span(rsv_jvm* s, void** keys_out, int64_t** hashes_out, int64_t* room);
+void rsv_jvm_stage_advance(rsv_jvm* s, int64_t n);
 /* Sampler.result (S:59-60): writes min(count, k) keys; a single-use sampler closes (S:345-350) */
 rsv_status rsv_jvm_result(rsv_jvm* s, void* out, int64_t cap, int64_t* out_n);
 /* zero-copy form for a producer that writes keys itself (keys-only samplers): the free tail of

@@ -6,11 +6,31 @@ import scala.reflect.ClassTag
 
 import lgbt.princess.reservoir.Sampler
 
+/** What a binding provides: a GPU sampler for one factory call.  The JNI binding lives in `core`
+  * (JDK 8+); the Panama FFM one (JDK 22+, `java.lang.foreign`) is a separate sbt module
+  * (`reservoir-gpu-ffm`, INTEGRATION.md) that `Backend` loads by name, so `core` itself never
+  * references `java.lang.foreign` and still compiles on the reference's CI JDKs 8/11/15 under
+  * `-Xlint -Werror` (build.sbt:37-42, :129-133). */
+private[reservoir] trait SamplerFactory {
+  def make[A, B](kind: Int, k: Int, reusable: Boolean, keys: KeyKind[B], hashKind: Int, engine: Int, seed: Long)(
+      map: A => B,
+      hash: B => Long,
+  ): Sampler[A, B]
+}
+
+private[reservoir] object JniFactory extends SamplerFactory {
+  def make[A, B](kind: Int, k: Int, reusable: Boolean, keys: KeyKind[B], hashKind: Int, engine: Int, seed: Long)(
+      map: A => B,
+      hash: B => Long,
+  ): Sampler[A, B] = new JniSampler[A, B](kind, k, reusable, keys, hashKind, engine, seed)(map, hash)
+}
+
 /** Backend selection behind the unchanged factories `Sampler.apply` / `Sampler.distinct`
   * (Sampler.scala:128-136, :171-180; SURVEY.md section 5 "Config / flags"): no signature changes.
   *
   *   -Dreservoir.backend=gpu        use the MI355X engine for B = Long or Int (else the JVM classes)
-  *   -Dreservoir.binding=ffm|jni    default: FFM on JDK 22+, JNI below
+  *   -Dreservoir.binding=ffm|jni    default: FFM when the JDK is 22+ and the reservoir-gpu-ffm jar is
+  *                                  on the class path, JNI otherwise
   *   -Dreservoir.engine=java_l      the reference's Algorithm L over java.util.Random, bit-identical
   *                                  to the JVM sampler for the same seed (default philox_r: Algorithm R)
   *
@@ -18,12 +38,28 @@ import lgbt.princess.reservoir.Sampler
   * SampleImpl.scala:10), so `Sample(k)(map)` picks the backend through `Sampler.apply`. */
 private[reservoir] object Backend {
   private[this] val enabled = System.getProperty("reservoir.backend", "cpu") == "gpu"
-  private[this] val ffm = System.getProperty("reservoir.binding") match {
-    case "ffm" => true
-    case "jni" => false
-    case _ =>
-      val v = System.getProperty("java.specification.version", "1.8")
-      !v.startsWith("1.") && v.toInt >= 22
+  private[this] val FfmFactoryClass = "lgbt.princess.reservoir.gpu.ffm.FfmFactory"
+
+  /** The FFM factory, loaded reflectively: absent module or pre-22 JDK -> JNI. */
+  private[this] lazy val factory: SamplerFactory = {
+    val wantFfm = System.getProperty("reservoir.binding") match {
+      case "ffm" => true
+      case "jni" => false
+      case _ =>
+        val v = System.getProperty("java.specification.version", "1.8")
+        !v.startsWith("1.") && v.toInt >= 22
+    }
+    if (!wantFfm) JniFactory
+    else
+      try Class.forName(FfmFactoryClass).getDeclaredConstructor().newInstance().asInstanceOf[SamplerFactory]
+      catch {
+        case _: ReflectiveOperationException | _: LinkageError =>
+          if (System.getProperty("reservoir.binding") == "ffm")
+            throw new UnsupportedOperationException(
+              s"-Dreservoir.binding=ffm needs JDK 22+ and $FfmFactoryClass (reservoir-gpu-ffm) on the class path"
+            )
+          JniFactory
+      }
   }
   private[this] val engine = if (System.getProperty("reservoir.engine", "") == "java_l") Abi.EngineJavaL else Abi.EnginePhiloxR
   private[this] val seeds  = new SecureRandom() // a fresh seed per sampler, like `new Random()` (Sampler.scala:199)
@@ -33,8 +69,7 @@ private[reservoir] object Backend {
       hash: B => Long,
   ): Sampler[A, B] = {
     val seed = seeds.nextLong()
-    if (ffm) FfmFactory.make[A, B](kind, k, reusable, keys, hashKind, engine, seed)(map, hash)
-    else new JniSampler[A, B](kind, k, reusable, keys, hashKind, engine, seed)(map, hash)
+    factory.make[A, B](kind, k, reusable, keys, hashKind, engine, seed)(map, hash)
   }
 
   /** Sampler.apply (validation already done by validateNonDistinctParams). */

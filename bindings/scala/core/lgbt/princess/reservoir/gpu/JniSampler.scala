@@ -1,12 +1,17 @@
 package lgbt.princess.reservoir.gpu
 
+import java.lang.ref.{PhantomReference, ReferenceQueue}
 import java.util.Arrays
+import java.util.concurrent.ConcurrentHashMap
 
 import scala.collection.immutable.ArraySeq
 
 import lgbt.princess.reservoir.Sampler
 
 /** JNI natives of bindings/jni/reservoir_jni.c, for the reference's CI JDKs 8/11/15 (build.sbt:37-42).
+  * No native call holds a JVM array pinned while the engine may wait: keys are copied with
+  * Get<Type>ArrayRegion straight into the engine's pinned staging, results come back through a
+  * native buffer and Set<Type>ArrayRegion.
   * A session is a native rsv_jvm (bindings/jvm/rsv_jvm.h) held as a Long. */
 private[reservoir] object Jni {
   System.loadLibrary("reservoir_jni")
@@ -35,6 +40,50 @@ private[reservoir] object Jni {
   @native def stageCommit(session: Long, n: Long): Unit
 }
 
+/** One native session (a malloc'd rsv_jvm, reservoir_jni.c) released exactly once: by a single-use
+  * `result()`, or by [[JniCleaner]] once its sampler is unreachable. */
+private[gpu] final class JniSession(initial: Long) {
+  @volatile private[this] var ptr = initial
+  def get: Long = ptr
+  def release(): Unit = synchronized {
+    if (ptr != 0L) {
+      Jni.destroy(ptr)
+      ptr = 0L
+    }
+  }
+}
+
+/** JDK 8 has no java.lang.ref.Cleaner and `finalize()` is deprecated since JDK 9 (an error under
+  * -Xlint -Werror on the reference's newer CI JDKs): a phantom reference per sampler on one queue,
+  * drained by a daemon thread that releases the session.  The reference holds the session, never
+  * the sampler, so the sampler can become unreachable. */
+private[gpu] object JniCleaner {
+  private final class Ref(owner: AnyRef, val session: JniSession, q: ReferenceQueue[AnyRef])
+      extends PhantomReference[AnyRef](owner, q)
+
+  private[this] val queue = new ReferenceQueue[AnyRef]
+  private[this] val live  = ConcurrentHashMap.newKeySet[Ref]() // the Refs themselves must stay reachable
+
+  private[this] val thread = {
+    val t = new Thread(new Runnable {
+      def run(): Unit =
+        while (true) {
+          val r = queue.remove().asInstanceOf[Ref]
+          live.remove(r)
+          r.session.release()
+        }
+    }, "reservoir-jni-cleaner")
+    t.setDaemon(true)
+    t.start()
+    t
+  }
+
+  def register(owner: AnyRef, session: JniSession): Unit = {
+    live.add(new Ref(owner, session, queue))
+    ()
+  }
+}
+
 /** A GPU-backed `Sampler[A, B]` over JNI, B = Long or Int: keys are buffered in a JVM array and handed
   * over 65536 at a time (one JNI call per batch, none per element); the native session copies them
   * into the engine's pinned staging buffer.  Lifecycle as FfmSampler: `isOpen` tracked here, the
@@ -52,8 +101,9 @@ private[reservoir] final class JniSampler[A, B](
   private[this] final val Batch = 65536
   private[this] val isLong      = keys.width == 8
   private[this] val precomputed = kind == Abi.KindDistinct && hashKind == Abi.HashPrecomputed
-  private[this] var session =
-    Jni.create(kind, maxSampleSize, keys.width, reusable, engine, hashKind, Abi.OrderAuto, seed, 0L, -1)
+  private[this] val session =
+    new JniSession(Jni.create(kind, maxSampleSize, keys.width, reusable, engine, hashKind, Abi.OrderAuto, seed, 0L, -1))
+  JniCleaner.register(this, session)
   private[this] val longs  = if (isLong) new Array[Long](Batch) else null
   private[this] val ints   = if (isLong) null else new Array[Int](Batch)
   private[this] val hashes = if (precomputed) new Array[Long](Batch) else null
@@ -62,7 +112,7 @@ private[reservoir] final class JniSampler[A, B](
 
   private[this] def flush(): Unit =
     if (n > 0) {
-      if (isLong) Jni.sampleLongs(session, longs, hashes, n) else Jni.sampleInts(session, ints, hashes, n)
+      if (isLong) Jni.sampleLongs(session.get, longs, hashes, n) else Jni.sampleInts(session.get, ints, hashes, n)
       n = 0
     }
 
@@ -81,27 +131,19 @@ private[reservoir] final class JniSampler[A, B](
     val res =
       if (isLong) {
         val out = new Array[Long](maxSampleSize)
-        val m   = Jni.resultLongs(session, out)
+        val m   = Jni.resultLongs(session.get, out)
         ArraySeq.unsafeWrapArray(if (m == out.length) out else Arrays.copyOf(out, m))
       } else {
         val out = new Array[Int](maxSampleSize)
-        val m   = Jni.resultInts(session, out)
+        val m   = Jni.resultInts(session.get, out)
         ArraySeq.unsafeWrapArray(if (m == out.length) out else Arrays.copyOf(out, m))
       }
     if (!reusable) { // the native side destroyed the handle inside result(); free the session now
       open = false
-      Jni.destroy(session)
-      session = 0L
+      session.release()
     }
     res.asInstanceOf[IndexedSeq[B]]
   }
 
   def isOpen: Boolean = open
-
-  // JDK 8 has no java.lang.ref.Cleaner: a reusable sampler's session goes with the object
-  override protected def finalize(): Unit =
-    if (session != 0L) {
-      Jni.destroy(session)
-      session = 0L
-    }
 }

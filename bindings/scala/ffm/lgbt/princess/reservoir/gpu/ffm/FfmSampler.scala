@@ -1,4 +1,7 @@
-package lgbt.princess.reservoir.gpu
+package lgbt.princess.reservoir.gpu.ffm
+
+// JDK 22+ only: the separate sbt module reservoir-gpu-ffm (INTEGRATION.md), loaded by gpu.Backend
+// through Class.forName, so the core module never links java.lang.foreign.
 
 import java.lang.foreign.{Arena, FunctionDescriptor, Linker, MemoryLayout, MemorySegment, StructLayout, SymbolLookup}
 import java.lang.foreign.ValueLayout.{ADDRESS, JAVA_INT, JAVA_LONG}
@@ -8,6 +11,7 @@ import java.lang.ref.Cleaner
 import scala.collection.immutable.ArraySeq
 
 import lgbt.princess.reservoir.Sampler
+import lgbt.princess.reservoir.gpu.{Abi, KeyKind, SamplerFactory}
 
 /** Panama FFM downcall handles of libreservoir_hip.so (JDK 22+, run with --enable-native-access).
   * Names carry an `rsv` prefix so nothing here shadows a Sampler member (e.g. `isOpen`). */
@@ -161,8 +165,10 @@ private[reservoir] final class FfmSampler[A, B](
   def isOpen: Boolean = open
 }
 
-/** Loaded only when the FFM binding is selected (Backend), so JDK 8-21 never resolves java.lang.foreign. */
-private[reservoir] object FfmFactory {
+/** Instantiated by gpu.Backend with Class.forName(...).getDeclaredConstructor().newInstance(): a class
+  * with a no-argument constructor (private[reservoir] is public in bytecode).  Only this module
+  * resolves java.lang.foreign. */
+private[reservoir] final class FfmFactory extends SamplerFactory {
   def make[A, B](kind: Int, k: Int, reusable: Boolean, keys: KeyKind[B], hashKind: Int, engine: Int, seed: Long)(
       map: A => B,
       hash: B => Long,

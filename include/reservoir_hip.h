@@ -205,6 +205,9 @@ typedef struct rsv_distinct_info {
     int64_t  size;         /* set size */
     int64_t  max_hash;     /* the set's largest scrambled hash (INT64_MIN when empty) */
     int64_t  log_entries;  /* ordered: upper bound on rsv_export_log's count */
+    int64_t  sched_passes;    /* ordered: batches taken by one verified scheduled pass */
+    int64_t  sched_fallbacks; /* ordered: scheduled passes that failed verification or overflowed and
+                               * left the batch to the chunk loop (the set restored) */
 } rsv_distinct_info;
 rsv_status rsv_get_distinct_info(rsv_sampler* s, rsv_distinct_info* out);
 /* Every logged candidate with scrambled hash < bound (all of them for bound = INT64_MAX), in

@@ -59,6 +59,8 @@ class RsvDistinctInfo(C.Structure):
         ("size", C.c_int64),
         ("max_hash", C.c_int64),
         ("log_entries", C.c_int64),
+        ("sched_passes", C.c_int64),
+        ("sched_fallbacks", C.c_int64),
     ]
 
 

@@ -1163,6 +1163,7 @@ struct DistinctState {
     bool arch_ok = true;
     std::vector<Seg> pre_segs;
     bool merged = false;
+    int64_t sched_passes = 0, sched_fallbacks = 0;  // rsv_distinct_info counters
 };
 
 // ~2 GB of host archive (16 B per candidate): beyond it rsv_export_log reports the log as not retained
@@ -2050,13 +2051,16 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
                      (long long)hv[7], (long long)k);
     if (c > cap || hv[1]) {  // buffer or bucket overflow: nothing was merged; the counts were not consumed
         STRY(hipMemsetAsync(d->sctl + kCtlWords, 0, (size_t)kCountStride * 4 * B, st));
+        ++d->sched_fallbacks;
         return RSV_OK;
     }
     if (hv[6] >= 0) {  // a predicted bound was too tight: put the set back, the chunk loop redoes the batch
         STRY(hipMemcpyAsync(d->set_h, d->bak_h, (size_t)k * 8, hipMemcpyDeviceToDevice, st));
         STRY(hipMemcpyAsync(d->set_k, d->bak_k, (size_t)k * kw, hipMemcpyDeviceToDevice, st));
+        ++d->sched_fallbacks;
         return RSV_OK;
     }
+    ++d->sched_passes;
     const int64_t old_max = d->max_h;
     d->m = std::min<int64_t>(hv[2], k);
     d->set_top = hv[3];
@@ -2229,7 +2233,9 @@ int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStre
 }
 
 void distinct_info(const DistinctState* d, int32_t* ordered, int32_t* tied, int32_t* retained, int64_t* size,
-                   int64_t* max_hash, int64_t* log_entries) {
+                   int64_t* max_hash, int64_t* log_entries, int64_t* sched_passes, int64_t* sched_fallbacks) {
+    *sched_passes = d->sched_passes;
+    *sched_fallbacks = d->sched_fallbacks;
     *ordered = d->ordered;
     *tied = d->m == d->k && d->over;
     *retained = d->ordered && d->arch_ok;

@@ -165,7 +165,7 @@ int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStre
 int distinct_merge_parts(DistinctState* d, const void* keys_dev, const int64_t* hash_dev, const int64_t* part_n,
                          int32_t parts, int64_t part_len, hipStream_t st);
 void distinct_info(const DistinctState* d, int32_t* ordered, int32_t* tied, int32_t* retained, int64_t* size,
-                   int64_t* max_hash, int64_t* log_entries);
+                   int64_t* max_hash, int64_t* log_entries, int64_t* sched_passes, int64_t* sched_fallbacks);
 // ordered samplers: every logged candidate with h < bound (all of them for bound = INT64_MAX) in
 // arrival order into host buffers; the exact replay of a concatenated candidate run
 int distinct_log_export(DistinctState* d, int64_t bound, int64_t* out_h, void* out_k, int64_t cap, int64_t* out_n,

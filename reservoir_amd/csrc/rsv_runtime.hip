@@ -950,7 +950,7 @@ rsv_status rsv_get_distinct_info(rsv_sampler* s, rsv_distinct_info* out) {
     touch(s);
     if (rsv_status st = flush_stage(s)) return st;
     distinct_info(s->distinct, &out->ordered, &out->tied, &out->log_retained, &out->size, &out->max_hash,
-                  &out->log_entries);
+                  &out->log_entries, &out->sched_passes, &out->sched_fallbacks);
     return RSV_OK;
 }
 

@@ -205,9 +205,9 @@ class GpuSampler:
     def sample_all(self, elements: Iterable) -> None:
         """Sampler.sampleAll (Sampler.scala:49-50): same result as sample() on each element."""
         if _is_torch_cuda(elements) and self._map is identity and not self._precomputed:
-            # device fast path: rsv_sample_batch itself raises IllegalStateException on a closed
-            # sampler (check_open, same message) before it touches the stream or the keys
-            if self._h is None:  # closed: the handle is gone
+            # device fast path; checkOpen() first, as the reference does before any other work
+            # (Sampler.scala:186, :417-419): a single-use sampler closed by result() keeps its handle
+            if self._h is None or not self._L.rsv_is_open(self._h):
                 raise IllegalStateException("use of sampler after calling `result()`")
             torch = _torch()
             t = elements if elements.is_contiguous() else elements.contiguous()

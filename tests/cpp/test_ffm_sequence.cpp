@@ -1,7 +1,7 @@
 // test_ffm_sequence.cpp -- replays, on the GPU and without a JDK, exactly the call sequences the two
 // JVM bindings drive:
 //   ffm   FfmMirror below: statement for statement the Panama FFM binding
-//         bindings/scala/lgbt/princess/reservoir/gpu/FfmSampler.scala over the raw C ABI
+//         bindings/scala/ffm/lgbt/princess/reservoir/gpu/ffm/FfmSampler.scala over the raw C ABI
 //         (stage_acquire / commit per ~1 Mi keys, open tracked on the JVM side, the single-use
 //         result() destroys the handle and nothing touches it afterwards)
 //   jni   bindings/jvm/rsv_jvm.c, the session logic every JNI native method of

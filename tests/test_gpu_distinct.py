@@ -479,6 +479,13 @@ def test_ordered_scheduled_pass(cuda, oracle, monkeypatch, k, n, seed, batches):
         d = Sampler.distinct(k, seed=17)()
         for a, b in zip(cuts[:-1], cuts[1:]):
             d.sample_all(vals[a:b])
+        info = d.distinct_info()  # which path ran (the fallbacks are silent otherwise)
+        if not env:
+            assert info["sched_passes"] >= 1 and info["sched_fallbacks"] == 0, info
+        elif "RSV_ORDERED_SCHED" in env:
+            assert info["sched_passes"] == 0 and info["sched_fallbacks"] == 0, info
+        else:
+            assert info["sched_fallbacks"] >= 1, info
         assert d.result().tolist() == want, env
         for key in env:
             monkeypatch.delenv(key)

@@ -131,6 +131,14 @@ def test_single_use_lifecycle(cuda):
         s.sample(1)  # :246-250
     with pytest.raises(IllegalStateException):
         s.result()  # :252-256
+    # the device fast path checks open first (Sampler.scala:186): a closed sampler raises
+    # IllegalStateException even for a tensor it would reject on dtype
+    import torch
+
+    with pytest.raises(IllegalStateException):
+        s.sample_all(torch.zeros(8, dtype=torch.int32, device=cuda))
+    with pytest.raises(IllegalStateException):
+        s.sample_all(torch.zeros(8, dtype=torch.int64, device=cuda))
 
 
 def test_reusable_does_not_clobber(cuda):

@@ -9,8 +9,9 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("k", [1, 5, 64, 100, 1024])
+@pytest.mark.parametrize("k", [1, 5, 64, 100, 1024, 3000, 4400])
 def test_ragged_parity(cuda, oracle, k):
+    """k = 3000 / 4400: the winner table exceeds 64 KB of dynamic LDS (k2::lds_bytes)."""
     import torch
 
     from reservoir_amd import batch
@@ -65,6 +66,29 @@ def test_long_streams_sparse_region(cuda, oracle, k):
                                       seed=5, stream_base=2**40 + 3)
     assert np.array_equal(cnt.cpu().numpy(), wcnt)
     assert np.array_equal(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("k", [64, 1000])
+def test_streams_past_2pow27(cuda, oracle, k):
+    """Streams of >= 2^27 keys take K2's 64-bit path (u64 LDS winner table, full Philox counter
+    words, 64-bit index rebuild in resolve_round).  keys = arange, so each output key is its global
+    index: segment s must hold offset_s + the oracle's last writer of every slot."""
+    import torch
+
+    from reservoir_amd import batch
+
+    lens = [(1 << 27) + 12_345, 1000, (1 << 27) + 1]
+    offs = np.r_[0, np.cumsum(lens)].astype(np.int64)
+    keys = torch.arange(int(offs[-1]), dtype=torch.int64, device=cuda)
+    out, cnt = batch.sample_segmented(keys, torch.from_numpy(offs).to(cuda), k, seed=41, stream_base=9)
+    out = out.cpu().numpy().reshape(len(lens), k)
+    assert cnt.cpu().numpy().tolist() == [k] * len(lens)
+    for s, n in enumerate(lens):
+        win = oracle.algo_r_last_writers(41, 9 + s, k, 0, n)
+        assert (win >= 0).all()
+        assert np.array_equal(out[s], offs[s] + win), s
+    del keys
+    torch.cuda.empty_cache()
 
 
 def test_int32_keys(cuda, oracle):
