@@ -278,10 +278,20 @@ class GpuSampler:
 
     def result_device(self, out_tensor) -> int:
         """Write the result into a device tensor (no host round trip); returns its length."""
+        self._order_after_torch(out_tensor)
         n = C.c_int64(0)
         N.check(self._L.rsv_result_device(self._h, C.c_void_p(out_tensor.data_ptr()),
                                           out_tensor.numel(), C.byref(n)))
         return n.value
+
+    def _order_after_torch(self, t) -> None:
+        """Device tensors handed to the engine were written (or allocated and filled) by torch on
+        its current stream; unless this handle runs on that stream, wait for it first -- the
+        engine's own stream is not ordered after torch's."""
+        if _is_torch_cuda(t):
+            torch = _torch()
+            if _current_raw_stream(torch, t) != self._stream:
+                torch.cuda.current_stream(t.device).synchronize()
 
     # -- multi-GPU helpers (reservoir_amd.distributed) ------------------------------------------
     @property
@@ -314,6 +324,7 @@ class GpuSampler:
         else:
             keys = torch.zeros(self._k, dtype=torch.int64 if self._width == 8 else torch.int32, device=device)
         hashes = torch.zeros(self._k, dtype=torch.int64, device=device)
+        self._order_after_torch(hashes)
         n = C.c_int64(0)
         N.check(self._L.rsv_export_state(self._h, C.c_void_p(idx.data_ptr()),
                                          C.c_void_p(keys.data_ptr()), C.c_void_p(hashes.data_ptr()),
@@ -323,12 +334,14 @@ class GpuSampler:
     def export_packed(self, row) -> None:
         """Element samplers: write ``[idx(k) | keys as int64 (k)]`` into the int64 device tensor
         ``row`` (one kernel, stream-ordered on a caller stream)."""
+        self._order_after_torch(row)
         N.check(self._L.rsv_export_packed(self._h, C.c_void_p(row.data_ptr())))
 
     def merge_packed(self, rows, total_count: int) -> None:
         """Element samplers: merge the packed rows of a ``[parts, width]`` int64 device tensor."""
         if rows.dim() != 2 or not rows.is_contiguous():
             raise IllegalArgumentException("rows must be a contiguous [parts, width] tensor")
+        self._order_after_torch(rows)
         N.check(self._L.rsv_merge_packed(self._h, C.c_void_p(rows.data_ptr()), int(rows.shape[0]),
                                          int(rows.shape[1]), int(total_count)))
 
@@ -368,6 +381,7 @@ class GpuSampler:
     def merge_state(self, idx, keys, hashes, part_n, total_count: int) -> None:
         """Merge gathered partial states ([parts, k] device tensors) into this sampler."""
         parts = int(keys.shape[0])
+        self._order_after_torch(keys)
         pn = np.ascontiguousarray(np.asarray(part_n, dtype=np.int64))
         N.check(self._L.rsv_merge_state(
             self._h, C.c_void_p(idx.data_ptr()), C.c_void_p(keys.data_ptr()),
