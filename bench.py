@@ -2,7 +2,9 @@
 
 A step is one full pass of the hot path over the batch: a fresh Sampler (Sampler.apply, created
 and closed inside the step) samples the device-resident keys (K1 last-writer kernel + resolve),
-then result() brings the k-slot reservoir to the host.  With N GPUs the stream is N x 1e9 elements
+then result() brings the k-slot reservoir to the host.  Two steps are in flight (step t+1's
+sampling is queued on the stream before step t's result is read, so the host turnaround overlaps
+the GPU); the one-at-a-time figure is reported beside it ("serial"; --serial times that instead).  With N GPUs the stream is N x 1e9 elements
 split by index range (each rank seeks to its offset, weak scaling) and the per-rank reservoirs are
 combined with one all_gather + merge kernel inside the step.
 
@@ -321,6 +323,8 @@ def main() -> None:
     ap.add_argument("--time-every", type=int, default=8,
                     help="HIP events around every N-th K1 launch of the timed steps (1 = every launch); "
                          "each timed launch carries ~10 us of marker packets and host calls")
+    ap.add_argument("--serial", action="store_true",
+                    help="one step at a time (no second sampler in flight) for the timed steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the other hot-path configs (C3 segmented, C4 distinct, C2 on java_l, C5)")
@@ -365,17 +369,42 @@ def main() -> None:
 
     L = _native.load()
 
-    def step():
-        # a fresh Sampler per step (Sampler.apply): creation and close are inside the step
+    def issue():
+        # a fresh Sampler per step (Sampler.apply): creation and close are inside the step.  On the
+        # caller's stream sample_all and the combine are stream-ordered: nothing here waits
         s = Sampler(k, seed=args.seed, stream_id=args.stream_id, device=local)()
         s.set_stream(stream)
         s.seek(offset)
         s.sample_all(keys)
         if world > 1:
             D.combine(s, device=dev, total_count=n * world)
-        r = s.result()
+        return s
+
+    def finish(s):
+        r = s.result()  # waits for this step's published reservoir
         s.close()
         return r
+
+    def step():
+        return finish(issue())
+
+    def run_steps(count: int, depth: int):
+        """`count` steps; depth 2 keeps two samplers in flight: step t+1 is issued (its kernels queue
+        behind step t's on the stream) before step t's result() is read, so the host's result /
+        close / create turnaround overlaps the GPU's next step instead of idling it.  Every step
+        still creates its sampler, samples all keys, reads its result and closes."""
+        res, pending = None, None
+        for _ in range(count):
+            s = issue()
+            if depth == 1:
+                res = finish(s)
+                continue
+            if pending is not None:
+                res = finish(pending)
+            pending = s
+        if pending is not None:
+            res = finish(pending)
+        return res
 
     def profile_read():
         ms, cnt = C.c_double(), C.c_int64()
@@ -394,10 +423,9 @@ def main() -> None:
         t = torch.tensor([min(n_ramp, 10_000)], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         n_ramp = int(t.item())
-    for _ in range(min(n_ramp, 10_000)):
-        step()
-    for _ in range(args.warmup):
-        step()
+    depth = 1 if args.serial else 2
+    run_steps(min(n_ramp, 10_000), depth)
+    run_steps(args.warmup, depth)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -407,9 +435,7 @@ def main() -> None:
     # pair adds ~5 us of marker packets to its step, so by default one step in eight carries them.
     _native.check(L.rsv_profile_global(max(1, args.time_every)))
     t0 = time.perf_counter()
-    res = None
-    for _ in range(args.steps):
-        res = step()
+    res = run_steps(args.steps, depth)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -417,10 +443,23 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     _native.check(L.rsv_profile_global(0))
     k1_ms, k1_launches = profile_read()
+    # the same steps one at a time (issue -> result -> close, nothing in flight): reported beside
+    # the pipelined figure, same barrier / synchronize bracketing, not the headline
+    serial_steps = min(args.steps, 40)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    run_steps(serial_steps, 1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed_serial = time.perf_counter() - t1
+    if world > 1:
+        t = torch.tensor([elapsed, elapsed_serial], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, elapsed_serial = float(t[0].item()), float(t[1].item())
 
     k1_s = k1_ms / max(k1_launches, 1) / 1e3  # K1 launch time (HIP events on the launch stream)
     assert res is not None and res.size == k
@@ -470,6 +509,11 @@ def main() -> None:
             },
             "roofline": roof,
             "ranks_seen": dist.get_world_size() if world > 1 else 1,
+            "steps_in_flight": depth,
+            "serial": {"steps": serial_steps, "ms_per_step": round(elapsed_serial / serial_steps * 1e3, 4),
+                       "value": round(n * world * serial_steps / elapsed_serial / 1e9, 3),
+                       "what": "the same step run one at a time (result read and sampler closed before the "
+                               "next is created): the host turnaround between steps idles the GPU"},
         }
         if c4 is not None:
             line["c4"] = c4

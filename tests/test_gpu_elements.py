@@ -368,3 +368,52 @@ def test_seek_past_k_after_partial_fill(cuda, oracle):
         got = s.result()
         assert got.size == 100
         assert np.array_equal(got[:40], keys.astype(dt)) and (got[40:] == 0).all()
+
+
+def test_caller_stream_pipelined_samplers(cuda, oracle):
+    """On a caller stream every call is stream-ordered and returns without a host wait: a second
+    sampler queued behind the first (bench.py's two steps in flight), the next batch on the
+    handle, export_packed and result_device must all see the finished slots, and results read one
+    step late are each step's own.  keys = arange: each slot's key is its last writer's index."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    n1, n2, k, seed, sid = 200_000_000, 100_000_000, 1024, 77, 3
+    keys = torch.arange(n1 + n2, dtype=torch.int64, device=cuda)
+    stream = torch.cuda.current_stream().cuda_stream
+    want = oracle.algo_r_last_writers(seed, sid, k, 0, n1 + n2)
+    want1 = oracle.algo_r_last_writers(seed, sid, k, 0, n1)
+    a = Sampler(k, seed=seed, stream_id=sid, reusable=True)()  # result_device, then result()
+    a.set_stream(stream)
+    a.sample_all(keys[:n1])
+    b = Sampler(k, seed=seed, stream_id=sid)()  # queued behind a's work
+    b.set_stream(stream)
+    b.sample_all(keys[:n1])
+    a.sample_all(keys[n1:])
+    row = torch.empty(2 * k, dtype=torch.int64, device=cuda)
+    a.export_packed(row)
+    dev_out = torch.empty(k, dtype=torch.int64, device=cuda)
+    assert a.result_device(dev_out) == k
+    torch.cuda.synchronize()
+    assert np.array_equal(row[:k].cpu().numpy(), want)
+    assert np.array_equal(row[k:].cpu().numpy(), want)
+    assert np.array_equal(dev_out.cpu().numpy(), want)
+    assert np.array_equal(b.result(), want1)
+    assert np.array_equal(a.result(), want)
+    b.close()
+    a.close()
+    # pipelined single-use steps, results read one step late
+    pending = None
+    for step in range(6):
+        s = Sampler(k, seed=seed, stream_id=sid)()
+        s.set_stream(stream)
+        s.sample_all(keys[:n1])
+        if pending is not None:
+            assert np.array_equal(pending.result(), want1), step
+            pending.close()
+        pending = s
+    assert np.array_equal(pending.result(), want1)
+    pending.close()
+    del keys
+    torch.cuda.empty_cache()
