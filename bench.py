@@ -411,14 +411,19 @@ def main() -> None:
         _native.check(L.rsv_profile_global_read(C.byref(ms), C.byref(cnt)))
         return ms.value, cnt.value
 
-    # Device warm-up (untimed): under sustained load the K1 launch time falls as clocks ramp over
-    # the first ~30 ms; run steps for 0.2 s before the W warmup steps so the timed region sees the
-    # steady state.  Every step holds a collective at N>1, so all ranks run the same number of
-    # steps: the count comes from one timed step, agreed as the max over ranks.
-    t_w = time.perf_counter()
+    # Device warm-up (untimed): under sustained load the K1 launch time falls as clocks ramp (98-104
+    # -> 88-90 us over tens of ms, tools/probe_k1env.py); run steps for 0.3 s before the W warmup
+    # steps so the timed region sees the steady state.  Every step holds a collective at N>1, so
+    # all ranks run the same number of steps, agreed as the max over ranks.  The count comes from
+    # steps timed AFTER the first one: the first carries the one-time module load and pool
+    # allocations, and timed alone it shrank the ramp to a handful of steps (the timed region
+    # then ran K1 at ~96 us on a still-ramping clock).
     step()
     torch.cuda.synchronize()
-    n_ramp = max(1, int(0.2 / max(time.perf_counter() - t_w, 1e-4)))
+    t_w = time.perf_counter()
+    run_steps(8, 1)
+    torch.cuda.synchronize()
+    n_ramp = max(1, int(0.3 / max((time.perf_counter() - t_w) / 8, 1e-5)))
     if world > 1:
         t = torch.tensor([min(n_ramp, 10_000)], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
