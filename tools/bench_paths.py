@@ -29,7 +29,17 @@ from workloads import c4_data, hash_twins, splitmix_fill  # noqa: E402
 HBM = 8000.0
 
 
+def ramp(fn, seconds=0.3):
+    """Run fn back to back for `seconds` (untimed): VALU-bound launches run ~10 % slower until the
+    clock has ramped under sustained load (tools/probe_k1env.py)."""
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        fn()
+        torch.cuda.synchronize()
+
+
 def timed(fn, reps=5, warm=1):
+    ramp(fn)
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
@@ -53,7 +63,7 @@ def c3(dev):
     keys = torch.empty(n, dtype=torch.int64, device=dev)
     splitmix_fill(keys, 0)
     offs = torch.arange(0, n + 1, L, dtype=torch.int64, device=dev)
-    t = timed(lambda: batch.sample_segmented(keys, offs, k, seed=1), reps=5)
+    t = timed(lambda: batch.sample_segmented(keys, offs, k, seed=1), reps=9)
     l0, l1 = R.k2_calls(S, L, k)
     # the memory floor: K2 must fetch each stream's 64 winning keys, ~57 distinct random 128-B lines
     # of its 32 KB segment (7.5 GB per launch by FETCH_SIZE, profiles/r02).  Timed here as a plain
@@ -87,6 +97,16 @@ def c4(dev, hash_kind="identity", order="auto", twins=False, seed=7):
     torch.cuda.synchronize()
     L = _native.load()
     times, kern = [], []
+
+    def one():
+        mk = Sampler.distinct(k, seed=seed, order=order)
+        d = mk(hash=hash_kind) if hash_kind != "default" else mk()
+        d.sample_all(vals)
+        d.result()
+        d.close()
+
+    if not twins:
+        ramp(one, 0.2)
     # reps 1..4 timed end to end with the filter timer off (its events add marker packets and host
     # calls to the batch); one more rep with it on, for the filter launches and their time
     for rep in range(6):
