@@ -733,18 +733,16 @@ struct SchedSink {
     }
 };
 
-// the scheduled pass: files the set's members (tag 0) and every candidate (tag 1 + batch index)
-// into the merge buckets as it goes, and logs the candidates in arrival order for the replica
+// the scheduled pass: logs the candidates (with their batch index) for the merge and the replica.
+// The merge buckets are filled by sched_file after it: filed inside the pass, every candidate batch
+// held its wave on the bucket atomics between streaming loads (C4 share: 790 us with the filing,
+// 696 us without, rocprof kernel stats; sched_file takes the filing off the streaming path).
 template <typename KeyT, int HASH>
 __global__ __launch_bounds__(kBlock) void sched_filter(const KeyT* __restrict__ keys, const int64_t* __restrict__ hashes,
                                                        int64_t n, int64_t r0, int64_t r1, const SchedDev* __restrict__ sd,
                                                        int64_t* __restrict__ cand_h, KeyT* __restrict__ cand_k,
                                                        uint32_t* __restrict__ cand_i, int64_t* __restrict__ ctl,
-                                                       int64_t cap, const int64_t* __restrict__ set_h,
-                                                       const KeyT* __restrict__ set_k, int64_t m, int64_t* __restrict__ bh,
-                                                       KeyT* __restrict__ bk, uint32_t* __restrict__ bi,
-                                                       int32_t log_bmax, int64_t* __restrict__ bak_h,
-                                                       KeyT* __restrict__ bak_k) {
+                                                       int64_t cap, int32_t log_bmax) {
     __shared__ int64_t sb[kMaxRanges + 1], stt[kMaxRanges];
     // (the plan is NOT a kernel argument: 8192 workgroups reading ~1.6 KB of kernarg memory each
     // made the pass 709 -> 769 us; a device copy, read through L2, costs one small copy dispatch)
@@ -758,22 +756,43 @@ __global__ __launch_bounds__(kBlock) void sched_filter(const KeyT* __restrict__ 
         if (i < nr) stt[i] = sd->t[i];
     }
     __syncthreads();
+    RangeBound rb{sb, stt, 0, 0, 0};
+    k3_filter_body<KeyT, HASH, true>(keys, hashes, n, r0, r1, rb, cand_h, cand_k, (unsigned long long*)ctl, cap, cand_i);
+}
+
+// the scheduled merge's bucket filing, after the pass: the set's members (tag 0; backed up first,
+// restored if a bound fails verification) and the pass's logged candidates (tag 1 + batch index,
+// their count from the pass's counter ctl[0], at most cap).  Grid-stride over all of them.
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void sched_file(const SchedDev* __restrict__ sd, const int64_t* __restrict__ cand_h,
+                                                     const KeyT* __restrict__ cand_k, const uint32_t* __restrict__ cand_i,
+                                                     int64_t* __restrict__ ctl, int64_t cap, const int64_t* __restrict__ set_h,
+                                                     const KeyT* __restrict__ set_k, int64_t m, int64_t* __restrict__ bh,
+                                                     KeyT* __restrict__ bk, uint32_t* __restrict__ bi,
+                                                     int64_t* __restrict__ bak_h, KeyT* __restrict__ bak_k) {
+    __shared__ int64_t stt[kMaxRanges];
+    const int nr = sd->nr;
+    for (int i = threadIdx.x; i < nr; i += blockDim.x) stt[i] = sd->t[i];
+    __syncthreads();
     const uint32_t B_lo = sd->B_lo;
     const uint64_t q = sd->lo_mult;
     SchedSink<KeyT> sink{SchedMap{sd, stt, sd->B, B_lo, (uint32_t)nr, stt[nr - 1], q > UINT64_MAX / B_lo ? UINT64_MAX : q * B_lo},
                          bucket_count(ctl), bh, bk, bi, ctl + 1};
-    const int64_t per = (m + gridDim.x - 1) / gridDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * per + threadIdx.x; i < std::min<int64_t>(m, (int64_t)(blockIdx.x + 1) * per);
-         i += blockDim.x) {
-        const int64_t h = set_h[i];
-        const KeyT key = set_k[i];
-        bak_h[i] = h;  // the set before the pass (restored if a bound fails verification)
-        bak_k[i] = key;
-        sink.put(h, key, 0u);
+    const int64_t c = std::min<int64_t>((int64_t)__hip_atomic_load((const unsigned long long*)ctl, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT), cap);
+    const int64_t total = m + c, stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+        if (t < m) {
+            const int64_t h = set_h[t];
+            const KeyT key = set_k[t];
+            bak_h[t] = h;
+            bak_k[t] = key;
+            sink.put(h, key, 0u);
+        } else {
+            const int64_t e = t - m;
+            sink.put(cand_h[e], cand_k[e], cand_i[e] + 1u);
+        }
     }
-    RangeBound rb{sb, stt, 0, 0, 0};
-    k3_filter_body<KeyT, HASH, true>(keys, hashes, n, r0, r1, rb, cand_h, cand_k, (unsigned long long*)ctl, cap, cand_i,
-                                     &sink);
 }
 
 // the plan into device memory: one workgroup copies its by-value argument (the first, so it starts
@@ -1976,10 +1995,10 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
     {
         const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 32 + 1), 1), 256 * 32);
         KeyT* lk = (KeyT*)d->log_k + d->log_n;
-#define RSV_SCHED_FILTER(H)                                                                                             \
-    hipLaunchKernelGGL((sched_filter<KeyT, H>), dim3(grid), dim3(kBlock), 0, st, keys, hashes, n, d->r0, d->r1,       \
-                       (const SchedDev*)d->sdev, d->log_h + d->log_n, lk, d->log_i + d->log_n, d->sctl, cap, d->set_h,  \
-                       (const KeyT*)d->set_k, k, d->sbh, bk, d->sbi, d->log_bmax_s, d->bak_h, (KeyT*)d->bak_k)
+#define RSV_SCHED_FILTER(H)                                                                                        \
+    hipLaunchKernelGGL((sched_filter<KeyT, H>), dim3(grid), dim3(kBlock), 0, st, keys, hashes, n, d->r0, d->r1,      \
+                       (const SchedDev*)d->sdev, d->log_h + d->log_n, lk, d->log_i + d->log_n, d->sctl, cap,        \
+                       d->log_bmax_s)
         switch (d->hash_kind) {
         case kHashJavaLong: RSV_SCHED_FILTER(kHashJavaLong); break;
         case kHashJavaInt: RSV_SCHED_FILTER(kHashJavaInt); break;
@@ -1987,6 +2006,15 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
         default: RSV_SCHED_FILTER(kHashIdentity);
         }
 #undef RSV_SCHED_FILTER
+        STRY(hipGetLastError());
+        // one entry per thread (the count is on the device: sized for the buffer's capacity, idle
+        // threads exit): every bucket atomic in flight at once -- a 1024-workgroup grid-stride over
+        // ~1.1 M entries waited on ~4 atomics per thread in sequence (61 us)
+        const unsigned fgrid = (unsigned)std::min<int64_t>((k + cap + kBlock - 1) / kBlock, 16384);
+        hipLaunchKernelGGL(sched_file<KeyT>, dim3(fgrid), dim3(kBlock), 0, st, (const SchedDev*)d->sdev,
+                           (const int64_t*)(d->log_h + d->log_n), (const KeyT*)lk, (const uint32_t*)(d->log_i + d->log_n),
+                           d->sctl, cap, (const int64_t*)d->set_h, (const KeyT*)d->set_k, k, d->sbh, bk, d->sbi,
+                           d->bak_h, (KeyT*)d->bak_k);
         STRY(hipGetLastError());
     }
     if (d->timer) d->timer->mark(st);
