@@ -91,6 +91,46 @@ __device__ __forceinline__ u32x4 philox4x32_10_uniform_hi(uint32_t c0, uint32_t 
     return {c0v, c1v, c2v, c3v};
 }
 
+// Two philox4x32_10_uniform_hi calls (counters c0 and c0 + 64, same uniform words) with their
+// rounds interleaved in the source, so the two dependent chains issue alternately (a lone chain
+// leaves every other issue slot of the wave waiting on its previous round: K1 measured 89 -> 125 us
+// when the scheduler emitted the second call after the first).
+__device__ __forceinline__ void philox4x32_10_uniform_hi_x2(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                            uint32_t k0, uint32_t k1, u32x4& a, u32x4& b) {
+    const uint64_t p1u = (uint64_t)kPhiloxM1 * c2;
+    const uint32_t n0u = (uint32_t)(p1u >> 32) ^ c1 ^ k0;
+    const uint64_t pa = (uint64_t)kPhiloxM0 * c0;
+    const uint64_t pb = (uint64_t)kPhiloxM0 * c0 + (uint64_t)kPhiloxM0 * 64u;
+    const uint32_t da2 = xor3_key((uint32_t)(pa >> 32), c3, k1), db2 = xor3_key((uint32_t)(pb >> 32), c3, k1);
+    const uint32_t d1u = (uint32_t)p1u;
+    const uint32_t da3 = (uint32_t)pa, db3 = (uint32_t)pb;
+    const uint64_t q0u = (uint64_t)kPhiloxM0 * n0u;
+    const uint64_t qa = (uint64_t)kPhiloxM1 * da2, qb = (uint64_t)kPhiloxM1 * db2;
+    uint32_t a0 = (uint32_t)(qa >> 32) ^ (d1u ^ (k0 + kPhiloxW0)), b0 = (uint32_t)(qb >> 32) ^ (d1u ^ (k0 + kPhiloxW0));
+    uint32_t a2 = da3 ^ ((uint32_t)(q0u >> 32) ^ (k1 + kPhiloxW1)), b2 = db3 ^ ((uint32_t)(q0u >> 32) ^ (k1 + kPhiloxW1));
+    uint32_t a1 = (uint32_t)qa, b1 = (uint32_t)qb;
+    uint32_t a3 = (uint32_t)q0u, b3 = (uint32_t)q0u;
+#pragma unroll
+    for (int r = 2; r < 10; ++r) {
+        const uint64_t pa0 = (uint64_t)kPhiloxM0 * a0, pb0 = (uint64_t)kPhiloxM0 * b0;
+        const uint64_t pa1 = (uint64_t)kPhiloxM1 * a2, pb1 = (uint64_t)kPhiloxM1 * b2;
+        const uint32_t na0 = xor3_key((uint32_t)(pa1 >> 32), a1, k0 + (uint32_t)r * kPhiloxW0);
+        const uint32_t nb0 = xor3_key((uint32_t)(pb1 >> 32), b1, k0 + (uint32_t)r * kPhiloxW0);
+        const uint32_t na2 = xor3_key((uint32_t)(pa0 >> 32), a3, k1 + (uint32_t)r * kPhiloxW1);
+        const uint32_t nb2 = xor3_key((uint32_t)(pb0 >> 32), b3, k1 + (uint32_t)r * kPhiloxW1);
+        a0 = na0;
+        b0 = nb0;
+        a1 = (uint32_t)pa1;
+        b1 = (uint32_t)pb1;
+        a2 = na2;
+        b2 = nb2;
+        a3 = (uint32_t)pa0;
+        b3 = (uint32_t)pb0;
+    }
+    a = {a0, a1, a2, a3};
+    b = {b0, b1, b2, b3};
+}
+
 struct DrawKey {
     uint32_t k0, k1;  // Philox key = seed
     uint32_t s0, s1;  // Philox stream words (counter words 2, 3)

@@ -21,21 +21,23 @@ namespace {
 
 constexpr int kBlock = 256;
 
-// K1: grid-stride over level-0 blocks (16 indices each); one bit per block marks a zero byte, and
-// every 16 iterations the marked blocks go through the wave's LDS queue -- with their 16-bit
-// zero-byte fold, so a sparse-region resolve needs no level-0 recompute -- and the level-1 draws
-// run with all 64 lanes busy (rsv_scan.h k1_body_z).  Hits (k ln(n/k) of them) go straight to
-// global atomicMax on the k-slot winner table: 14k atomics per 1e9 indices at k = 1024.
+// K1: grid-stride over level-0 blocks (16 indices each), two per lane per iteration; one bit per
+// such pair marks a zero byte, and every 12 iterations the marked pairs go through the wave's LDS
+// queue -- with their 32-bit zero-byte fold, so a sparse-region resolve needs no level-0 recompute
+// -- and the level-1 draws run with all 64 lanes busy (rsv_scan.h k1_body_p).  Hits (k ln(n/k) of
+// them) go straight to global atomicMax on the k-slot winner table: 14k atomics per 1e9 indices at k = 1024.
 constexpr int kK1Unroll = 2;  // level-0 blocks per lane per iteration (two Philox chains in flight)
 
 constexpr unsigned kK1Grid = 256 * 12;
 
-// per-wave LDS of k1_body_z: block queue (< 64 waiting + one round of 64), the window's folds,
-// the per-candidate queue
+// per-wave LDS of k1_body_p: pair queue (< 64 waiting + one round of 64), the window's pair folds,
+// the per-candidate queue.  12 iterations per window: tools/micro_k1o (r03p) 87.5-88.3 us per 1e9
+// indices vs 87.6-89.5 for 10 and 16, and 88.8-89.3 for the per-block entries of k1_body_z.
+constexpr int kK1Win = 12;
 struct K1Lds {
     uint64_t q[kBlock / 64][128];
-    uint16_t wy[kBlock / 64][kK1ZWin * 64];
-    uint32_t tab[kBlock / 64][kK1ZWin];
+    uint32_t wz[kBlock / 64][kK1Win * 64];
+    uint32_t tab[kBlock / 64][kK1Win];
     uint64_t cq[kBlock / 64][kQueue];
 };
 
@@ -45,7 +47,7 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
                                                          unsigned long long* __restrict__ win) {
     __shared__ K1Lds L;
     const int w = threadIdx.x >> 6;
-    k1_body_z<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wy[w], L.tab[w], L.cq[w]);
+    k1_body_p<kK1Win>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wz[w], L.tab[w], L.cq[w]);
 }
 
 // K1 + resolve_publish in one dispatch (single-launch batches, k <= kK1FusedMaxK): every
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(kBlock) void k1_resolve_publish(DrawKey dk, uint32_
     __shared__ K1Lds L;
     __shared__ uint32_t last;
     const int w = threadIdx.x >> 6;
-    k1_body_z<kK1Unroll>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wy[w], L.tab[w], L.cq[w]);
+    k1_body_p<kK1Win>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wz[w], L.tab[w], L.cq[w]);
     // This wave's winner atomics are performed once vmcnt drains: on gfx942/gfx950 a global atomic
     // without return still counts in vmcnt until the memory system acknowledges it (there is no
     // separate vscnt), and an agent-scope atomic is performed at the agent's coherence point (the

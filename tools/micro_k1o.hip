@@ -3,12 +3,18 @@
 // MI355X_MICROARCH.md "Residency") and with amdgpu_num_sgpr limits that admit 8, over a grid sweep.
 // Every variant's winner table is checked against the default's.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../include tools/micro_k1o.hip -o tools/micro_k1o
+//        (+ -DK1O_DEBUG -o tools/micro_k1o_dbg: per-launch counters, mode 'd')
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 
 #include <vector>
 
+__device__ unsigned long long g_dbg[8];
+#ifdef K1O_DEBUG  // counters (mode 'd'); the timing build leaves them out
+#define RSV_K1P_COUNT(i, v) \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_dbg[i], (unsigned long long)(v))
+#endif
 #include "../reservoir_amd/csrc/rsv_device.h"
 #include "../reservoir_amd/csrc/rsv_scan.h"
 
@@ -42,8 +48,78 @@ KDEF(k1_base, )
 KDEF(k1_s80, __attribute__((amdgpu_num_sgpr(80))))
 KDEF(k1_s72, __attribute__((amdgpu_num_sgpr(72))))
 
+// pair entries (k1_body_p), W iterations per window
+template <int W>
+struct K1PLds {
+    uint64_t q[4][128];
+    uint32_t wz[4][W * 64];
+    uint32_t tab[4][W];
+    uint64_t cq[4][kQueue];
+};
+template <int W>
+__global__ __launch_bounds__(256) void k1_pair(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                               uint64_t n_groups, unsigned long long* __restrict__ win) {
+    __shared__ K1PLds<W> L;
+    const int w = threadIdx.x >> 6;
+    k1_body_p<W>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wz[w], L.tab[w], L.cq[w]);
+}
+
+template <bool NOP>
+__global__ void fold_check(const uint32_t* in, uint32_t* out) {
+    const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+    const uint32_t xa = in[2 * t], xb = in[2 * t + 1];
+    uint32_t z, bits = 0;
+    if (NOP) asm volatile("v_or_b32_sdwa %0, %2, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+        "s_nop 0\n\t"
+        "v_or_b32_sdwa %0, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+        "s_nop 0\n\t"
+        "v_cmp_ne_u32_e32 vcc, -1, %0\n\t"
+        "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
+        : "=&v"(z), "+v"(bits)
+        : "v"(xa), "v"(xb)
+        : "vcc");
+    else asm volatile("v_or_b32_sdwa %0, %2, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+        "v_or_b32_sdwa %0, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+        "v_cmp_ne_u32_e32 vcc, -1, %0\n\t"
+        "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
+        : "=&v"(z), "+v"(bits)
+        : "v"(xa), "v"(xb)
+        : "vcc");
+    out[2 * t] = z;
+    out[2 * t + 1] = bits;
+}
+
 int main(int argc, char** argv) {
-    const uint64_t n = 1000000000ull, lo = 1024, n_groups = (n + 15) / 16;
+    for (int nop = 0; nop < 2; ++nop) {  // the pair fold's SDWA + mark: z = fold(xa) | fold(xb) << 16, bits = (z != ~0)
+        const int N = 64 * 4096;
+        std::vector<uint32_t> in(2 * N), out(2 * N);
+        uint64_t st = 0x9E3779B97F4A7C15ull;
+        for (int t = 0; t < 2 * N; ++t) {
+            st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+            uint32_t v = (uint32_t)st;
+            if ((st >> 40) % 3 == 0) v |= 0xFFFF0000u >> (16 * (t & 1));  // fold 0xFFFF often
+            if ((st >> 44) % 5 == 0) v = 0xFFFF0000u;
+            in[t] = v;
+        }
+        uint32_t *di, *dout;
+        CK(hipMalloc(&di, 8 * N));
+        CK(hipMalloc(&dout, 8 * N));
+        CK(hipMemcpy(di, in.data(), 8 * N, hipMemcpyHostToDevice));
+        int bad = 0;
+        for (int rep = 0; rep < 20; ++rep) {
+            if (nop) hipLaunchKernelGGL(fold_check<true>, dim3(N / 64), dim3(64), 0, 0, di, dout);
+            else hipLaunchKernelGGL(fold_check<false>, dim3(N / 64), dim3(64), 0, 0, di, dout);
+            CK(hipMemcpy(out.data(), dout, 8 * N, hipMemcpyDeviceToHost));
+            for (int t = 0; t < N; ++t) {
+                const uint32_t fa = (in[2 * t] | (in[2 * t] >> 16)) & 0xFFFFu, fb = (in[2 * t + 1] | (in[2 * t + 1] >> 16)) & 0xFFFFu;
+                const uint32_t z = fa | (fb << 16);
+                if (out[2 * t] != z || out[2 * t + 1] != (uint32_t)(z != 0xFFFFFFFFu)) ++bad;
+            }
+        }
+        CK(hipFree(di));
+        CK(hipFree(dout));
+        printf("{\"fold_check_nop\": %d, \"bad\": %d, \"of\": %d}\n", nop, bad, 20 * N);
+    }    const uint64_t n = 1000000000ull, lo = 1024, n_groups = (n + 15) / 16;
     const uint32_t k = 1024;
     DrawKey dk{0xC0FFEE, 0, 0x5A5A, 0};
     unsigned long long* win;
@@ -76,6 +152,16 @@ int main(int argc, char** argv) {
     };
     if (run(k1_base, 3072, ref)) return 1;
     // argv: passes, then grids (each pass visits every grid, in the given order)
+    if (argc > 1 && argv[1][0] == 'd') {  // counters of one pair10 launch
+        unsigned long long z[8] = {0};
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof z));
+        if (run(k1_pair<10>, 4096, got)) return 1;
+        if (run(k1_base, 4096, got)) return 1;
+        CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(g_dbg), sizeof z));
+        printf("{\"resolves\": %llu, \"valid\": %llu, \"dense\": %llu, \"windows\": %llu, \"rounds\": %llu, "
+               "\"pushed\": %llu, \"base_pushed\": %llu, \"match\": %s}\n", z[0], z[1], z[2], z[3], z[4], z[5], z[6], got == ref ? "true" : "false");
+        return 0;
+    }
     const int passes = argc > 1 ? atoi(argv[1]) : 2;
     std::vector<int> grids;
     for (int a = 2; a < argc; ++a) grids.push_back(atoi(argv[a]));
@@ -83,7 +169,9 @@ int main(int argc, char** argv) {
     for (int p = 0; p < passes; ++p)
         for (int g : grids) {
             if (time_v(k1_base, "base", g)) return 1;
-            if (time_v(k1_s80, "s80", g)) return 1;
+            if (time_v(k1_pair<10>, "pair10", g)) return 1;
+            if (time_v(k1_pair<12>, "pair12", g)) return 1;
+            if (time_v(k1_pair<16>, "pair16", g)) return 1;
         }
     return 0;
 }
