@@ -45,9 +45,12 @@ hipError_t launch_segmented(const void* keys, int key_width, const int64_t* offs
     const uint32_t k0 = (uint32_t)dp.seed, k1 = (uint32_t)(dp.seed >> 32);
     const uint64_t blocks = ((uint64_t)S + kWaves - 1) / kWaves;
     const unsigned grid = (unsigned)std::min<uint64_t>(blocks, 256ull * 16);
-    // RSV_K2_FIFO_CAP (tests): a lower bulk-append limit, so the ballot-round overflow path runs
-    const char* cap_env = std::getenv("RSV_K2_FIFO_CAP");
-    const uint32_t fifo_cap = cap_env ? (uint32_t)std::atoi(cap_env) : k2::kQCap;
+    // RSV_K2_FIFO_CAP (tests, read once per process): a lower bulk-append limit, so the ballot-
+    // round overflow path runs
+    static const uint32_t fifo_cap = [] {
+        const char* e = std::getenv("RSV_K2_FIFO_CAP");
+        return e ? (uint32_t)std::atoi(e) : k2::kQCap;
+    }();
     if (key_width == 8)
         hipLaunchKernelGGL(k2_segmented<int64_t>, dim3(grid), dim3(64 * kWaves), lds, st, (const int64_t*)keys,
                            offsets, S, k, k0, k1, dp.stream, (int64_t*)out, counts, fifo_cap);

@@ -28,16 +28,15 @@ def test_ragged_parity(cuda, oracle, k):
     assert np.array_equal(out.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("k", [64, 256, 1000])
-def test_fifo_overflow_rounds(cuda, oracle, monkeypatch, k):
-    """An iteration with more candidates than the FIFO takes (RSV_K2_FIFO_CAP lowers the bulk-append
-    limit to 128; at k = 256 an iteration past the dense head holds ~177) goes through the ballot-
-    round path of rsv_k2.h: same reservoirs as the oracle."""
-    import torch
-
-    from reservoir_amd import batch
-
-    monkeypatch.setenv("RSV_K2_FIFO_CAP", "128")
+_FIFO_CASE = """
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, {root!r})
+from oracle import oracle
+from reservoir_amd import batch
+cuda = torch.device("cuda", 0)
+for k in (64, 256, 1000):
     rng = np.random.default_rng(500 + k)
     lens = rng.integers(0, 20_000, size=200)
     lens[:4] = [k, k + 1, 4096, 19_999]
@@ -46,8 +45,26 @@ def test_fifo_overflow_rounds(cuda, oracle, monkeypatch, k):
     want, wcnt = oracle.algo_r_segmented(31, 77, k, keys, offs)
     out, cnt = batch.sample_segmented(torch.from_numpy(keys).to(cuda), torch.from_numpy(offs).to(cuda), k,
                                       seed=31, stream_base=77)
-    assert np.array_equal(cnt.cpu().numpy(), wcnt)
-    assert np.array_equal(out.cpu().numpy(), want)
+    assert np.array_equal(cnt.cpu().numpy(), wcnt), k
+    assert np.array_equal(out.cpu().numpy(), want), k
+print("fifo overflow ok")
+"""
+
+
+def test_fifo_overflow_rounds(cuda, oracle):
+    """An iteration with more candidates than the FIFO takes (RSV_K2_FIFO_CAP lowers the bulk-append
+    limit to 128; at k = 256 an iteration past the dense head holds ~177) goes through the ballot-
+    round path of rsv_k2.h: same reservoirs as the oracle, k = 64, 256, 1000.  The engine reads the
+    variable once per process, so the cases run in a child process that sets it."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RSV_K2_FIFO_CAP="128")
+    r = subprocess.run([sys.executable, "-c", _FIFO_CASE.format(root=root)], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and "fifo overflow ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
 @pytest.mark.parametrize("k", [2, 7, 64])

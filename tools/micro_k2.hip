@@ -11,7 +11,7 @@
 #include <algorithm>
 #include <vector>
 
-#include "k2_lanes_exp.h"
+#include "../reservoir_amd/csrc/rsv_k2.h"
 
 using namespace rsv;
 
@@ -84,30 +84,6 @@ int main(int argc, char** argv) {
             if (run(k2::k2_segmented<int64_t, 0>, name, true)) return 1;
         }
         return 0;
-    }
-    if (!(argc > 1 && argv[1][0] == 'g')) {  // the lane-per-stream form (k2_segmented2)
-        const size_t lds2 = k2::lds_bytes2(k);
-        const unsigned grid2 = (unsigned)((S + 64 * k2::kWaves2 - 1) / (64 * k2::kWaves2));
-        std::vector<float> ts;
-        for (int rep = 0; rep < 7; ++rep) {
-            CK(hipMemset(out, 0, S * k * 8));
-            CK(hipEventRecord(e0));
-            hipLaunchKernelGGL(k2::k2_segmented2<int64_t>, dim3(grid2), dim3(64 * k2::kWaves2), lds2, 0,
-                               (const int64_t*)keys, (const int64_t*)offs, S, k, 1u, 0u, 0ull, out, cnt);
-            CK(hipEventRecord(e1));
-            CK(hipEventSynchronize(e1));
-            float ms;
-            CK(hipEventElapsedTime(&ms, e0, e1));
-            if (rep) ts.push_back(ms);
-        }
-        std::sort(ts.begin(), ts.end());
-        printf("{\"variant\": \"lanes (k2_segmented2)\", \"median_ms\": %.4f, \"min_ms\": %.4f, \"lds\": %zu}\n",
-               ts[ts.size() / 2], ts[0], lds2);
-        CK(hipMemcpy(got.data(), out, S * k * 8, hipMemcpyDeviceToHost));
-        size_t bad = 0;
-        for (size_t i = 0; i < got.size(); ++i) bad += got[i] != ref[i];
-        printf("  identical to wave-per-stream: %s (%zu of %zu differ)\n", bad ? "NO" : "yes", bad, got.size());
-        if (bad) return 2;
     }
     if (argc > 1 && argv[1][0] == 'l') return 0;  // the two product forms only
     if (argc > 1 && argv[1][0] == 'p') return 0;  // one variant only (rocprofv3 --pmc passes)
