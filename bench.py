@@ -278,7 +278,7 @@ def c4_leg(args, rank: int, world: int, dev, backend: str) -> dict:
 
 def load_traffic(n: int):
     """HBM bytes per K1 launch from the committed PMC pass (profiles/), if one matches n."""
-    for path in (os.path.join(ROOT, "profiles", "r02", "pmc_k1.json"), os.path.join(ROOT, "profiles", "pmc_k1.json")):
+    for path in (os.path.join(ROOT, "profiles", r, "pmc_k1.json") for r in ("r03", "r02", "")):
         try:
             d = json.load(open(path))
             if int(d.get("n", -1)) == n:
