@@ -146,7 +146,8 @@ int64_t    rsv_count(const rsv_sampler* s);   /* elements sampled so far (S:203)
  * handle's own stream every call returns with its device work finished (ownership of caller
  * buffers returns at once); on a caller stream, calls that take or fill DEVICE buffers
  * (rsv_sample_batch with RSV_MEM_DEVICE, rsv_export_state, rsv_merge_state, rsv_result_device) are
- * stream-ordered and return without a host wait. */
+ * stream-ordered and return without a host wait.  rsv_set_stream orders the work already queued
+ * on the previous stream before the new stream's next work (an event wait, no host wait). */
 rsv_status rsv_set_stream(rsv_sampler* s, void* hip_stream);
 void*      rsv_get_stream(const rsv_sampler* s);
 rsv_status rsv_synchronize(rsv_sampler* s);

@@ -34,8 +34,10 @@ def sample_segmented(keys, offsets, k: int, seed: int, stream_base: int = 0):
     keys = keys.contiguous()
     offsets = offsets.contiguous()
     S = offsets.numel() - 1
-    out = torch.zeros((max(S, 0), k), dtype=keys.dtype, device=keys.device)
-    counts = torch.zeros(max(S, 0), dtype=torch.int64, device=keys.device)
+    # the kernel writes every slot (empty ones as 0) and every count: no zero-fill (at C3's shape
+    # torch.zeros was a 512 MB memset beside the 1.7 ms launch)
+    out = torch.empty((max(S, 0), k), dtype=keys.dtype, device=keys.device)
+    counts = torch.empty(max(S, 0), dtype=torch.int64, device=keys.device)
     if S <= 0:
         return out, counts
     N.check(L.rsv_sample_segmented(

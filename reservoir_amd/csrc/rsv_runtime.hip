@@ -155,6 +155,7 @@ struct rsv_sampler {
     uint32_t pub_gen = 0;
     bool pub_valid = false;
     KernelTimer timer;
+    hipEvent_t handover = nullptr;  // rsv_set_stream's event (kept until destroy: see there)
     // device work enqueued on `stream` by this handle, in groups, vs the groups known complete
     // (a stream synchronize, or the host flag of a publication that was the last group)
     uint64_t ops = 0, ops_done = 0, pub_ops = 0;
@@ -485,6 +486,9 @@ void free_all(rsv_sampler* s) {
         pool_release_event(s->device, s->stage_free[b], hipEventDisableTiming);
     }
     pool_host_free(s->result_h);
+    // the handover record has completed: the stream waiting on it was synchronized, or its
+    // publication seen, before this
+    if (s->handover) pool_release_event(s->device, s->handover, hipEventDisableTiming);
     if (s->distinct) distinct_destroy(s->distinct);
     if (s->stream && s->own_stream) pool_release_stream(s->device, s->stream);
 }
@@ -815,8 +819,15 @@ int64_t rsv_count(const rsv_sampler* s) { return s ? s->count + s->stage_n : 0; 
 rsv_status rsv_set_stream(rsv_sampler* s, void* hip_stream) {
     if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
     DeviceGuard g(s->device);
-    if (s->ops != s->ops_done) RSV_HIP_TRY(sync_stream(s));  // a fresh handle: none
-    s->ops_done = s->ops;
+    if (s->ops != s->ops_done && (hipStream_t)hip_stream != s->stream) {
+        // stream-ordered hand-over, no host wait: the new stream waits for the work queued so far
+        // (e.g. a combine moved to a communication stream while the next batch samples on the
+        // first).  The event is the handle's own until rsv_destroy: handed back to the pool at
+        // once, its next record elsewhere could land before the wait binds
+        if (!s->handover) RSV_HIP_TRY(pool_event(&s->handover, hipEventDisableTiming));
+        RSV_HIP_TRY(hipEventRecord(s->handover, s->stream));
+        RSV_HIP_TRY(hipStreamWaitEvent((hipStream_t)hip_stream, s->handover, 0));
+    }
     if (s->own_stream) pool_release_stream(s->device, s->stream);
     s->stream = (hipStream_t)hip_stream;
     s->own_stream = false;

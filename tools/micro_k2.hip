@@ -2,7 +2,8 @@
 // k = 64 (development tool, not product).  Variants: 0 = product kernel, 1 = no winner-key gather,
 // 2 = no level-1 Philox, 8 = candidates dropped after the FIFO append, 9 = 8 + 1, 16 = the
 // winner keys stored right after their gather (the product defers the store by one stream),
-// 8192 = the 8-plane candidate mask for every block (the product takes 4 planes once T <= 16).
+// 8192 = the 8-plane candidate mask for every block (the product takes 4 planes once T <= 16),
+// 512 = the dense head [k, 4k) uncut (the product cuts it to whole 64-pair rounds).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/micro_k2.hip -o tools/micro_k2
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -54,7 +55,8 @@ int main(int argc, char** argv) {
     size_t lds_run = lds;
     auto run = [&](auto kern, const char* name, bool check) -> int {
         std::vector<float> ts;
-        for (int rep = 0; rep < 15; ++rep) {
+        // the first ~20 launches run on a still-ramping clock (bench.py's ramp note): timed after them
+        for (int rep = 0; rep < 45; ++rep) {
             CK(hipEventRecord(e0));
             hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * k2::kWaves), lds_run, 0, (const int64_t*)keys,
                                (const int64_t*)offs, S, k, 1u, 0u, 0ull, out, cnt, 0xFFFFFFFFu);
@@ -62,7 +64,7 @@ int main(int argc, char** argv) {
             CK(hipEventSynchronize(e1));
             float ms;
             CK(hipEventElapsedTime(&ms, e0, e1));
-            if (rep) ts.push_back(ms);
+            if (rep >= 25) ts.push_back(ms);
         }
         std::sort(ts.begin(), ts.end());
         printf("{\"variant\": \"%s\", \"median_ms\": %.4f, \"min_ms\": %.4f}\n", name, ts[ts.size() / 2], ts[0]);
@@ -110,6 +112,13 @@ int main(int argc, char** argv) {
         if (run(k2::k2_segmented<int64_t, 9 | 1024 | 2048>, "9 + no head + no append", false)) return 1;
         if (run(k2::k2_segmented<int64_t, 9 | 1024 | 2048 | 4096>, "9 + no head + no append + no candidates", false)) return 1;
         if (run(k2::k2_segmented<int64_t, 1 | 1024>, "1 + no head (resolve kept)", false)) return 1;
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'r') {  // dense head cut to whole 64-pair rounds vs uncut (A/B/A/B)
+        for (int rep = 0; rep < 2; ++rep) {
+            if (run(k2::k2_segmented<int64_t, 512>, "512 head [k, 4k) uncut (r02)", true)) return 1;
+            if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+        }
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'h') {  // dense-head multiplier: 4 (product), 2, none
