@@ -178,7 +178,7 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
     // The head is cut to whole 64-pair rounds (k = 64: [64, 192) instead of [64, 256): its 96 pairs
     // took two rounds, the second half empty; the 64 indices moved to the FIFO add ~20 candidates
     // to rounds it runs anyway): C3 1.75-1.76 -> 1.67-1.69 ms (tools/micro_k2 r, warm clock).
-    constexpr uint32_t HM = (V & 32) ? 2u : (V & 64) ? 1u : 4u;
+    constexpr uint32_t HM = (V & 32) ? 2u : (V & 64) ? 1u : (V & 16384) ? 6u : (V & 32768) ? 8u : 4u;
     uint64_t hx = (uint64_t)HM * k;
     if constexpr ((V & 512) == 0) hx = k + ((hx - k) & ~(uint64_t)127);  // (V & 512: the r02 head)
     const IdxT hend = (IdxT)std::min<uint64_t>((uint64_t)len, hx);

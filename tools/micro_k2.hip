@@ -3,7 +3,8 @@
 // 2 = no level-1 Philox, 8 = candidates dropped after the FIFO append, 9 = 8 + 1, 16 = the
 // winner keys stored right after their gather (the product defers the store by one stream),
 // 8192 = the 8-plane candidate mask for every block (the product takes 4 planes once T <= 16),
-// 512 = the dense head [k, 4k) uncut (the product cuts it to whole 64-pair rounds).
+// 512 = the dense head [k, 4k) uncut (the product cuts it to whole 64-pair rounds), 16384 / 32768 =
+// heads [k, 6k) / [k, 8k) (cut to whole rounds).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/micro_k2.hip -o tools/micro_k2
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -117,6 +118,14 @@ int main(int argc, char** argv) {
     if (argc > 1 && argv[1][0] == 'r') {  // dense head cut to whole 64-pair rounds vs uncut (A/B/A/B)
         for (int rep = 0; rep < 2; ++rep) {
             if (run(k2::k2_segmented<int64_t, 512>, "512 head [k, 4k) uncut (r02)", true)) return 1;
+            if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+        }
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'm') {  // head multiplier 4 (product) vs 6, 8 (whole rounds)
+        for (int rep = 0; rep < 2; ++rep) {
+            if (run(k2::k2_segmented<int64_t, 16384>, "16384 head [k, 6k) in whole rounds", true)) return 1;
+            if (run(k2::k2_segmented<int64_t, 32768>, "32768 head [k, 8k) in whole rounds", true)) return 1;
             if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
         }
         return 0;
