@@ -417,3 +417,44 @@ def test_caller_stream_pipelined_samplers(cuda, oracle):
     pending.close()
     del keys
     torch.cuda.empty_cache()
+
+
+def test_set_stream_hands_over_pending_work(cuda, oracle):
+    """rsv_set_stream with work still queued: the new stream is ordered after it by an event wait
+    (no host synchronize).  A sampler samples on one torch stream and, with its K1 pass in flight,
+    moves to a second stream where its combine kernels (export_packed, merge_packed), a further
+    batch and result_device run; then back to the first for result().  keys = arange: each slot's
+    key is its last writer's index; the merged rows are two copies of the same state."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    n1, n2, k, seed, sid = 150_000_000, 50_000_000, 1024, 91, 5
+    keys = torch.arange(n1 + n2, dtype=torch.int64, device=cuda)
+    a_stream, b_stream = torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)
+    a_stream.wait_stream(torch.cuda.current_stream())
+    b_stream.wait_stream(torch.cuda.current_stream())
+    want1 = oracle.algo_r_last_writers(seed, sid, k, 0, n1)
+    want = oracle.algo_r_last_writers(seed, sid, k, 0, n1 + n2)
+    s = Sampler(k, seed=seed, stream_id=sid, reusable=True)()
+    s.set_stream(a_stream.cuda_stream)
+    s.sample_all(keys[:n1])  # K1 + resolve queued on a
+    s.set_stream(b_stream.cuda_stream)  # pending: b waits for a's record
+    with torch.cuda.stream(b_stream):
+        rows = torch.empty((2, 2 * k), dtype=torch.int64, device=cuda)
+        s.export_packed(rows[0])
+        s.export_packed(rows[1])
+        s.merge_packed(rows, n1)
+        mid = torch.empty(k, dtype=torch.int64, device=cuda)
+        assert s.result_device(mid) == k
+        s.sample_all(keys[n1:])
+    s.set_stream(a_stream.cuda_stream)  # and back, with b's work pending
+    got = s.result()
+    torch.cuda.synchronize()
+    assert np.array_equal(rows[0, :k].cpu().numpy(), want1)
+    assert np.array_equal(mid.cpu().numpy(), want1)
+    assert np.array_equal(got, want)
+    s.close()
+    del keys
+    torch.cuda.empty_cache()
+
