@@ -293,11 +293,13 @@ __device__ __forceinline__ void k1_body_bits(const DrawKey& dk, uint32_t k, uint
 
 constexpr uint32_t kK1ZWin = 20;  // blocks per lane per window (W x U); 16..32 within 2 us, 20 best (r02ad)
 
-// the 16-bit OR of a block's plane halves: bit e clear <=> b_e == 0 (one SDWA op for the fold)
+// the 16-bit OR of a block's plane halves: bit e clear <=> b_e == 0 (one SDWA op for the fold; the
+// wait state after it keeps a reader right behind from the gfx950 SDWA hazard, see fold_pair)
 __device__ __forceinline__ uint32_t fold16(const u32x4& w) {
     const uint32_t x = w.x | w.y | w.z | w.w;
     uint32_t y;
-    asm("v_or_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
+    asm("v_or_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+        "s_nop 0"
         : "=v"(y)
         : "v"(x));
     return y;
