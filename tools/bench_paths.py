@@ -107,10 +107,10 @@ def c4(dev, hash_kind="identity", order="auto", twins=False, seed=7):
 
     if not twins:
         ramp(one, 0.2)
-    # reps 1..4 timed end to end with the filter timer off (its events add marker packets and host
+    # reps 1..9 timed end to end with the filter timer off (its events add marker packets and host
     # calls to the batch); one more rep with it on, for the filter launches and their time
-    for rep in range(6):
-        prof = rep == 5
+    for rep in range(11):
+        prof = rep == 10
         mk = Sampler.distinct(k, seed=seed, order=order)
         d = mk(hash=hash_kind) if hash_kind != "default" else mk()
         d.set_stream(torch.cuda.current_stream().cuda_stream)
