@@ -28,7 +28,10 @@ constexpr int kBlock = 256;
 // them) go straight to global atomicMax on the k-slot winner table: 14k atomics per 1e9 indices at k = 1024.
 constexpr int kK1Unroll = 2;  // level-0 blocks per lane per iteration (two Philox chains in flight)
 
-constexpr unsigned kK1Grid = 256 * 12;
+// ~20 four-wave workgroups per CU (6 resident: .sgpr_count 104): tools/micro_k1o r03ae/r03af, 1e9
+// draws, 12-iteration windows: 85.0-85.5 us at 5086 workgroups (2 whole windows per wave) vs
+// 87.5-89 us at 3072, 3390 (3 windows), 4096, 6144, 7629 and 10172 (1 window)
+constexpr unsigned kK1Grid = 256 * 20;
 
 // per-wave LDS of k1_body_p: pair queue (< 64 waiting + one round of 64), the window's pair folds,
 // the per-candidate queue.  12 iterations per window: tools/micro_k1o (r03p) 87.5-88.3 us per 1e9
@@ -458,6 +461,17 @@ inline unsigned grid_for(uint64_t items, unsigned cap) {
     return (unsigned)(b < cap ? b : cap);
 }
 
+// K1's grid: a wave's last window, when partial, takes the per-block path (clip and dense
+// checks, ~30 more VALU per iteration); so the grid is sized for whole windows per wave --
+// m windows, m nearest to what kK1Grid workgroups would run -- where the launch is large enough
+// (1e9 draws: 5086 workgroups, 2 windows of 12 iterations per wave)
+inline unsigned k1_grid(uint64_t n_groups) {
+    constexpr uint64_t per_window = (uint64_t)kK1Unroll * kBlock * kK1Win;  // blocks per workgroup-window
+    const uint64_t m = (n_groups + per_window * kK1Grid / 2) / (per_window * kK1Grid);
+    if (m == 0) return grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, kK1Grid);
+    return (unsigned)std::max<uint64_t>(1, n_groups / (per_window * m));
+}
+
 }  // namespace
 
 hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
@@ -470,9 +484,7 @@ hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, 
         // and no launch crosses a multiple of 2^32 blocks: the counter's high word is a scalar
         const uint64_t g_wrap = ((g_begin >> 32) + 1) << 32;
         n_groups = std::min<uint64_t>(std::min<uint64_t>(g_end, g_wrap) - g_begin, kMaxGroups);
-        // 12 four-wave workgroups per CU (with the 20-block window's 18.5 KB of LDS, 8 resident):
-        // measured best of 2560..4096 (tools/micro_k1 zf, r02ad)
-        const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, kK1Grid);
+        const unsigned grid = k1_grid(n_groups);
         hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
                            g_begin, n_groups, batch_win);
         hipError_t e = hipGetLastError();
@@ -495,7 +507,7 @@ hipError_t launch_k1_resolve_publish(const DrawParams& dp, uint32_t k, uint64_t 
                                      hipStream_t st) {
     if (!k1_fused_ok(lo, hi, k, key_width)) return hipErrorInvalidValue;
     const uint64_t g_begin = lo >> 4, n_groups = ((hi + 15) >> 4) - g_begin;
-    const unsigned grid = grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, kK1Grid);
+    const unsigned grid = k1_grid(n_groups);
     if (key_width == 8)
         hipLaunchKernelGGL(k1_resolve_publish<int64_t>, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
                            g_begin, n_groups, batch_win, ticket, (const int64_t*)keys, base, n, (int64_t*)slot_key,
