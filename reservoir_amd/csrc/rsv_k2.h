@@ -295,7 +295,16 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     uint16_t* lut = (uint16_t*)lds;
     const uint64_t dense_lim = 256ull * k;
-    for (uint32_t g = threadIdx.x; g < kLut; g += blockDim.x) lut[g] = (uint16_t)block_threshold((uint64_t)g << 4, dense_lim);
+    // (32-bit division while the dividend fits: the table is rebuilt by every workgroup, and the
+    // 64-bit form was ~2.5 % of a C3 launch at 32768 workgroups)
+    for (uint32_t g = threadIdx.x; g < kLut; g += blockDim.x) {
+        const uint64_t i0 = (uint64_t)g << 4;
+        uint32_t T;
+        if (i0 + 1 >= dense_lim) T = 0;
+        else if (dense_lim + i0 <= 0xFFFFFFFFull) T = std::min<uint32_t>(256u, (uint32_t)(dense_lim + i0) / (uint32_t)(i0 + 1));
+        else T = block_threshold(i0, dense_lim);
+        lut[g] = (uint16_t)T;
+    }
     __syncthreads();
     // wave index in a scalar register: stream numbers and offsets[] loads below are wave-uniform
     // (scalar loads, counted by lgkmcnt -- never waited for together with the deferred key gather)

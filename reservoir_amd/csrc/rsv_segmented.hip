@@ -44,7 +44,10 @@ hipError_t launch_segmented(const void* keys, int key_width, const int64_t* offs
     if (form == 1 || lds > 160 * 1024) return launch_segmented_v1(keys, key_width, offsets, S, k, dp, out, counts, st);
     const uint32_t k0 = (uint32_t)dp.seed, k1 = (uint32_t)(dp.seed >> 32);
     const uint64_t blocks = ((uint64_t)S + kWaves - 1) / kWaves;
-    const unsigned grid = (unsigned)std::min<uint64_t>(blocks, 256ull * 16);
+    // up to 128 four-wave workgroups per CU over the launch (C3: 8 streams per wave): tools/micro_k2 G
+    // (r03ai) 1.78 ms at 4096 workgroups, 1.71 at 16384, 1.65 at 32768, 1.66-1.68 at 65536, 1.84 at
+    // one stream per wave (262144: every workgroup rebuilds the threshold table)
+    const unsigned grid = (unsigned)std::min<uint64_t>(blocks, 256ull * 128);
     // RSV_K2_FIFO_CAP (tests, read once per process): a lower bulk-append limit, so the ballot-
     // round overflow path runs
     static const uint32_t fifo_cap = [] {

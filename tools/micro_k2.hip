@@ -48,7 +48,7 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, keys, n, offs, S, L);
     CK(hipDeviceSynchronize());
     const size_t lds = k2::lds_bytes(k);
-    const unsigned grid = (unsigned)std::min<int64_t>(S / k2::kWaves, 256 * 16);
+    unsigned grid = (unsigned)std::min<int64_t>(S / k2::kWaves, 256 * 128);  // the product's cap (rsv_segmented.hip)
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -113,6 +113,16 @@ int main(int argc, char** argv) {
         if (run(k2::k2_segmented<int64_t, 9 | 1024 | 2048>, "9 + no head + no append", false)) return 1;
         if (run(k2::k2_segmented<int64_t, 9 | 1024 | 2048 | 4096>, "9 + no head + no append + no candidates", false)) return 1;
         if (run(k2::k2_segmented<int64_t, 1 | 1024>, "1 + no head (resolve kept)", false)) return 1;
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'G') {  // grid sweep of the product (argv[2..]: grids)
+        for (int pass = 0; pass < 2; ++pass)
+            for (int a = 2; a < argc; ++a) {
+                grid = (unsigned)atoi(argv[a]);
+                char name[64];
+                snprintf(name, sizeof name, "0 product, grid %u", grid);
+                if (run(k2::k2_segmented<int64_t, 0>, name, true)) return 1;
+            }
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'r') {  // dense head cut to whole 64-pair rounds vs uncut (A/B/A/B)
