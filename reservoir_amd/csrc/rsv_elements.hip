@@ -467,8 +467,9 @@ inline unsigned grid_for(uint64_t items, unsigned cap) {
 // (1e9 draws: 5086 workgroups, 2 windows of 12 iterations per wave)
 inline unsigned k1_grid(uint64_t n_groups) {
     constexpr uint64_t per_window = (uint64_t)kK1Unroll * kBlock * kK1Win;  // blocks per workgroup-window
-    const uint64_t m = (n_groups + per_window * kK1Grid / 2) / (per_window * kK1Grid);
-    if (m == 0) return grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, kK1Grid);
+    // below ~3 whole-window workgroups per CU, every CU gets work instead (partial windows)
+    if (n_groups < per_window * 768) return grid_for((n_groups + kK1Unroll - 1) / kK1Unroll, kK1Grid);
+    const uint64_t m = std::max<uint64_t>(1, (n_groups + per_window * kK1Grid / 2) / (per_window * kK1Grid));
     return (unsigned)std::max<uint64_t>(1, n_groups / (per_window * m));
 }
 
