@@ -993,6 +993,7 @@ __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap
         }
     }
     __syncthreads();
+    if (AGG == 3) return;  // DEV A/B: the accumulator atomics' share of the kernel (wrong verdict)
     int* acc = vacc + (size_t)(blockIdx.x % kVerifyCopies) * (kMaxRanges + 1);
     for (int i = threadIdx.x; i <= nr; i += blockDim.x)
         if (sdiff[i]) atomicAdd(&acc[i], sdiff[i]);
@@ -2025,7 +2026,7 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
             const char* e = std::getenv("RSV_SCHED_AGG");
             return e ? std::atoi(e) : 1;
         }();
-        auto kern = agg == 0 ? sched_sort<KeyT, 0> : agg == 2 ? sched_sort<KeyT, 2> : sched_sort<KeyT, 1>;
+        auto kern = agg == 0 ? sched_sort<KeyT, 0> : agg == 2 ? sched_sort<KeyT, 2> : agg == 3 ? sched_sort<KeyT, 3> : sched_sort<KeyT, 1>;
         hipLaunchKernelGGL(kern, dim3((B + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, k, cap, d->sctl,
                            d->log_bmax_s, d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
     }
