@@ -103,13 +103,17 @@ def cpu_baseline(k: int, n_stream: int, seed: int, c4_host=None) -> dict:
     # stands in for the 8 GB array (the path reads only ~k ln(n/k) elements, all of them zeros)
     zbuf = mmap.mmap(-1, n_stream * 8)
     addr = C.addressof(C.c_char.from_buffer(zbuf))
+    # one untimed pass first: it maps every page the walk reads (the same ~14 k elements each run,
+    # same seed), so the timed runs read resident memory as the reference's array would be
+    L.or_time_algo_l_indexed(k, seed, C.c_void_p(addr), n_stream, op)
     ts = _median(lambda: L.or_time_algo_l_indexed(k, seed, C.c_void_p(addr), n_stream, op))
     del addr
     zbuf.close()
     legs.append({"config": "C2 sampleAll(IndexedSeq) skip path (Sampler.scala:261-273)", "cores": 1,
                  "Gelem_s": round(n_stream / ts / 1e9, 2),
-                 "sample": f"{n_stream:.0e} elements, k={k}; input = an untouched zero-page mapping (the path "
-                           "touches ~k ln(n/k) elements, so their values do not matter)"})
+                 "sample": f"{n_stream:.0e} elements, k={k}; input = a zero-page mapping whose pages the walk "
+                           "reads were mapped by an untimed first pass (the path touches ~k ln(n/k) elements, "
+                           "so their values do not matter)"})
 
     # C1: 10 M Longs (the first 1e7 of the C2 stream), k = 100, both samplers
     n1, k1 = 10_000_000, 100
@@ -176,13 +180,15 @@ def secondary(dev) -> list:
             ("C4 default/set", lambda: P.c4(dev, "default", "set")),
             ("C4 default/ordered", lambda: P.c4(dev, "default")),
             ("C4 default/ordered replay branch", lambda: P.c4_replay(dev)),
-            ("C2 java_l", lambda: P.c2l(dev))]
+            ("C2 java_l", lambda: P.c2l(dev)), ("C2 indexed", lambda: P.c2_indexed(dev)),
+            ("C4 combine", lambda: P.c4_merge(dev))]
     for name, fn in jobs:
         try:
-            r = fn()
+            rs = fn()
         except Exception as ex:  # noqa: BLE001 -- reported, not raised
-            r = {"config": name, "error": f"{type(ex).__name__}: {ex}"}
-        out.append({kk: (round(v, 6) if isinstance(v, float) else v) for kk, v in r.items()})
+            rs = {"config": name, "error": f"{type(ex).__name__}: {ex}"}
+        for r in (rs if isinstance(rs, list) else [rs]):
+            out.append({kk: (round(v, 6) if isinstance(v, float) else v) for kk, v in r.items()})
         torch.cuda.empty_cache()
     return out
 
@@ -224,18 +230,27 @@ def c4_leg(args, rank: int, world: int, dev, backend: str) -> dict:
            "ranks": world, "backend": backend, "legs": []}
 
     def make(hash_kind):
-        mk = Sampler.distinct(k, seed=7)
+        mk = Sampler.distinct(k, seed=7, retain_log=hash_kind == "default")  # the exact replay reads the log
         return mk(hash="identity") if hash_kind == "identity" else mk()
 
     for hash_kind in ("identity", "default"):
         replays = 0
+        marks = []  # per timed step: events before sampling / before the combine / after it
 
-        def step():
+        def step(mark=False):
             nonlocal replays
             s = make(hash_kind)
             s.set_stream(stream)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if mark else None
+            if ev:
+                ev[0].record()
             s.sample_all(keys)
+            if ev:
+                ev[1].record()
             replays += D.combine(s, device=dev, total_count=total)
+            if ev:
+                ev[2].record()
+                marks.append(ev)
             r = s.result()
             s.close()
             return r
@@ -249,7 +264,7 @@ def c4_leg(args, rank: int, world: int, dev, backend: str) -> dict:
         t0 = time.perf_counter()
         res = None
         for _ in range(args.c4_steps):
-            res = step()
+            res = step(mark=True)
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
@@ -257,10 +272,16 @@ def c4_leg(args, rank: int, world: int, dev, backend: str) -> dict:
                           device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         elapsed = float(el.item())
+        # the step split on the stream's own clock (events around sample_all and around combine:
+        # the all-gather, the device merge, and for the default hash its one host read-back)
+        samp = statistics.median(a.elapsed_time(b) for a, b, _ in marks)
+        comb = statistics.median(b.elapsed_time(c) for _, b, c in marks)
         leg = {"hash": hash_kind + (" (Long.hashCode, ordered: exact sequential set)" if hash_kind == "default"
                                     else " (set mode, bit-exact bottom-k)"),
                "steps": args.c4_steps, "ms_per_step": round(elapsed / args.c4_steps * 1e3, 4),
-               "Gelem_s": round(total * args.c4_steps / elapsed / 1e9, 3), "exact_replays": replays}
+               "Gelem_s": round(total * args.c4_steps / elapsed / 1e9, 3), "exact_replays": replays,
+               "sample_ms_median": round(samp, 4), "combine_ms_median": round(comb, 4),
+               "split_clock": "HIP events on the sampler's (torch's) stream, this rank"}
         if rank == 0:  # the merged set vs one sampler over the whole stream (same seed, same hash)
             full = workloads.c4_slice(total, 0, total, dev)
             one = make(hash_kind)

@@ -164,3 +164,43 @@ JNIEXPORT void JNICALL JNI_FN(stageCommit)(JNIEnv* env, jobject self, jlong s, j
     rsv_status st = rsv_jvm_stage_commit(session(s), n);
     if (st != RSV_OK) throw_status(env, st);
 }
+
+/* Sampler.sampleAll over a known-size IndexedSeq (Sampler.scala:289-312 -> sampleIndexed :261-273):
+ * the engine samples indices 0 until n of the sequence and fills `offsets` (length >= k) with the
+ * offset of the element each slot now holds, or -1; JniSampler maps exactly those elements and
+ * hands their keys back with fillLongs / fillInts (a k-key array in slot order). */
+JNIEXPORT void JNICALL JNI_FN(sampleIndexed)(JNIEnv* env, jobject self, jlong s, jlong n, jlongArray offsets) {
+    (void)self;
+    const jsize len = (*env)->GetArrayLength(env, offsets);
+    if (len < session(s)->k) {
+        throw_status(env, RSV_E_ILLEGAL_ARGUMENT);
+        return;
+    }
+    int64_t* buf = (int64_t*)malloc((size_t)len * sizeof(int64_t));
+    if (!buf) {
+        throw_status(env, RSV_E_OUT_OF_MEMORY);
+        return;
+    }
+    rsv_status st = rsv_jvm_sample_indexed(session(s), n, buf);
+    if (st == RSV_OK) (*env)->SetLongArrayRegion(env, offsets, 0, session(s)->k, (const jlong*)buf);
+    free(buf);
+    if (st != RSV_OK) throw_status(env, st);
+}
+
+#define FILL_ARRAY(NAME, JARR, JT, GET)                                                  \
+    JNIEXPORT void JNICALL JNI_FN(NAME)(JNIEnv * env, jobject self, jlong s, JARR keys) { \
+        (void)self;                                                                     \
+        const jint k = session(s)->k;                                                   \
+        JT* buf = (JT*)malloc((size_t)k * sizeof(JT));                                  \
+        if (!buf) {                                                                     \
+            throw_status(env, RSV_E_OUT_OF_MEMORY);                                     \
+            return;                                                                     \
+        }                                                                               \
+        (*env)->GET(env, keys, 0, k, buf);                                              \
+        rsv_status st = (*env)->ExceptionCheck(env) ? RSV_OK : rsv_jvm_fill_slots(session(s), buf); \
+        free(buf);                                                                      \
+        if (st != RSV_OK) throw_status(env, st);                                        \
+    }
+
+FILL_ARRAY(fillLongs, jlongArray, jlong, GetLongArrayRegion)
+FILL_ARRAY(fillInts, jintArray, jint, GetIntArrayRegion)

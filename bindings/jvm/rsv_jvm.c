@@ -113,6 +113,20 @@ rsv_status rsv_jvm_sample_array(rsv_jvm* s, const void* keys, const int64_t* has
     return RSV_OK;
 }
 
+rsv_status rsv_jvm_sample_indexed(rsv_jvm* s, int64_t n, int64_t* slot_offsets) {
+    g_local_error = 0;
+    if (!s->open) return closed();
+    rsv_status st = commit_pending(s); /* the staged keys come first in index order */
+    if (st == RSV_OK) st = rsv_sample_indexed(s->h, n, slot_offsets);
+    return st;
+}
+
+rsv_status rsv_jvm_fill_slots(rsv_jvm* s, const void* keys) {
+    g_local_error = 0;
+    if (!s->open) return closed();
+    return rsv_fill_slots(s->h, keys);
+}
+
 rsv_status rsv_jvm_result(rsv_jvm* s, void* out, int64_t cap, int64_t* out_n) {
     g_local_error = 0;
     if (!s->open) return closed();

@@ -48,6 +48,12 @@ rsv_status rsv_jvm_sample_array(rsv_jvm* s, const void* keys, const int64_t* has
  * RSV_HASH_PRECOMPUTED, else *hashes_out = NULL); rsv_jvm_stage_advance(n) records n keys written */
 rsv_status rsv_jvm_stage_span(rsv_jvm* s, void** keys_out, int64_t** hashes_out, int64_t* room);
 void rsv_jvm_stage_advance(rsv_jvm* s, int64_t n);
+/* Sampler.sampleAll over a known-size IndexedSeq (S:289-312 -> sampleIndexed S:261-273): the n
+ * elements seq(0 until n) are sampled by index alone; slot_offsets[k] receives per slot the offset
+ * of the element that now holds it, or -1.  The binding maps exactly those elements into
+ * keys[slot] (a k-key array, other entries ignored) and passes it to rsv_jvm_fill_slots. */
+rsv_status rsv_jvm_sample_indexed(rsv_jvm* s, int64_t n, int64_t* slot_offsets);
+rsv_status rsv_jvm_fill_slots(rsv_jvm* s, const void* keys);
 /* Sampler.result (S:59-60): writes min(count, k) keys; a single-use sampler closes (S:345-350) */
 rsv_status rsv_jvm_result(rsv_jvm* s, void* out, int64_t cap, int64_t* out_n);
 /* zero-copy form for a producer that writes keys itself (keys-only samplers): the free tail of

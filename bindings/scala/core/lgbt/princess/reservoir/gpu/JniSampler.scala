@@ -38,6 +38,9 @@ private[reservoir] object Jni {
   @native def destroy(session: Long): Unit
   @native def stageAcquire(session: Long): java.nio.ByteBuffer
   @native def stageCommit(session: Long, n: Long): Unit
+  @native def sampleIndexed(session: Long, n: Long, offsets: Array[Long]): Unit
+  @native def fillLongs(session: Long, keys: Array[Long]): Unit
+  @native def fillInts(session: Long, keys: Array[Int]): Unit
 }
 
 /** One native session (a malloc'd rsv_jvm, reservoir_jni.c) released exactly once: by a single-use
@@ -109,11 +112,17 @@ private[reservoir] final class JniSampler[A, B](
   private[this] val hashes = if (precomputed) new Array[Long](Batch) else null
   private[this] var n      = 0
   private[this] var open   = true
+  // Every native call passes the raw session pointer only, so the JIT may consider `this` dead
+  // during the call and let JniCleaner release the session under it.  A volatile store to this
+  // field after each call keeps `this` reachable until the call has returned (JDK 8 has no
+  // Reference.reachabilityFence).
+  @volatile private[this] var fence = 0
 
   private[this] def flush(): Unit =
     if (n > 0) {
       if (isLong) Jni.sampleLongs(session.get, longs, hashes, n) else Jni.sampleInts(session.get, ints, hashes, n)
       n = 0
+      fence = 1
     }
 
   def sample(element: A): Unit = {
@@ -123,6 +132,39 @@ private[reservoir] final class JniSampler[A, B](
     if (precomputed) hashes(n) = hash(b)
     n += 1
     if (n == Batch) flush()
+  }
+
+  /** sampleAll over a known-size IndexedSeq (Sampler.scala:289-312 -> sampleIndexed :261-273): the
+    * engine samples the indices alone, and `map` runs only on the elements that end up holding a
+    * slot -- no key crosses JNI or PCIe for the rest (the reference reads ~k ln(n/k) of them).
+    * Distinct samplers keep the trait's per-element default (Sampler.scala:50). */
+  override def sampleAll(elements: IterableOnce[A]): Unit = elements match {
+    case seq: collection.IndexedSeq[A @unchecked] if kind == Abi.KindElements && seq.knownSize > 0 =>
+      if (!open) throw new IllegalStateException(Abi.ClosedMessage)
+      flush()
+      val offsets = new Array[Long](maxSampleSize)
+      Jni.sampleIndexed(session.get, seq.length.toLong, offsets)
+      if (isLong) {
+        val ks = new Array[Long](maxSampleSize)
+        var j  = 0
+        while (j < maxSampleSize) {
+          val o = offsets(j)
+          if (o >= 0) ks(j) = map(seq(o.toInt)).asInstanceOf[Long]
+          j += 1
+        }
+        Jni.fillLongs(session.get, ks)
+      } else {
+        val ks = new Array[Int](maxSampleSize)
+        var j  = 0
+        while (j < maxSampleSize) {
+          val o = offsets(j)
+          if (o >= 0) ks(j) = map(seq(o.toInt)).asInstanceOf[Int]
+          j += 1
+        }
+        Jni.fillInts(session.get, ks)
+      }
+      fence = 1
+    case _ => super.sampleAll(elements)
   }
 
   def result(): IndexedSeq[B] = {
@@ -138,6 +180,7 @@ private[reservoir] final class JniSampler[A, B](
         val m   = Jni.resultInts(session.get, out)
         ArraySeq.unsafeWrapArray(if (m == out.length) out else Arrays.copyOf(out, m))
       }
+    fence = 1
     if (!reusable) { // the native side destroyed the handle inside result(); free the session now
       open = false
       session.release()

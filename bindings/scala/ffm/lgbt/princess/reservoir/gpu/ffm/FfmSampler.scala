@@ -47,6 +47,9 @@ private[reservoir] object Native {
   val rsvResult: MethodHandle =
     downcall("rsv_result", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS))
   val rsvLastError: MethodHandle = downcall("rsv_last_error", FunctionDescriptor.of(ADDRESS))
+  val rsvSampleIndexed: MethodHandle =
+    downcall("rsv_sample_indexed", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS))
+  val rsvFillSlots: MethodHandle = downcall("rsv_fill_slots", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS))
 
   val cleaner: Cleaner = Cleaner.create()
 
@@ -134,6 +137,39 @@ private[reservoir] final class FfmSampler[A, B](
     else stage.setAtIndex(JAVA_INT, filled, b.asInstanceOf[Int])
     if (precomputed) stageHash.setAtIndex(JAVA_LONG, filled, hash(b))
     filled += 1
+  }
+
+  /** sampleAll over a known-size IndexedSeq (Sampler.scala:289-312 -> sampleIndexed :261-273): the
+    * engine samples the indices alone (rsv_sample_indexed) and `map` runs only on the elements now
+    * holding a slot, whose keys go back in one downcall (rsv_fill_slots).  Distinct samplers keep
+    * the trait's per-element default (Sampler.scala:50). */
+  override def sampleAll(elements: IterableOnce[A]): Unit = elements match {
+    case seq: collection.IndexedSeq[A @unchecked] if kind == Abi.KindElements && seq.knownSize > 0 =>
+      if (!open) throw new IllegalStateException(Abi.ClosedMessage)
+      if (filled > 0) { // the staged keys come first in index order
+        val f = filled
+        filled = 0
+        check(rsvStageCommit.invoke(handle, f).asInstanceOf[Int])
+      }
+      cap = 0
+      val tmp = Arena.ofConfined()
+      try {
+        val offsets = tmp.allocate(8L * maxSampleSize, 8L)
+        check(rsvSampleIndexed.invoke(handle, seq.length.toLong, offsets).asInstanceOf[Int])
+        val ks = tmp.allocate(keys.width.toLong * maxSampleSize, 8L)
+        var j  = 0
+        while (j < maxSampleSize) {
+          val o = offsets.getAtIndex(JAVA_LONG, j.toLong)
+          if (o >= 0) {
+            val b = map(seq(o.toInt))
+            if (isLong) ks.setAtIndex(JAVA_LONG, j.toLong, b.asInstanceOf[Long])
+            else ks.setAtIndex(JAVA_INT, j.toLong, b.asInstanceOf[Int])
+          }
+          j += 1
+        }
+        check(rsvFillSlots.invoke(handle, ks).asInstanceOf[Int])
+      } finally tmp.close()
+    case _ => super.sampleAll(elements)
   }
 
   def result(): IndexedSeq[B] = {

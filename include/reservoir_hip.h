@@ -130,6 +130,21 @@ rsv_status rsv_stage_commit(rsv_sampler* s, int64_t n);
 rsv_status rsv_sample_batch(rsv_sampler* s, const void* keys, int64_t n, int32_t mem,
                             const int64_t* hashes);
 
+/* Sampler.sampleAll over a known-size IndexedSeq WITHOUT its keys (sampleAllImpl S:289-312 ->
+ * sampleIndexed S:261-273, which reads only seq(nextSampleCount - count - 1) per eviction): the n
+ * elements at global indices [count, count+n) are sampled by index alone -- a draw depends only on
+ * the index (PHILOX_R), or the eviction events come from java.util.Random (JAVA_L) -- so only the
+ * elements that end up in the reservoir need `map`.  slot_offsets_host[k] receives, per slot, the
+ * offset in [0, n) of the element that now holds it (fill phase S:253-255 included), or -1 where
+ * the slot did not change.  The caller maps exactly those elements (seq(offset)) and passes their
+ * keys to rsv_fill_slots; until then every other call on the handle returns RSV_E_ILLEGAL_STATE.
+ * ELEMENTS samplers only (Sampler.distinct maps every element: its sampleAll is the trait default,
+ * S:50).  One K1 pass over the index range, k x 8 B back over PCIe -- no key crosses the link. */
+rsv_status rsv_sample_indexed(rsv_sampler* s, int64_t n, int64_t* slot_offsets_host);
+/* The keys owed after rsv_sample_indexed: keys_host holds k keys in slot order; entry j is read
+ * only where slot_offsets_host[j] >= 0 (the rest may be anything). */
+rsv_status rsv_fill_slots(rsv_sampler* s, const void* keys_host);
+
 /* Sampler.result() (S:59-60; resultImpl S:318-331; RandomValues.result S:411).  Writes
  * min(count, k) keys (ELEMENTS: slot order, which is part of the reference result) or the distinct
  * set (DISTINCT: ascending scrambled hash; the reference's order is HashSet order) into host
@@ -211,9 +226,14 @@ typedef struct rsv_distinct_info {
                                * left the batch to the chunk loop (the set restored) */
 } rsv_distinct_info;
 rsv_status rsv_get_distinct_info(rsv_sampler* s, rsv_distinct_info* out);
+/* Keep every logged candidate on the host for rsv_export_log (ORDERED samplers; off by default: the
+ * archive holds 12-16 B per replayed candidate, up to 2^27 of them).  Call it before the first
+ * sample -- switched on later, the log is reported as not retained. */
+rsv_status rsv_retain_log(rsv_sampler* s, int32_t on);
 /* Every logged candidate with scrambled hash < bound (all of them for bound = INT64_MAX), in
  * arrival order, into host buffers of cap entries (keys as key_width values); *out_n = the count
- * (RSV_E_ILLEGAL_ARGUMENT when it exceeds cap).  RSV_E_UNSUPPORTED if the log was not retained.
+ * (RSV_E_ILLEGAL_ARGUMENT when it exceeds cap; cap = 0 is a count-only query, the buffers may be
+ * NULL).  RSV_E_UNSUPPORTED if the log was not retained (rsv_retain_log).
  * Stays available after rsv_merge_state until the sampler samples again. */
 rsv_status rsv_export_log(rsv_sampler* s, int64_t bound, int64_t* hashes_host, void* keys_host, int64_t cap,
                           int64_t* out_n);
@@ -222,14 +242,22 @@ rsv_status rsv_export_log(rsv_sampler* s, int64_t bound, int64_t* hashes_host, v
 rsv_status rsv_merge_log(rsv_sampler* s, const int64_t* hashes_host, const void* keys_host, int64_t n,
                          int64_t total_count);
 
-/* Packed form of the two calls above for ELEMENTS samplers, the one-collective combine of
- * reservoir_amd/distributed.py: row_dev[0..k) = global index per slot (-1 = empty),
- * row_dev[k..2k) = the slot's key widened to int64 (sign-extended for 4-byte keys); for wide keys
- * (key_width > 8) the k keys follow as key_width/8 int64 words each.  One kernel, no host wait on
- * a caller stream. */
+/* Packed form of rsv_export_state / rsv_merge_state, the one-collective combine of
+ * reservoir_amd/distributed.py.  One kernel, no host wait on a caller stream.
+ *   ELEMENTS: row_dev[0..k) = global index per slot (-1 = empty), row_dev[k..2k) = the slot's key
+ *     widened to int64 (sign-extended for 4-byte keys); for wide keys (key_width > 8) the k keys
+ *     follow as key_width/8 int64 words each.
+ *   DISTINCT: 2k + 6 words: [keys widened to int64 (k) | scrambled hashes (k) | n, count, tied,
+ *     max_hash, log_retained, ordered] -- the set ascending by (hash, key), n entries valid. */
 rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev);
 /* Merge `parts` packed rows (row p at rows_dev + p*row_stride, row_stride >= the row length), e.g. the output
- * of an all-gather of every rank's rsv_export_packed row: per slot the largest global index wins. */
+ * of an all-gather of every rank's rsv_export_packed row.
+ *   ELEMENTS: per slot the largest global index wins.
+ *   DISTINCT: the bottom-k by (hash, key) of the union with the sampler's set, on the device (four
+ *     kernels, no host wait: the set's size and tie state are read back at the next call on the
+ *     handle); `tied` as rsv_merge_state.  On a caller stream the rows must stay valid and
+ *     unchanged until the next call on the handle returns (a degenerate hash that overflows the
+ *     merge's buckets is redone from them then). */
 rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t parts, int64_t row_stride,
                             int64_t total_count);
 

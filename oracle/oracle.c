@@ -155,6 +155,33 @@ void or_algo_l_sample_all_indexed(or_algo_l* s, const int64_t* elems, int64_t n)
     s->count = start_count + n;
 }
 
+/* The same sampleIndexed walk over the virtual sequence seq(i) = base_value + i (e.g. a Range,
+ * SamplerTest.scala:117-142 feeds 1 to 3000): no element array, so a 1e9-element stream costs only
+ * its ~k ln(n/k) evictions.  Element i is read exactly where or_algo_l_sample_all_indexed reads
+ * elems[i]. */
+void or_algo_l_sample_all_iota(or_algo_l* s, int64_t base_value, int64_t n) {
+    if (n <= 0) return;
+    int64_t start_count = s->count, i = 0;
+    if (start_count < s->k) {
+        int64_t c = start_count;
+        while (c < s->k && i < n) { s->samples[c] = base_value + i; c++; i++; }
+    }
+    int64_t start = i, len = n - i; /* 64-bit: a Range is not limited to Int indices here */
+    int64_t cnt = start_count + i;
+    while (len > 0) {
+        int64_t nsc = s->next_sample_count;
+        int64_t off = nsc - cnt;
+        if (!(len >= off)) break;
+        if (off <= 0) break;
+        int64_t next_start = start + off;
+        algo_l_evict(s, base_value + next_start - 1, cnt + off);
+        start = next_start;
+        len -= off;
+        cnt = nsc;
+    }
+    s->count = start_count + n;
+}
+
 int64_t or_algo_l_result(const or_algo_l* s, int64_t* out) {
     /* resultImpl, Sampler.scala:318-331: the array is min(count, k) long in every growth state */
     int64_t m = s->count < s->k ? s->count : s->k;

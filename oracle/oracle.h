@@ -63,6 +63,7 @@ void or_algo_l_free(or_algo_l* s);
 void or_algo_l_sample(or_algo_l* s, int64_t elem);
 /* sampleAll over an IndexedSeq with knownSize, Sampler.scala:289-312 + sampleIndexed :261-273 */
 void or_algo_l_sample_all_indexed(or_algo_l* s, const int64_t* elems, int64_t n);
+void or_algo_l_sample_all_iota(or_algo_l* s, int64_t base_value, int64_t n);
 /* resultImpl, Sampler.scala:318-331: returns min(count, k) */
 int64_t or_algo_l_result(const or_algo_l* s, int64_t* out);
 

@@ -57,6 +57,7 @@ def lib():
     L.or_algo_l_free.argtypes = [C.POINTER(_AlgoL)]
     L.or_algo_l_sample.argtypes = [C.POINTER(_AlgoL), C.c_int64]
     L.or_algo_l_sample_all_indexed.argtypes = [C.POINTER(_AlgoL), i64p, C.c_int64]
+    L.or_algo_l_sample_all_iota.argtypes = [C.POINTER(_AlgoL), C.c_int64, C.c_int64]
     L.or_algo_l_result.argtypes = [C.POINTER(_AlgoL), i64p]; L.or_algo_l_result.restype = C.c_int64
     L.or_distinct_new.argtypes = [C.c_int32, C.c_int64, C.c_int]; L.or_distinct_new.restype = C.c_void_p
     L.or_distinct_free.argtypes = [C.c_void_p]
@@ -135,6 +136,11 @@ class AlgoL:
     def sample_all(self, xs) -> None:
         a = np.ascontiguousarray(np.asarray(xs, dtype=np.int64))
         lib().or_algo_l_sample_all_indexed(C.byref(self._s), a, a.size)
+
+    def sample_all_iota(self, base_value: int, n: int) -> None:
+        """sampleAll over the Range base_value until base_value + n (the sampleIndexed walk without
+        an element array, or_algo_l_sample_all_iota)."""
+        lib().or_algo_l_sample_all_iota(C.byref(self._s), int(base_value), int(n))
 
     def result(self) -> np.ndarray:
         out = np.zeros(self.k, dtype=np.int64)

@@ -813,7 +813,7 @@ __device__ __forceinline__ bool ent_less3(int64_t ha, KeyT ka, uint32_t ia, int6
 // one wave per bucket: sort by (h, key, tag), keep the first of each (h, key) run (its earliest
 // arrival), write them back compacted; each kept element adds +1 / -1 at ranges r_a / r_h + 1 of
 // the block's difference array (sdiff, LDS)
-template <typename KeyT, int R, int AGG>
+template <typename KeyT, int R>
 __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(int64_t* gh, KeyT* gk, uint32_t* gi, uint32_t n,
                                                             const int64_t* sb, const int64_t* stt, int nr,
                                                             int* sdiff) {
@@ -922,33 +922,18 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(int64_t* gh, KeyT* g
         // bucket's elements share r_h almost always: one atomic for the wave's -1s then, instead of
         // up to 64 on one LDS word
         const bool part = ra <= rh;
-        if constexpr (AGG == 0) {  // one atomic per element and end (RSV_SCHED_AGG=0, A/B)
-            if (part) {
-                atomicAdd(&sdiff[ra], 1);
+        const unsigned long long pm = __ballot(part);
+        if (pm) {
+            const int lead = __builtin_ctzll(pm);
+            const int rh0 = __shfl(rh, lead);
+            if (__ballot(part && rh != rh0) == 0) {
+                if ((int)(threadIdx.x & 63) == lead) atomicAdd(&sdiff[rh0 + 1], -(int)__popcll(pm));
+            } else if (part) {
                 atomicAdd(&sdiff[rh + 1], -1);
             }
-        } else {
-            const unsigned long long pm = __ballot(part);
-            if (pm) {
-                const int lead = __builtin_ctzll(pm);
-                const int rh0 = __shfl(rh, lead);
-                if (__ballot(part && rh != rh0) == 0) {
-                    if ((int)(threadIdx.x & 63) == lead) atomicAdd(&sdiff[rh0 + 1], -(int)__popcll(pm));
-                } else if (part) {
-                    atomicAdd(&sdiff[rh + 1], -1);
-                }
-                if constexpr (AGG == 2) {  // +1s too: one atomic per distinct r_a of the wave
-                    unsigned long long left = pm;
-                    while (left) {
-                        const int ra0 = __shfl(ra, __builtin_ctzll(left));
-                        const unsigned long long same = __ballot(part && ra == ra0);
-                        if ((int)(threadIdx.x & 63) == __builtin_ctzll(same)) atomicAdd(&sdiff[ra0], (int)__popcll(same));
-                        left &= ~same;
-                    }
-                } else if (part) {
-                    atomicAdd(&sdiff[ra], 1);
-                }
-            }
+            // (the +1s stay one atomic each: aggregating them per distinct r_a was slower, 69 vs
+            // 60 us, DESIGN.md 5 decision 6)
+            if (part) atomicAdd(&sdiff[ra], 1);
         }
         base += (uint32_t)__popcll(bal);
         prev_h_last = shfl_any(h[r], 63);
@@ -957,7 +942,7 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(int64_t* gh, KeyT* g
     return base;
 }
 
-template <typename KeyT, int AGG>
+template <typename KeyT>
 __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap, int64_t* __restrict__ ctl,
                                                      int32_t log_bmax, int64_t* __restrict__ bh, KeyT* __restrict__ bk,
                                                      uint32_t* __restrict__ bi, const SchedDev* __restrict__ sd,
@@ -983,9 +968,9 @@ __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap
         uint32_t* gi = bi + (size_t)b * kBucketCap;
         uint32_t nd = 0;
         if (n > 0)
-            nd = n <= 64    ? wave_sort_bucket_tagged<KeyT, 1, AGG>(gh, gk, gi, n, sb, stt, nr, sdiff)
-                 : n <= 128 ? wave_sort_bucket_tagged<KeyT, 2, AGG>(gh, gk, gi, n, sb, stt, nr, sdiff)
-                            : wave_sort_bucket_tagged<KeyT, 4, AGG>(gh, gk, gi, n, sb, stt, nr, sdiff);
+            nd = n <= 64    ? wave_sort_bucket_tagged<KeyT, 1>(gh, gk, gi, n, sb, stt, nr, sdiff)
+                 : n <= 128 ? wave_sort_bucket_tagged<KeyT, 2>(gh, gk, gi, n, sb, stt, nr, sdiff)
+                            : wave_sort_bucket_tagged<KeyT, 4>(gh, gk, gi, n, sb, stt, nr, sdiff);
         if ((threadIdx.x & 63) == 0) {
             *bdist = nd;
             if (nd) atomicAdd(bucket_group(ctl, log_bmax) + (b >> 4), nd);
@@ -993,7 +978,6 @@ __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap
         }
     }
     __syncthreads();
-    if (AGG == 3) return;  // DEV A/B: the accumulator atomics' share of the kernel (wrong verdict)
     int* acc = vacc + (size_t)(blockIdx.x % kVerifyCopies) * (kMaxRanges + 1);
     for (int i = threadIdx.x; i <= nr; i += blockDim.x)
         if (sdiff[i]) atomicAdd(&acc[i], sdiff[i]);
@@ -1085,6 +1069,226 @@ __global__ __launch_bounds__(kBlock) void permute_log(const uint32_t* __restrict
         oh[t] = h[p];
         ok[t] = k[p];
     }
+}
+
+// ---- device combine of packed rows (rsv_export_packed / rsv_merge_packed on DISTINCT samplers) ---
+// A row is one sampler's set: [keys widened to int64 (k) | hashes (k) | meta], ascending (h, key),
+// meta = n, count, tied, max_hash, log_retained, ordered (reservoir_amd/distributed.py reads it).
+// The merge of `parts` rows with the sampler's own set (run 0) is the bottom-k by (h, key) of the
+// union -- the bucketed merge of the filter path, fed from the runs directly: every run is already
+// sorted, so a bucket's entries are one contiguous range per run.  rows_bounds finds the ranges in
+// one streaming pass (no atomics), rows_sort gathers each bucket (one wave) from the runs into LDS,
+// sorts and dedups it, bucket_emit places the distinct entries by rank, merge_publish hands the
+// control words to the host (coherent memory + flag) -- four dispatches and no host wait.
+// Entries above `top` are dropped first: top = the smallest maximum of a FULL run (k entries: the
+// bottom-k of the union lies at or below it) and at most the largest hash present.
+constexpr int kRowMeta = 6;
+
+template <typename KeyT>
+struct Runs {
+    const int64_t* rows;
+    int64_t stride, k;
+    const int64_t* set_h;
+    const KeyT* set_k;
+    int64_t m;
+    __device__ __forceinline__ int64_t n(int r) const {
+        if (r == 0) return m;
+        const int64_t v = rows[(int64_t)(r - 1) * stride + 2 * k];
+        return v < 0 ? 0 : (v > k ? k : v);
+    }
+    __device__ __forceinline__ int64_t h(int r, int64_t i) const {
+        return r == 0 ? set_h[i] : rows[(int64_t)(r - 1) * stride + k + i];
+    }
+    __device__ __forceinline__ KeyT key(int r, int64_t i) const {
+        return r == 0 ? set_k[i] : (KeyT)rows[(int64_t)(r - 1) * stride + i];
+    }
+    __device__ __forceinline__ int64_t max_h(int r) const { return rows[(int64_t)(r - 1) * stride + 2 * k + 3]; }
+    __device__ __forceinline__ bool tied(int r) const { return rows[(int64_t)(r - 1) * stride + 2 * k + 2] != 0; }
+    __device__ __forceinline__ bool ordered(int r) const { return rows[(int64_t)(r - 1) * stride + 2 * k + 5] != 0; }
+};
+
+// the cut and its tie flag (thread-local; every workgroup of rows_bounds computes it, <= 64 runs).
+// T = the smallest maximum of a full run; tiedT: a full run whose own boundary bucket was
+// oversubscribed sits at T (its export holds only part of that bucket -- with the merged maximum at
+// T the union's tie word cannot see it)
+template <typename KeyT>
+__device__ __forceinline__ void runs_top(const Runs<KeyT>& R, int parts, int64_t set_max, bool set_over,
+                                         int64_t* top, int64_t* T_out, bool* tiedT, bool* all_ordered) {
+    int64_t T = R.m == R.k ? set_max : INT64_MAX;
+    int64_t mx = R.m > 0 ? set_max : INT64_MIN;
+    bool tt = R.m == R.k && set_over, ord = true;
+    for (int r = 1; r <= parts; ++r) {
+        const int64_t n = R.n(r), mh = R.max_h(r);
+        ord = ord && R.ordered(r);
+        if (n > 0) mx = std::max(mx, mh);
+        if (n == R.k) {
+            const bool t = R.tied(r);
+            if (mh < T) {
+                T = mh;
+                tt = t;
+            } else if (mh == T) {
+                tt = tt || t;
+            }
+        }
+    }
+    *top = std::min(T, mx);
+    *T_out = T;
+    *tiedT = tt;
+    *all_ordered = ord;
+}
+
+// start[r * (B + 1) + b] = first index of run r whose bucket is >= b (entries above top: bucket B).
+// One thread per index i in [0, n_r] (i = n_r closes the run); grid (x, parts + 1), y = run.
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void rows_bounds(Runs<KeyT> R, int32_t parts, int64_t set_max, int32_t set_over,
+                                                      uint32_t lb, int64_t* __restrict__ ctl, int32_t log_bmax,
+                                                      uint32_t* __restrict__ start) {
+    __shared__ int64_t s_top;
+    __shared__ uint64_t s_q;
+    const int r = (int)blockIdx.y;
+    if (threadIdx.x == 0) {
+        int64_t top, T;
+        bool tiedT, ord;
+        runs_top(R, parts, set_max, set_over != 0, &top, &T, &tiedT, &ord);
+        const uint64_t span = (uint64_t)top - (uint64_t)INT64_MIN;
+        s_top = top;
+        s_q = span == UINT64_MAX ? 1ull : UINT64_MAX / (span + 1);
+        if (blockIdx.x == 0 && r == 0) {
+            ctl[5] = 0;  // bucket_emit's tie word
+            ctl[6] = (tiedT ? 2 : 0) | (ord ? 1 : 0);
+            ctl[7] = T;
+        }
+    }
+    if (blockIdx.x == 0 && r == 0) zero_bucket_groups(ctl, log_bmax);
+    __syncthreads();
+    const int64_t top = s_top;
+    const BucketMap map(s_q, lb);
+    const uint32_t B = 1u << lb;
+    const int64_t n = R.n(r);
+    uint32_t* st = start + (size_t)r * (B + 1);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += stride) {
+        uint32_t bi = B;
+        if (i < n) {
+            const int64_t h = R.h(r, i);
+            if (h <= top) bi = map(h);
+        }
+        int64_t bp = -1;
+        if (i > 0) {
+            const int64_t h = R.h(r, i - 1);
+            bp = h <= top ? (int64_t)map(h) : (int64_t)B;
+        }
+        for (int64_t b = bp + 1; b <= (int64_t)bi; ++b) st[b] = (uint32_t)i;
+    }
+}
+
+// one wave per bucket: its entries from every run (contiguous ranges by rows_bounds) into LDS,
+// sorted by (h, key), duplicates dropped (wave_sort_bucket), the distinct ones written compacted to
+// the bucket area; bucket_distinct / group sums as bucket_sort leaves them.  > kBucketCap entries (a
+// degenerate hash): the overflow word, and the host redoes the merge on the radix-sort path.
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void rows_sort(Runs<KeyT> R, int32_t parts, uint32_t lb,
+                                                    const uint32_t* __restrict__ start, int64_t* __restrict__ ctl,
+                                                    int32_t log_bmax, int64_t* __restrict__ bh, KeyT* __restrict__ bk) {
+    constexpr int kMaxRuns = 65;
+    __shared__ int64_t s_h[kBlock / 64][kBucketCap];
+    __shared__ KeyT s_k[kBlock / 64][kBucketCap];
+    __shared__ int64_t s_lo[kBlock / 64][kMaxRuns], s_ex[kBlock / 64][kMaxRuns + 1];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t B = 1u << lb;
+    const uint32_t b = blockIdx.x * (kBlock / 64) + w;
+    if (b >= B) return;
+    const int nr = parts + 1;
+    // per run: [lo, hi) of this bucket; exclusive prefix of the counts (runs > 64: a second round)
+    int64_t base = 0;
+    for (int r0 = 0; r0 < nr; r0 += 64) {
+        const int r = r0 + (int)lane;
+        int64_t lo = 0, cnt = 0;
+        if (r < nr) {
+            lo = start[(size_t)r * (B + 1) + b];
+            cnt = (int64_t)start[(size_t)r * (B + 1) + b + 1] - lo;
+        }
+        int64_t incl = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t v = shfl_any(incl, (int)(lane >= (uint32_t)off ? lane - off : lane));
+            if (lane >= (uint32_t)off) incl += v;
+        }
+        if (r < nr) {
+            s_lo[w][r] = lo;
+            s_ex[w][r] = base + incl - cnt;
+        }
+        base += shfl_any(incl, 63);
+    }
+    if (lane == 0) s_ex[w][nr] = base;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t* bdist = bucket_distinct(ctl, log_bmax) + b;
+    if (base > (int64_t)kBucketCap) {
+        if (lane == 0) {
+            ctl[1] = 1;
+            *bdist = 0;
+        }
+        return;
+    }
+    const uint32_t n = (uint32_t)base;
+    if (n == 0) {
+        if (lane == 0) *bdist = 0;
+        return;
+    }
+    for (uint32_t j = lane; j < n; j += 64) {
+        int r = 0;
+        while (s_ex[w][r + 1] <= (int64_t)j) ++r;
+        const int64_t i = s_lo[w][r] + ((int64_t)j - s_ex[w][r]);
+        s_h[w][j] = R.h(r, i);
+        s_k[w][j] = R.key(r, i);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nd = n <= 64    ? wave_sort_bucket<KeyT, 1>(s_h[w], s_k[w], n, bdist)
+                        : n <= 128 ? wave_sort_bucket<KeyT, 2>(s_h[w], s_k[w], n, bdist)
+                                   : wave_sort_bucket<KeyT, 4>(s_h[w], s_k[w], n, bdist);
+    __builtin_amdgcn_wave_barrier();
+    int64_t* gh = bh + (size_t)b * kBucketCap;
+    KeyT* gk = bk + (size_t)b * kBucketCap;
+    for (uint32_t j = lane; j < nd; j += 64) {
+        gh[j] = s_h[w][j];
+        gk[j] = s_k[w][j];
+    }
+    if (lane == 0 && nd) atomicAdd(bucket_group(ctl, log_bmax) + (b >> 4), nd);
+}
+
+// the merge's control words (ctl[0..7]) to coherent host memory + flag; re-arms ctl[0..1]
+__global__ __launch_bounds__(64) void merge_publish(int64_t* __restrict__ ctl, int64_t* dst, uint32_t* flag,
+                                                    uint32_t gen) {
+    if (threadIdx.x < 8) {
+        const int64_t v = ctl[threadIdx.x];
+        dst[threadIdx.x] = v;
+        if (threadIdx.x < 2) ctl[threadIdx.x] = 0;
+    }
+    publish_flag(flag, gen);
+}
+
+// one sampler's set as a packed row
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void export_row_kernel(const int64_t* __restrict__ set_h,
+                                                            const KeyT* __restrict__ set_k, int64_t m, int64_t k,
+                                                            int64_t* __restrict__ row, int64_t count, int64_t tied,
+                                                            int64_t max_hash, int64_t retained, int64_t ordered) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < k; i += stride) {
+        row[i] = i < m ? (int64_t)set_k[i] : 0;
+        row[k + i] = i < m ? set_h[i] : INT64_MAX;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < kRowMeta) {
+        const int64_t meta[kRowMeta] = {m, count, tied, max_hash, retained, ordered};
+        row[2 * k + threadIdx.x] = meta[threadIdx.x];
+    }
+}
+
+// int64-widened row keys -> KeyT (the overflow fallback's merge_into_set input)
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void narrow_keys(const int64_t* __restrict__ src, int64_t n, KeyT* __restrict__ dst) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = (KeyT)src[i];
 }
 
 inline unsigned grid_1d(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -1179,14 +1383,32 @@ struct DistinctState {
     // the replica consumed (arrival order, host) + the segments still in the log, and the segments
     // logged before the last merge -- together every candidate logged since creation (`arch_ok`).
     // Sampling again after a merge drops them (the merged state has no single arrival order).
-    std::vector<int64_t> arch_h, arch_k;
+    // Opt-in (rsv_retain_log, before the first sample): the archive holds 12-16 B per consumed
+    // candidate on the host, up to kArchMax of them.
+    bool retain = false;
+    std::vector<int64_t> arch_h, arch_k;  // keys: arch_k (8-byte keys) or arch_k4 (4-byte keys)
+    std::vector<int32_t> arch_k4;
     bool arch_ok = true;
     std::vector<Seg> pre_segs;
     bool merged = false;
     int64_t sched_passes = 0, sched_fallbacks = 0;  // rsv_distinct_info counters
+    // the replica lags the set arrays (a merge replaced the set): rebuilt from them before the
+    // next replay, which is the only reader (a merge without a later tie never pays for it)
+    bool rep_stale = false;
+    // device combine of packed rows (distinct_merge_rows): enqueued without a host wait; the host
+    // fields (m, max_h, set_top, over) are settled from its published words at the next call
+    bool pend = false;
+    uint32_t pend_gen = 0;
+    uint32_t pend_lb = 0;
+    const int64_t* pend_rows = nullptr;  // caller rows, valid until the settle (overflow fallback)
+    int32_t pend_parts = 0;
+    int64_t pend_stride = 0;
+    uint32_t* mstart = nullptr;  // [(parts + 1) x (B + 1)] bucket starts of every run
+    int64_t mstart_cap = 0;
 };
 
-// ~2 GB of host archive (16 B per candidate): beyond it rsv_export_log reports the log as not retained
+// <= 2 GB of host archive (12-16 B per candidate): beyond it rsv_export_log reports the log as not
+// retained
 constexpr int64_t kArchMax = (int64_t)1 << 27;
 
 void distinct_set_timer(DistinctState* d, KernelTimer* t) { d->timer = t; }
@@ -1342,7 +1564,7 @@ void distinct_destroy(DistinctState* d) {
     void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->ctl, d->bh, d->bk, d->mh0, d->mh1, d->mk0,
                   d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp, d->log_h, d->log_k, d->log_i,
                   d->perm, d->sorted_i, d->ord_h, d->ord_k, d->sdev, d->sctl, d->sbh, d->sbk, d->sbi, d->vacc,
-                  d->bak_h, d->bak_k};
+                  d->bak_h, d->bak_k, d->mstart};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
     pool_host_free(d->h_pinned);
     pool_host_free(d->hc);
@@ -1812,26 +2034,47 @@ static void archive_drop(DistinctState* d) {
     d->arch_ok = false;
     std::vector<int64_t>().swap(d->arch_h);
     std::vector<int64_t>().swap(d->arch_k);
+    std::vector<int32_t>().swap(d->arch_k4);
+}
+
+// The replica from the set arrays, in (h, key) order, after a merge replaced the set (a merged set
+// has no single arrival order; rsv_merge_log is the exact form).
+template <typename KeyT>
+static hipError_t rebuild_replica(DistinctState* d, hipStream_t st) {
+    std::vector<int64_t> hh((size_t)d->m);
+    std::vector<KeyT> kk((size_t)d->m);
+    hipError_t e = hipSuccess;
+    if (d->m) {
+        if ((e = hipMemcpyAsync(hh.data(), d->set_h, (size_t)d->m * 8, hipMemcpyDeviceToHost, st))) return e;
+        if ((e = hipMemcpyAsync(kk.data(), d->set_k, (size_t)d->m * sizeof(KeyT), hipMemcpyDeviceToHost, st))) return e;
+        if ((e = hipStreamSynchronize(st))) return e;
+    }
+    d->rep.reset(d->k);
+    for (int64_t i = 0; i < d->m; ++i) d->rep.sample((int64_t)kk[(size_t)i], hh[(size_t)i]);
+    if (d->m == d->k) d->max_h = d->rep.max_hash;
+    d->rep_stale = false;
+    return hipSuccess;
 }
 
 // Every logged segment, in order, through the host replica (RandomValues.sample on each candidate,
-// Sampler.scala:394-409); the consumed candidates are kept in the host archive for rsv_export_log.
+// Sampler.scala:394-409); the consumed candidates are kept in the host archive for rsv_export_log
+// when the sampler retains its log (rsv_retain_log).
 template <typename KeyT>
 static hipError_t replay_log(DistinctState* d, hipStream_t st) {
     hipError_t e;
+    if (d->rep_stale && (e = rebuild_replica<KeyT>(d, st))) return e;
     for (const DistinctState::Seg& g : d->segs) {
         if (g.c == 0) continue;
         if ((e = segment_to_host<KeyT>(d, g, st))) return e;
         const KeyT* pk = (const KeyT*)d->pk;
         const int64_t* ph = d->ph;
-        if (d->arch_ok) {
+        if (d->retain && d->arch_ok) {
             if ((int64_t)d->arch_h.size() + g.c > kArchMax) {
                 archive_drop(d);
             } else {
                 d->arch_h.insert(d->arch_h.end(), ph, ph + g.c);
-                const size_t a = d->arch_k.size();
-                d->arch_k.resize(a + (size_t)g.c);
-                for (int64_t t = 0; t < g.c; ++t) d->arch_k[a + (size_t)t] = (int64_t)pk[t];
+                if constexpr (sizeof(KeyT) == 8) d->arch_k.insert(d->arch_k.end(), pk, pk + g.c);
+                else d->arch_k4.insert(d->arch_k4.end(), pk, pk + g.c);
             }
         }
         d->rep.sample_run(g.c, [&](int64_t t) { return (int64_t)pk[t]; }, [&](int64_t t) { return ph[t]; });
@@ -2019,17 +2262,10 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
         STRY(hipGetLastError());
     }
     if (d->timer) d->timer->mark(st);
-    {
-        // the difference array's LDS atomics aggregated per wave (RSV_SCHED_AGG: 0 none, 1 the -1s,
-        // 2 both; read once, for A/B runs)
-        static const int agg = [] {
-            const char* e = std::getenv("RSV_SCHED_AGG");
-            return e ? std::atoi(e) : 1;
-        }();
-        auto kern = agg == 0 ? sched_sort<KeyT, 0> : agg == 2 ? sched_sort<KeyT, 2> : agg == 3 ? sched_sort<KeyT, 3> : sched_sort<KeyT, 1>;
-        hipLaunchKernelGGL(kern, dim3((B + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, k, cap, d->sctl,
-                           d->log_bmax_s, d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
-    }
+    // the difference array's -1s aggregated per wave (one LDS atomic per bucket, not per element):
+    // sched_sort 64.9 -> 60.4 us (DESIGN.md 5 decision 6)
+    hipLaunchKernelGGL(sched_sort<KeyT>, dim3((B + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, k, cap,
+                       d->sctl, d->log_bmax_s, d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
     hipLaunchKernelGGL(bucket_emit<KeyT>, dim3((B + kEmitBuckets - 1) / kEmitBuckets), dim3(kBlock), 0, st, k, cap,
                        d->sctl, d->log_bmax_s, (const int64_t*)d->sbh, (const KeyT*)bk, k, d->set_h, (KeyT*)d->set_k,
                        (int32_t)sp->lb);
@@ -2229,6 +2465,7 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
 
 int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* hashes, int64_t n,
                            hipStream_t st) {
+    if (int rc = distinct_settle(d, st)) return rc;
     if (d->merged && n > 0) {  // sampling on after a merge: the pre-merge candidates are history
         d->merged = false;
         d->pre_segs.clear();
@@ -2243,6 +2480,7 @@ int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* ha
 }
 
 int distinct_finalize(DistinctState* d, hipStream_t st) {
+    if (int rc = distinct_settle(d, st)) return rc;
     if (!d->ordered || d->exact) return RSV_OK;
     hipError_t e = d->kw == 8 ? replay_log<int64_t>(d, st) : replay_log<int32_t>(d, st);
     if (e == hipSuccess) e = d->kw == 8 ? upload_replica<int64_t>(d, st) : upload_replica<int32_t>(d, st);
@@ -2267,13 +2505,25 @@ void distinct_info(const DistinctState* d, int32_t* ordered, int32_t* tied, int3
     *sched_fallbacks = d->sched_fallbacks;
     *ordered = d->ordered;
     *tied = d->m == d->k && d->over;
-    *retained = d->ordered && d->arch_ok;
+    *retained = d->ordered && d->retain && d->arch_ok;
     *size = d->m;
     *max_hash = d->m ? d->set_top : INT64_MIN;
     int64_t c = (int64_t)d->arch_h.size();
     for (const DistinctState::Seg& g : d->pre_segs) c += g.c;
     for (const DistinctState::Seg& g : d->segs) c += g.c;
     *log_entries = d->ordered ? c : 0;
+}
+
+// After a merge replaced the set: an ordered sampler's replica starts over from the union (rebuilt
+// lazily, rep_stale); the logged segments stay readable for rsv_export_log until the next sample.
+static void merged_bookkeeping(DistinctState* d) {
+    d->spec_ok = false;
+    if (!d->ordered) return;
+    d->rep_stale = true;
+    d->pre_segs.insert(d->pre_segs.end(), d->segs.begin(), d->segs.end());
+    d->segs.clear();
+    d->exact = true;
+    d->merged = true;
 }
 
 // Merge `parts` external (key, hash) runs (device; run p at keys + p part_len, part_n[p] entries)
@@ -2286,6 +2536,7 @@ int distinct_merge_parts(DistinctState* d, const void* keys_dev, const int64_t* 
                          int32_t parts, int64_t part_len, hipStream_t st) {
     int64_t total = 0;
     for (int32_t p = 0; p < parts; ++p) total += std::max<int64_t>(0, std::min(part_n[p], part_len));
+    if (int rc = distinct_settle(d, st)) return rc;
     if (total == 0) return RSV_OK;
     if (int rc = distinct_finalize(d, st)) return rc;
     bool tie = d->m == d->k && d->over;
@@ -2310,30 +2561,174 @@ int distinct_merge_parts(DistinctState* d, const void* keys_dev, const int64_t* 
         }
     }
     d->over = tie;
-    d->spec_ok = false;
-    if (d->ordered) {
-        std::vector<int64_t> hh((size_t)d->m), kk((size_t)d->m);
-        std::vector<int32_t> k4(d->kw == 4 ? (size_t)d->m : 0);
-        hipError_t e = hipMemcpyAsync(hh.data(), d->set_h, (size_t)d->m * 8, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(d->kw == 8 ? (void*)kk.data() : (void*)k4.data(), d->set_k, (size_t)d->m * d->kw,
-                               hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) {
-            set_error(std::string("distinct_merge: ") + hipGetErrorString(e));
-            return RSV_E_DEVICE;
-        }
-        d->rep.reset(d->k);
-        for (int64_t i = 0; i < d->m; ++i) d->rep.sample(d->kw == 8 ? kk[(size_t)i] : (int64_t)k4[(size_t)i], hh[(size_t)i]);
-        d->max_h = d->rep.max_hash;
-        // the replica starts over from the union (the set arrays are its set); the logged segments
-        // stay readable for rsv_export_log until the next sample
-        d->pre_segs.insert(d->pre_segs.end(), d->segs.begin(), d->segs.end());
-        d->segs.clear();
-        d->exact = true;
-        d->merged = true;
-    }
+    merged_bookkeeping(d);
     return RSV_OK;
+}
+
+// ---- packed rows (rsv_export_packed / rsv_merge_packed) ----------------------------------------
+
+int distinct_export_row(DistinctState* d, int64_t* row, int64_t count, hipStream_t st) {
+    if (int rc = distinct_settle(d, st)) return rc;
+    if (int rc = distinct_finalize(d, st)) return rc;
+    const int64_t k = d->k;
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(k), 1), 2048);
+    const int64_t tied = d->m == k && d->over, mx = d->m ? d->set_top : INT64_MIN;
+    const int64_t ret = d->ordered && d->retain && d->arch_ok;
+    if (d->kw == 8)
+        hipLaunchKernelGGL(export_row_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, st, (const int64_t*)d->set_h,
+                           (const int64_t*)d->set_k, d->m, k, row, count, tied, mx, ret, (int64_t)d->ordered);
+    else
+        hipLaunchKernelGGL(export_row_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, st, (const int64_t*)d->set_h,
+                           (const int32_t*)d->set_k, d->m, k, row, count, tied, mx, ret, (int64_t)d->ordered);
+    RSV_HIP_TRY(hipGetLastError());
+    return RSV_OK;
+}
+
+// The radix-sort form of a rows merge (host waits): rows whose merge overflows a bucket (a
+// degenerate hash), more than 64 rows, or buckets beyond 1 GiB.  `over` as the device form sets it.
+template <typename KeyT>
+static int merge_rows_radix(DistinctState* d, const int64_t* rows, int32_t parts, int64_t stride, hipStream_t st) {
+    const int64_t k = d->k;
+    std::vector<int64_t> meta((size_t)parts * kRowMeta);
+    for (int32_t p = 0; p < parts; ++p)
+        RSV_HIP_TRY(hipMemcpyAsync(meta.data() + (size_t)p * kRowMeta, rows + (size_t)p * stride + 2 * k,
+                                   kRowMeta * 8, hipMemcpyDeviceToHost, st));
+    RSV_HIP_TRY(hipStreamSynchronize(st));
+    // the cut's tie rule (runs_top): the smallest maximum of a full run, tied there
+    int64_t T = d->m == k ? d->set_top : INT64_MAX;
+    bool tiedT = d->m == k && d->over;
+    for (int32_t p = 0; p < parts; ++p) {
+        const int64_t* mt = meta.data() + (size_t)p * kRowMeta;
+        if (std::min(std::max<int64_t>(mt[0], 0), k) != k) continue;
+        if (mt[3] < T) {
+            T = mt[3];
+            tiedT = mt[2] != 0;
+        } else if (mt[3] == T) {
+            tiedT = tiedT || mt[2] != 0;
+        }
+    }
+    bool tie = d->m == k && d->over;
+    for (int32_t p = 0; p < parts; ++p) {
+        const int64_t n = std::min(std::max<int64_t>(meta[(size_t)p * kRowMeta], 0), k);
+        if (n == 0) continue;
+        const int64_t* rk = rows + (size_t)p * stride;
+        const KeyT* keys = (const KeyT*)rk;
+        if constexpr (sizeof(KeyT) == 4) {  // row keys are int64-widened
+            RSV_HIP_TRY(ensure_caps(d, std::min<int64_t>(n, d->cand_limit), 0, st));
+            keys = (const KeyT*)d->cand_k;
+        }
+        for (int64_t off = 0; off < n;) {  // chunks that fit the merge buffer
+            const int64_t c = std::min<int64_t>(n - off, d->cand_limit);
+            if constexpr (sizeof(KeyT) == 4) {
+                hipLaunchKernelGGL(narrow_keys<KeyT>, dim3((unsigned)std::min<int64_t>(grid_1d(c), 1024)), dim3(kBlock),
+                                   0, st, rk + off, c, (KeyT*)d->cand_k);
+                RSV_HIP_TRY(hipGetLastError());
+            }
+            const int64_t old_max = d->max_h;
+            const bool was_full = d->m == k;
+            int64_t nd = 0;
+            RSV_HIP_TRY(merge_into_set<KeyT>(d, rk + k + off, sizeof(KeyT) == 4 ? keys : keys + off, c, &nd, st));
+            tie = d->m == k && (d->last_tie || (tie && was_full && d->max_h == old_max));
+            off += c;
+        }
+    }
+    d->over = d->m == k && (tie || (tiedT && d->set_top == T));
+    return RSV_OK;
+}
+
+// Settle a pending device merge: wait for its published words (normally long since there) and take
+// the new set's size, maximum and tie state; a bucket overflow redoes the merge on the radix path.
+template <typename KeyT>
+static int settle_impl(DistinctState* d, hipStream_t st) {
+    d->pend = false;
+    uint32_t* flag = (uint32_t*)(d->shc + 12);
+    const auto t0 = std::chrono::steady_clock::now();
+    bool seen = false;
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == d->pend_gen) {
+            seen = true;
+            break;
+        }
+        __builtin_ia32_pause();
+        if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+    }
+    if (!seen) {
+        RSV_HIP_TRY(hipStreamSynchronize(st));
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != d->pend_gen) RSV_HIP_TRY(hipErrorUnknown);
+    }
+    int64_t hv[8];
+    for (int i = 0; i < 8; ++i) hv[i] = __atomic_load_n(d->shc + i, __ATOMIC_RELAXED);
+    const int64_t k = d->k;
+    if (hv[1])  // a bucket overflowed (rows_sort): nothing was merged
+        return merge_rows_radix<KeyT>(d, d->pend_rows, d->pend_parts, d->pend_stride, st);
+    d->m = std::min<int64_t>(hv[2], k);
+    if (d->m) d->set_top = hv[3];
+    if (d->m == k) d->max_h = d->set_top;
+    d->over = d->m == k && (hv[5] != 0 || ((hv[6] & 2) && d->set_top == hv[7]));
+    return RSV_OK;
+}
+
+int distinct_settle(DistinctState* d, hipStream_t st) {
+    if (!d->pend) return RSV_OK;
+    return d->kw == 8 ? settle_impl<int64_t>(d, st) : settle_impl<int32_t>(d, st);
+}
+
+template <typename KeyT>
+static int merge_rows_impl(DistinctState* d, const int64_t* rows, int32_t parts, int64_t stride, hipStream_t st) {
+    const int64_t k = d->k;
+    const int64_t total = d->m + (int64_t)parts * k;
+    int32_t lb = 1;  // <= 64 entries per bucket on average: most sort in one 64-lane pass
+    while (((int64_t)1 << (lb + 6)) < total) ++lb;
+    const bool device = parts <= 64 && (((int64_t)kBucketCap * (8 + (int64_t)sizeof(KeyT)) + 20) << lb) <= ((int64_t)1 << 30);
+    if (!device) {
+        if (int rc = merge_rows_radix<KeyT>(d, rows, parts, stride, st)) return rc;
+        merged_bookkeeping(d);
+        return RSV_OK;
+    }
+    RSV_HIP_TRY(ensure_caps(d, 0, k, st));  // bucket_emit writes the set by rank: full-size arrays
+    RSV_HIP_TRY(sched_ensure<KeyT>(d, lb, st));
+    const uint32_t B = 1u << lb;
+    const int64_t need = (int64_t)(parts + 1) * (B + 1);
+    if (need > d->mstart_cap) {
+        RSV_HIP_TRY(grow((void**)&d->mstart, 0, (size_t)need * 4, false, st));
+        d->mstart_cap = need;
+    }
+    const Runs<KeyT> R{rows, stride, k, d->set_h, (const KeyT*)d->set_k, d->m};
+    const int64_t longest = std::max<int64_t>(d->m, k) + 1;
+    const dim3 bgrid((unsigned)std::min<int64_t>((longest + kBlock - 1) / kBlock, 1024), (unsigned)(parts + 1));
+    hipLaunchKernelGGL(rows_bounds<KeyT>, bgrid, dim3(kBlock), 0, st, R, parts, d->m ? d->set_top : INT64_MIN,
+                       (int32_t)(d->m == k && d->over), (uint32_t)lb, d->sctl, d->log_bmax_s, d->mstart);
+    KeyT* bk = (KeyT*)d->sbk;
+    hipLaunchKernelGGL(rows_sort<KeyT>, dim3((B + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, R, parts,
+                       (uint32_t)lb, (const uint32_t*)d->mstart, d->sctl, d->log_bmax_s, d->sbh, bk);
+    hipLaunchKernelGGL(bucket_emit<KeyT>, dim3((B + kEmitBuckets - 1) / kEmitBuckets), dim3(kBlock), 0, st, d->m,
+                       INT64_MAX, d->sctl, d->log_bmax_s, (const int64_t*)d->sbh, (const KeyT*)bk, k, d->set_h,
+                       (KeyT*)d->set_k, lb);
+    const uint32_t gen = ++d->sgen;
+    hipLaunchKernelGGL(merge_publish, dim3(1), dim3(64), 0, st, d->sctl, d->shc_dev, (uint32_t*)(d->shc_dev + 12), gen);
+    RSV_HIP_TRY(hipGetLastError());
+    d->pend = true;
+    d->pend_gen = gen;
+    d->pend_lb = (uint32_t)lb;
+    d->pend_rows = rows;
+    d->pend_parts = parts;
+    d->pend_stride = stride;
+    merged_bookkeeping(d);
+    return RSV_OK;
+}
+
+int distinct_merge_rows(DistinctState* d, const int64_t* rows, int32_t parts, int64_t stride, hipStream_t st) {
+    if (int rc = distinct_settle(d, st)) return rc;
+    if (parts <= 0) return RSV_OK;
+    if (int rc = distinct_finalize(d, st)) return rc;  // an ordered set must be exact before it merges
+    return d->kw == 8 ? merge_rows_impl<int64_t>(d, rows, parts, stride, st)
+                      : merge_rows_impl<int32_t>(d, rows, parts, stride, st);
+}
+
+void distinct_retain_log(DistinctState* d, bool on) {
+    if (on && !d->retain && d->seen > 0) d->arch_ok = false;  // earlier candidates are gone
+    d->retain = on;
+    if (!on) archive_drop(d);
 }
 
 template <typename KeyT>
@@ -2350,7 +2745,8 @@ static int log_export_impl(DistinctState* d, int64_t bound, int64_t* out_h, KeyT
             ++cnt;
         }
     };
-    for (size_t i = 0; i < d->arch_h.size(); ++i) emit(d->arch_h[i], d->arch_k[i]);
+    for (size_t i = 0; i < d->arch_h.size(); ++i)
+        emit(d->arch_h[i], sizeof(KeyT) == 8 ? d->arch_k[i] : (int64_t)d->arch_k4[i]);
     for (const std::vector<DistinctState::Seg>* v : {&d->pre_segs, &d->segs})
         for (const DistinctState::Seg& g : *v) {
             if (g.c == 0) continue;
@@ -2362,7 +2758,7 @@ static int log_export_impl(DistinctState* d, int64_t bound, int64_t* out_h, KeyT
             for (int64_t t = 0; t < g.c; ++t) emit(d->ph[t], (int64_t)pk[t]);
         }
     *out_n = cnt;
-    if (cnt > cap) {
+    if (cnt > cap && cap > 0) {  // (cap 0: a count-only query)
         set_error("rsv_export_log: cap is smaller than the number of candidates (*out_n)");
         return RSV_E_ILLEGAL_ARGUMENT;
     }
@@ -2371,10 +2767,12 @@ static int log_export_impl(DistinctState* d, int64_t bound, int64_t* out_h, KeyT
 
 int distinct_log_export(DistinctState* d, int64_t bound, int64_t* out_h, void* out_k, int64_t cap, int64_t* out_n,
                         hipStream_t st) {
-    if (!d->ordered || !d->arch_ok) {
-        set_error(!d->ordered ? "rsv_export_log needs an RSV_DISTINCT_ORDERED sampler"
-                              : "rsv_export_log: the candidate log was not retained (archive limit, or sampled "
-                                "after a merge)");
+    if (int rc = distinct_settle(d, st)) return rc;
+    if (!d->ordered || !d->retain || !d->arch_ok) {
+        set_error(!d->ordered  ? "rsv_export_log needs an RSV_DISTINCT_ORDERED sampler"
+                  : !d->retain ? "rsv_export_log: the candidate log was not retained (rsv_retain_log before sampling)"
+                               : "rsv_export_log: the candidate log was not retained (archive limit, or sampled "
+                                 "after a merge)");
         return RSV_E_UNSUPPORTED;
     }
     return d->kw == 8 ? log_export_impl<int64_t>(d, bound, out_h, (int64_t*)out_k, cap, out_n, st)
@@ -2390,7 +2788,9 @@ int distinct_log_merge(DistinctState* d, const int64_t* h, const void* keys, int
         set_error("rsv_merge_log needs an RSV_DISTINCT_ORDERED sampler");
         return RSV_E_UNSUPPORTED;
     }
+    if (int rc = distinct_settle(d, st)) return rc;
     d->rep.reset(d->k);
+    d->rep_stale = false;
     if (d->kw == 8) {
         const int64_t* kk = (const int64_t*)keys;
         d->rep.sample_run(n, [&](int64_t t) { return kk[t]; }, [&](int64_t t) { return h[t]; });

@@ -4,7 +4,6 @@
 //   K1  k1_last_writer   single stream: per-slot last writer (max index) of an index range
 //   --  resolve          fill phase + gather of the winning keys into the reservoir
 //   K1' replay_events    the reference's Algorithm-L eviction events -> per-slot last writer
-//   K2  k2_segmented_v1  round-1 segmented kernel (K2 is rsv_segmented.hip)
 //   --  merge_slots      multi-GPU combine of exported partial reservoirs (last writer wins)
 //
 // None of these kernels streams the key array: a draw depends only on (seed, stream, index), so
@@ -205,77 +204,6 @@ __global__ __launch_bounds__(kBlock) void export_draws_kernel(DrawKey dk, uint64
     const uint64_t i = i0 + (uint64_t)t;
     const u32x4 w = level0(dk, i >> 4);
     out[t] = exact_j(dk, i, level0_byte(w, (uint32_t)(i & 15)));
-}
-
-// K2: one wave per stream; the wave's k-entry last-writer table and candidate queue live in LDS.
-// A wave touches only its own LDS region, and LDS operations of one wave execute in order, so the
-// waves of a workgroup never synchronise with each other (no __syncthreads); each wave walks its
-// own sequence of streams and prefetches the next stream's offsets.
-template <typename KeyT>
-__global__ __launch_bounds__(kBlock) void k2_segmented_v1(const KeyT* __restrict__ keys,
-                                                       const int64_t* __restrict__ offsets, int64_t S,
-                                                       uint32_t k, uint32_t k0, uint32_t k1,
-                                                       uint64_t stream_base, KeyT* __restrict__ out,
-                                                       int64_t* __restrict__ counts) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_tab[];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t wpb = blockDim.x >> 6;
-    // per wave: k-entry last-writer table, then the candidate queue
-    unsigned long long* tab = lds_tab + (size_t)wave * (k + kQueue);
-    uint64_t* q = (uint64_t*)(tab + k);
-    const uint64_t dense_lim = 256ull * k;
-    const int64_t wave_stride = (int64_t)gridDim.x * wpb;
-    int64_t s = (int64_t)blockIdx.x * wpb + wave;
-    int64_t off = 0, end = 0;
-    if (s < S) {
-        off = offsets[s];
-        end = offsets[s + 1];
-    }
-    for (; s < S; s += wave_stride) {
-        const int64_t len = end - off;
-        const int64_t s_next = s + wave_stride;
-        int64_t off_next = 0, end_next = 0;
-        if (s_next < S) {  // prefetch: the loads are in flight during this stream's work
-            off_next = offsets[s_next];
-            end_next = offsets[s_next + 1];
-        }
-        for (uint32_t j = lane; j < k; j += 64) tab[j] = 0;
-        __builtin_amdgcn_wave_barrier();
-        const uint64_t stream = stream_base + (uint64_t)s;
-        const DrawKey dk{k0, k1, (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)stream),
-                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(stream >> 32))};
-        const uint64_t n_groups = ((uint64_t)len + 15) >> 4;
-        auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&tab[j], (unsigned long long)i); };
-        uint32_t qn = 0;
-        // two level-0 blocks per lane per iteration: two independent Philox chains in flight
-        for (uint64_t gb = k >> 4; gb < n_groups; gb += 128) {
-            const uint64_t ga = gb + lane, gc = gb + 64 + lane;
-            const u32x4 wa = level0(dk, ga);
-            const u32x4 wc = level0(dk, gc);
-            uint32_t ma = 0, mc = 0;
-            if (ga < n_groups) {
-                ma = candidate_mask16(wa, ga << 4, dense_lim);
-                if (ma) ma &= clip_mask16(ga << 4, k, (uint64_t)len);
-            }
-            if (gc < n_groups) {
-                mc = candidate_mask16(wc, gc << 4, dense_lim);
-                if (mc) mc &= clip_mask16(gc << 4, k, (uint64_t)len);
-            }
-            enqueue_block(dk, wa, ga << 4, ma, q, qn, lane, k, hit);
-            enqueue_block(dk, wc, gc << 4, mc, q, qn, lane, k, hit);
-        }
-        drain_queue(dk, q, qn, lane, k, hit);
-        __builtin_amdgcn_wave_barrier();
-        KeyT* o = out + s * (int64_t)k;
-        for (uint32_t j = lane; j < k; j += 64) {
-            const unsigned long long wi = tab[j];
-            o[j] = wi ? keys[off + (int64_t)wi] : ((int64_t)j < len ? keys[off + j] : (KeyT)0);
-        }
-        if (lane == 0) counts[s] = len < (int64_t)k ? len : (int64_t)k;
-        __builtin_amdgcn_wave_barrier();
-        off = off_next;
-        end = end_next;
-    }
 }
 
 template <typename KeyT>
@@ -638,6 +566,61 @@ hipError_t launch_resolve_publish(const void* keys, int key_width, int64_t base,
     return hipGetLastError();
 }
 
+// ---- index-only batches (rsv_sample_indexed / rsv_fill_slots) -------------------------------
+// The resolve of a batch sampled by index alone: per slot j the batch's last writer (win[j]), else
+// the fill of j < k from this batch, becomes slot_idx[j], and offs[j] = its offset in the batch
+// (-1: the slot did not change).  The keys arrive later from the caller (fill_slots_kernel).
+__global__ __launch_bounds__(kBlock) void resolve_indices_kernel(int64_t base, int64_t n, uint32_t k,
+                                                                 unsigned long long* __restrict__ win,
+                                                                 int64_t* __restrict__ slot_idx, int fresh,
+                                                                 uint8_t* __restrict__ slot_key, int key_width,
+                                                                 int64_t* __restrict__ offs) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += stride) {
+        const unsigned long long wi = win[j];
+        int64_t off = -1;
+        if (wi) {  // last eviction into slot j (Sampler.scala:243-246)
+            slot_idx[j] = (int64_t)wi;
+            win[j] = 0;
+            off = (int64_t)wi - base;
+        } else if ((int64_t)j >= base && (int64_t)j < base + n) {  // fill phase (Sampler.scala:253-255)
+            slot_idx[j] = (int64_t)j;
+            off = (int64_t)j - base;
+        } else if (fresh) {
+            slot_idx[j] = -1;
+            for (int q = 0; q < key_width; ++q) slot_key[j * key_width + q] = 0;
+        }
+        offs[j] = off;
+    }
+}
+
+// keys[j] (host-supplied, one per slot, slot order) into every slot the index-only batch changed
+__global__ __launch_bounds__(kBlock) void fill_slots_kernel(const int64_t* __restrict__ offs, const uint8_t* __restrict__ keys,
+                                                            uint32_t k, int key_width, uint8_t* __restrict__ slot_key) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += stride) {
+        if (offs[j] < 0) continue;
+        if (key_width == 8) ((int64_t*)slot_key)[j] = ((const int64_t*)keys)[j];
+        else if (key_width == 4) ((int32_t*)slot_key)[j] = ((const int32_t*)keys)[j];
+        else
+            for (int q = 0; q < key_width; ++q) slot_key[j * key_width + q] = keys[j * key_width + q];
+    }
+}
+
+hipError_t launch_resolve_indices(int64_t base, int64_t n, uint32_t k, unsigned long long* batch_win, int64_t* slot_idx,
+                                  bool fresh, void* slot_key, int key_width, int64_t* offs, hipStream_t st) {
+    hipLaunchKernelGGL(resolve_indices_kernel, dim3(grid_for(k, 256 * 64)), dim3(kBlock), 0, st, base, n, k, batch_win,
+                       slot_idx, (int)fresh, (uint8_t*)slot_key, key_width, offs);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_slots(const int64_t* offs, const void* keys, uint32_t k, int key_width, void* slot_key,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(fill_slots_kernel, dim3(grid_for(k, 256 * 64)), dim3(kBlock), 0, st, offs, (const uint8_t*)keys,
+                       k, key_width, (uint8_t*)slot_key);
+    return hipGetLastError();
+}
+
 hipError_t launch_replay_events(const int64_t* ev_pos, const int32_t* ev_slot, int64_t n_events,
                                 uint32_t k, unsigned long long* batch_win, hipStream_t st) {
     if (n_events <= 0) return hipSuccess;
@@ -652,31 +635,6 @@ hipError_t launch_export_draws(const DrawParams& dp, uint64_t i0, int64_t n, uin
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(export_draws_kernel, dim3(grid), dim3(kBlock), 0, st, make_key(dp), i0, n, j);
-    return hipGetLastError();
-}
-
-int segmented_waves_per_block(uint32_t k) {
-    const uint32_t w = 8192u / (k ? k : 1);
-    return (int)(w < 1 ? 1 : (w > 4 ? 4 : w));
-}
-
-// the round-1 K2 (rsv_segmented.hip launch_segmented: RSV_K2=1, or a table too big for its LDS)
-hipError_t launch_segmented_v1(const void* keys, int key_width, const int64_t* offsets, int64_t S,
-                               uint32_t k, const DrawParams& dp, void* out, int64_t* counts,
-                               hipStream_t st) {
-    if (S <= 0) return hipSuccess;
-    const int wpb = segmented_waves_per_block(k);
-    const size_t lds = (size_t)wpb * (k + kQueue) * sizeof(unsigned long long);
-    uint64_t blocks = ((uint64_t)S + wpb - 1) / wpb;
-    const uint64_t cap = 256ull * 16;
-    const unsigned grid = (unsigned)(blocks < cap ? blocks : cap);
-    const uint32_t k0 = (uint32_t)dp.seed, k1 = (uint32_t)(dp.seed >> 32);
-    if (key_width == 8)
-        hipLaunchKernelGGL(k2_segmented_v1<int64_t>, dim3(grid), dim3(64 * wpb), lds, st,
-                           (const int64_t*)keys, offsets, S, k, k0, k1, dp.stream, (int64_t*)out, counts);
-    else
-        hipLaunchKernelGGL(k2_segmented_v1<int32_t>, dim3(grid), dim3(64 * wpb), lds, st,
-                           (const int32_t*)keys, offsets, S, k, k0, k1, dp.stream, (int32_t*)out, counts);
     return hipGetLastError();
 }
 

@@ -109,6 +109,12 @@ hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t
 hipError_t launch_resolve_publish(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,
                                   unsigned long long* batch_win, void* slot_key, int64_t* slot_idx, bool fresh,
                                   int64_t m, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st);
+// index-only batches: resolve into slot_idx with offs[k] = the batch offset of each changed slot
+// (-1: unchanged); then the caller's keys into the changed slots
+hipError_t launch_resolve_indices(int64_t base, int64_t n, uint32_t k, unsigned long long* batch_win, int64_t* slot_idx,
+                                  bool fresh, void* slot_key, int key_width, int64_t* offs, hipStream_t st);
+hipError_t launch_fill_slots(const int64_t* offs, const void* keys, uint32_t k, int key_width, void* slot_key,
+                             hipStream_t st);
 // K1': events (1-based pos, slot) -> batch_win
 hipError_t launch_replay_events(const int64_t* ev_pos, const int32_t* ev_slot, int64_t n_events,
                                 uint32_t k, unsigned long long* batch_win, hipStream_t st);
@@ -172,5 +178,14 @@ int distinct_log_export(DistinctState* d, int64_t bound, int64_t* out_h, void* o
                         hipStream_t st);
 int distinct_log_merge(DistinctState* d, const int64_t* h, const void* keys, int64_t n, int64_t seen,
                        hipStream_t st);
+// packed rows [keys as int64 (k) | hashes (k) | n, count, tied, max_hash, log_retained, ordered]:
+// export of the set (count = the handle's element count), and the device merge of `parts` rows into
+// the set -- enqueued without a host wait; `rows` must stay valid until the next call on the state,
+// which settles the merge (distinct_settle; every other distinct_* call settles first)
+int distinct_export_row(DistinctState* d, int64_t* row, int64_t count, hipStream_t st);
+int distinct_merge_rows(DistinctState* d, const int64_t* rows, int32_t parts, int64_t stride, hipStream_t st);
+int distinct_settle(DistinctState* d, hipStream_t st);
+// ordered samplers: keep every replayed candidate on the host for rsv_export_log (opt-in)
+void distinct_retain_log(DistinctState* d, bool on);
 
 }  // namespace rsv

@@ -25,10 +25,15 @@ __host__ __device__ constexpr uint32_t qcap_of(int V) { return (V & 128) ? 2048u
 // stash ring of variant V (V & 256: 2 iterations, occupancy probe)
 __host__ __device__ constexpr uint32_t ring_of(int V) { return (V & 256) ? 2u : kRing; }
 
-// bytes of dynamic LDS per workgroup: T table + per wave (stash | FIFO | k-slot table)
-__host__ __device__ inline size_t lds_bytes(uint32_t k, int V = 0) {
-    return kLutBytes + (size_t)kWaves * (ring_of(V) * 64 * 16 + qcap_of(V) * 2 + (size_t)k * 8);
+// bytes of dynamic LDS per workgroup: T table + per wave (stash | FIFO | k-slot table; GT: the
+// table lives in global memory)
+__host__ __device__ inline size_t lds_bytes(uint32_t k, int V = 0, bool GT = false) {
+    return kLutBytes + (size_t)kWaves * (ring_of(V) * 64 * 16 + qcap_of(V) * 2 + (GT ? 0 : (size_t)k * 8));
 }
+
+// the LDS table form serves k while lds_bytes fits one workgroup's 160 KB (k <= 4416); above that
+// each wave's k-slot table is a slice of a global scratch buffer (k2_segmented<..., GT = true>)
+constexpr size_t kLdsMax = 160 * 1024;
 
 // T = ceil(256 k / (i0 + 1)), the block threshold of the dense region (T > 255: every byte is a
 // candidate -> 256); 0 marks the sparse region (i0 + 1 >= 256 k: only b == 0 can hit)
@@ -124,15 +129,20 @@ struct Wave {
 // One stream on one wave.  SMALL: n < 2^27 -- 32-bit indices, u32 winner table, and Philox counters
 // whose high words are wave-uniform (level 0: g < 2^32; level 1: i/2 < 2^32).
 // DEFER (k <= 64): the lane's winner index is returned (-1: none) and the caller gathers its key
-// after storing the previous stream's, so the random gather's latency overlaps the next stream's draws
-template <typename KeyT, int V, bool SMALL, bool DEFER>
+// after storing the previous stream's, so the random gather's latency overlaps the next stream's draws.
+// GT: the winner table is the wave's slice of global scratch (large k).  It is all zero when the
+// stream starts (zeroed once before the launch, and the gather below takes every entry with an
+// atomic exchange against 0), and the gather waits for the wave's own atomics (vmcnt counts
+// returnless global atomics on gfx950 until they are performed) before it reads them.
+template <typename KeyT, int V, bool SMALL, bool DEFER, bool GT = false>
 __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restrict__ keys, int64_t off, int64_t len,
                                              uint64_t stream, KeyT* __restrict__ o) {
     using IdxT = typename std::conditional<SMALL, uint32_t, uint64_t>::type;
     constexpr uint32_t QC = qcap_of(V), RG = ring_of(V), WIN = RG * 1024;  // WIN: indices in the ring
     const uint32_t lane = W.lane, k = W.k;
     IdxT* tab = (IdxT*)W.tab;
-    for (uint32_t j = lane; j < k; j += 64) tab[j] = 0;
+    if constexpr (!GT)
+        for (uint32_t j = lane; j < k; j += 64) tab[j] = 0;
     const uint32_t s0 = (uint32_t)stream, s1 = (uint32_t)(stream >> 32);
     const DrawKey dk{W.k0, W.k1, s0, s1};
     const IdxT n_groups = (IdxT)(((uint64_t)len + 15) >> 4);
@@ -180,7 +190,10 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
     // to rounds it runs anyway): C3 1.75-1.76 -> 1.67-1.69 ms (tools/micro_k2 r, warm clock).
     constexpr uint32_t HM = (V & 32) ? 2u : (V & 64) ? 1u : (V & 16384) ? 6u : (V & 32768) ? 8u : 4u;
     uint64_t hx = (uint64_t)HM * k;
-    if constexpr ((V & 512) == 0) hx = k + ((hx - k) & ~(uint64_t)127);  // (V & 512: the r02 head)
+    // (only where the head holds at least one whole round: below k = 43 the cut would remove it and
+    // send the 25-100 % dense region through the FIFO; V & 512: the r02 head everywhere)
+    if constexpr ((V & 512) == 0)
+        if (hx - k >= 128) hx = k + ((hx - k) & ~(uint64_t)127);
     const IdxT hend = (IdxT)std::min<uint64_t>((uint64_t)len, hx);
     const IdxT flo = std::max<IdxT>((IdxT)k, hend);
     for (; gb < n_groups; gb += 64, ring = (ring + 1) & (RG - 1)) {
@@ -274,8 +287,11 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
         __builtin_amdgcn_wave_barrier();
         return at;
     }
+    if constexpr (GT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (uint32_t j = lane; j < k; j += 64) {
-        const IdxT wi = tab[j];
+        IdxT wi;
+        if constexpr (GT) wi = __hip_atomic_exchange(&tab[j], (IdxT)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else wi = tab[j];
         if constexpr ((V & 1) != 0)  // variant: no winner-key gather (cost probe)
             o[j] = (KeyT)wi;
         else
@@ -285,13 +301,15 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
     return -1;
 }
 
-// V: development variants for tools/micro_k2.hip (0 = the product kernel)
-template <typename KeyT, int V = 0>
+// V: development variants for tools/micro_k2.hip (0 = the product kernel).  GT: winner tables in
+// global scratch `gtab` (k * 8 bytes per wave of the grid, all zero at launch; see k2_stream)
+template <typename KeyT, int V = 0, bool GT = false>
 __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restrict__ keys,
                                                             const int64_t* __restrict__ offsets, int64_t S,
                                                             uint32_t k, uint32_t k0, uint32_t k1, uint64_t stream_base,
                                                             KeyT* __restrict__ out, int64_t* __restrict__ counts,
-                                                            uint32_t fifo_cap = qcap_of(V)) {
+                                                            uint32_t fifo_cap = qcap_of(V),
+                                                            unsigned long long* __restrict__ gtab = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     uint16_t* lut = (uint16_t*)lds;
     const uint64_t dense_lim = 256ull * k;
@@ -311,8 +329,11 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     // per wave: stash [kRing][64] x 16 B | FIFO kQCap x u16 | last-writer table k x (u32 | u64)
     constexpr size_t qbytes = qcap_of(V) * 2, sbytes = ring_of(V) * 64 * 16;
-    unsigned char* base = lds + kLutBytes + (size_t)wave * (sbytes + qbytes + (size_t)k * 8);
-    const Wave W{(u32x4*)base, (uint16_t*)(base + sbytes), base + sbytes + qbytes, lut, lane, k,
+    const size_t tbytes = GT ? 0 : (size_t)k * 8;
+    unsigned char* base = lds + kLutBytes + (size_t)wave * (sbytes + qbytes + tbytes);
+    void* tab = base + sbytes + qbytes;
+    if constexpr (GT) tab = gtab + ((size_t)blockIdx.x * kWaves + wave) * k;
+    const Wave W{(u32x4*)base, (uint16_t*)(base + sbytes), tab, lut, lane, k,
                  k0, k1, dense_lim, std::min<uint32_t>(std::max<uint32_t>(fifo_cap, 128u), qcap_of(V))};
     const int64_t wave_stride = (int64_t)gridDim.x * kWaves;
     int64_t s = (int64_t)blockIdx.x * kWaves + wave;
@@ -321,7 +342,7 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
         off = offsets[s];
         end = offsets[s + 1];
     }
-    const bool defer = k <= 64 && (V & 16) == 0 && (V & 1) == 0;
+    const bool defer = !GT && k <= 64 && (V & 16) == 0 && (V & 1) == 0;
     KeyT* pend_o = nullptr;
     KeyT pend_v = 0;
     bool pend_ok = false;
@@ -339,9 +360,9 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
         const int64_t off_next = offsets[s_pf], end_next = offsets[s_pf + 1];
         const uint64_t stream = stream_base + (uint64_t)s;
         KeyT* o = out + s * (int64_t)k;
-        if (defer) {  // k <= 64: this stream's key is stored after the next stream's draws
-            const int64_t at = len < kSmallLen ? k2_stream<KeyT, V, true, true>(W, keys, off, len, stream, o)
-                                               : k2_stream<KeyT, V, false, true>(W, keys, off, len, stream, o);
+        if (!GT && defer) {  // k <= 64: this stream's key is stored after the next stream's draws
+            const int64_t at = len < kSmallLen ? k2_stream<KeyT, V, true, !GT>(W, keys, off, len, stream, o)
+                                               : k2_stream<KeyT, V, false, !GT>(W, keys, off, len, stream, o);
             // the previous stream's key (loaded a whole stream ago) leaves its register before this
             // stream's load lands in it: no copy of a load in flight, so no s_waitcnt at the stream end
             if (pend_o && lane < k) pend_o[lane] = pend_ok ? pend_v : (KeyT)0;
@@ -349,9 +370,9 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
             pend_ok = at >= 0;  // else an empty slot: the load below reads a valid dummy word
             pend_v = *(pend_ok ? keys + off + at : (const KeyT*)offsets);
         } else if (len < kSmallLen) {
-            k2_stream<KeyT, V, true, false>(W, keys, off, len, stream, o);
+            k2_stream<KeyT, V, true, false, GT>(W, keys, off, len, stream, o);
         } else {
-            k2_stream<KeyT, V, false, false>(W, keys, off, len, stream, o);
+            k2_stream<KeyT, V, false, false, GT>(W, keys, off, len, stream, o);
         }
         if (lane == 0) counts[s] = len < (int64_t)k ? len : (int64_t)k;
         off = off_next;

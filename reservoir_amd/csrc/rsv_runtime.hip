@@ -23,7 +23,6 @@ namespace rsv {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
-int segmented_waves_per_block(uint32_t k);
 
 // ---------------------------------------------------------------------------------------------
 // java.util.Random + Algorithm L event generator for RSV_ENGINE_JAVA_L (product implementation;
@@ -125,6 +124,10 @@ struct rsv_sampler {
     int64_t* ev_pos_d = nullptr;
     int32_t* ev_slot_d = nullptr;
     int64_t ev_cap = 0;
+    // index-only batches (rsv_sample_indexed): per slot the batch offset of its new element, and
+    // whether the caller still owes those elements' keys (rsv_fill_slots)
+    int64_t* idx_offs_d = nullptr;
+    bool keys_owed = false;
     // DISTINCT
     DistinctState* distinct = nullptr;
     int hash_kind = kHashIdentity;
@@ -234,6 +237,7 @@ rsv_status fail(rsv_status st, const std::string& msg) {
 rsv_status check_open(const rsv_sampler* s) {  // SingleUse.checkOpen, Sampler.scala:185-186
     if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
     if (!s->open) return fail(RSV_E_ILLEGAL_STATE, "use of sampler after calling `result()`");
+    if (s->keys_owed) return fail(RSV_E_ILLEGAL_STATE, "rsv_fill_slots is pending after rsv_sample_indexed");
     return RSV_OK;
 }
 
@@ -478,7 +482,7 @@ rsv_status flush_stage(rsv_sampler* s) {
 void free_all(rsv_sampler* s) {
     // callers have synchronized the stream: nothing queued touches these any more
     if (s->slots && s->win_zero && give_clean_slots(s->slots, s->k, s->kw, s->device)) s->slots = nullptr;
-    void* ds[] = {s->slots, s->ev_pos_d, s->ev_slot_d, s->chunk_d, s->chunk_hash_d};
+    void* ds[] = {s->slots, s->ev_pos_d, s->ev_slot_d, s->chunk_d, s->chunk_hash_d, s->idx_offs_d};
     for (void* p : ds) pool_device_free(p);
     for (int b = 0; b < 2; ++b) {
         pool_host_free(s->stage_h[b]);
@@ -705,6 +709,82 @@ rsv_status rsv_sample_batch(rsv_sampler* s, const void* keys, int64_t n, int32_t
     if (mem == RSV_MEM_DEVICE) return process_device_batch(s, keys, pre ? hashes : nullptr, n);
     if (mem == RSV_MEM_HOST) return process_host_batch(s, keys, pre ? hashes : nullptr, n);
     return fail(RSV_E_ILLEGAL_ARGUMENT, "mem must be RSV_MEM_HOST or RSV_MEM_DEVICE");
+}
+
+rsv_status rsv_sample_indexed(rsv_sampler* s, int64_t n, int64_t* slot_offsets_host) {
+    if (rsv_status st = check_open(s)) return st;
+    if (s->cfg.kind != RSV_KIND_ELEMENTS)
+        return fail(RSV_E_UNSUPPORTED, "rsv_sample_indexed needs an ELEMENTS sampler (distinct maps every element, S:50)");
+    if (n < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative batch size");
+    if (!slot_offsets_host) return fail(RSV_E_NULL_POINTER, "slot_offsets_host is NULL");
+    if (n == 0) {
+        for (uint32_t j = 0; j < s->k; ++j) slot_offsets_host[j] = -1;
+        return RSV_OK;
+    }
+    DeviceGuard g(s->device);
+    if (rsv_status st = flush_stage(s)) return st;  // keep global index order
+    if (!s->idx_offs_d) RSV_HIP_TRY(pool_device_alloc((void**)&s->idx_offs_d, (size_t)s->k * 8));
+    touch(s);
+    const int64_t base = s->count;
+    if (!s->win_zero) {  // never-used block: full init
+        RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream, s->k1_ticket));
+        s->slots_init = s->win_zero = true;
+    }
+    const bool fresh = !s->slots_init;
+    s->win_zero = false;
+    if (s->cfg.engine == RSV_ENGINE_JAVA_L) {  // the reference's own events (S:261-273 skips by them)
+        s->ev_pos_h.clear();
+        s->ev_slot_h.clear();
+        s->algo_l.events(base, n, s->ev_pos_h, s->ev_slot_h);
+        const int64_t ne = (int64_t)s->ev_pos_h.size();
+        if (ne) {
+            if (rsv_status st = ensure_events(s, ne)) return st;
+            RSV_HIP_TRY(hipMemcpyAsync(s->ev_pos_d, s->ev_pos_h.data(), ne * 8, hipMemcpyHostToDevice, s->stream));
+            RSV_HIP_TRY(hipMemcpyAsync(s->ev_slot_d, s->ev_slot_h.data(), ne * 4, hipMemcpyHostToDevice, s->stream));
+            RSV_HIP_TRY(launch_replay_events(s->ev_pos_d, s->ev_slot_d, ne, s->k, s->batch_win, s->stream));
+        }
+    } else {
+        const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
+        const uint64_t lo = std::max<uint64_t>((uint64_t)base, s->k), hi = (uint64_t)(base + n);
+        const bool pm = prof_begin(s, s->stream);
+        RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
+        prof_end(s, s->stream, pm);
+    }
+    RSV_HIP_TRY(launch_resolve_indices(base, n, s->k, s->batch_win, s->slot_idx, fresh, s->slot_key, s->kw,
+                                       s->idx_offs_d, s->stream));
+    RSV_HIP_TRY(hipMemcpyAsync(slot_offsets_host, s->idx_offs_d, (size_t)s->k * 8, hipMemcpyDeviceToHost, s->stream));
+    RSV_HIP_TRY(sync_stream(s));
+    s->slots_init = s->win_zero = true;
+    s->pub_valid = false;
+    s->count = base + n;
+    s->keys_owed = true;
+    return RSV_OK;
+}
+
+rsv_status rsv_fill_slots(rsv_sampler* s, const void* keys_host) {
+    if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
+    if (!s->keys_owed) return fail(RSV_E_ILLEGAL_STATE, "rsv_fill_slots without a pending rsv_sample_indexed");
+    if (!keys_host) return fail(RSV_E_NULL_POINTER, "keys_host is NULL");
+    DeviceGuard g(s->device);
+    const size_t bytes = (size_t)s->k * s->kw;
+    void* dev = nullptr;
+    touch(s);
+    if ((int64_t)s->k <= kChunkKeys) {  // the handle's host-batch chunk
+        if (rsv_status st = ensure_chunk(s)) return st;
+        dev = s->chunk_d;
+    } else {
+        RSV_HIP_TRY(hipMallocAsync(&dev, bytes, s->stream));
+    }
+    hipError_t e = hipMemcpyAsync(dev, keys_host, bytes, hipMemcpyHostToDevice, s->stream);
+    if (e == hipSuccess) e = launch_fill_slots(s->idx_offs_d, dev, s->k, s->kw, s->slot_key, s->stream);
+    if (dev != s->chunk_d) {
+        const hipError_t e2 = hipFreeAsync(dev, s->stream);
+        if (e == hipSuccess) e = e2;
+    }
+    RSV_HIP_TRY(e);
+    RSV_HIP_TRY(sync_stream(s));  // the caller's buffer is theirs again
+    s->keys_owed = false;
+    return RSV_OK;
 }
 
 // Wait until publish_kernel has stored `gen` (acquire).  Spins for up to ~2 ms -- the K1 pass of a
@@ -960,6 +1040,7 @@ rsv_status rsv_get_distinct_info(rsv_sampler* s, rsv_distinct_info* out) {
     DeviceGuard g(s->device);
     touch(s);
     if (rsv_status st = flush_stage(s)) return st;
+    if (int rc = distinct_settle(s->distinct, s->stream)) return (rsv_status)rc;
     distinct_info(s->distinct, &out->ordered, &out->tied, &out->log_retained, &out->size, &out->max_hash,
                   &out->log_entries, &out->sched_passes, &out->sched_fallbacks);
     return RSV_OK;
@@ -971,6 +1052,7 @@ rsv_status rsv_export_log(rsv_sampler* s, int64_t bound, int64_t* hashes_host, v
     if (!out_n) return fail(RSV_E_NULL_POINTER, "out_n is NULL");
     if (cap < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative cap");
     if (cap > 0 && (!hashes_host || !keys_host)) return fail(RSV_E_NULL_POINTER, "hashes_host/keys_host is NULL");
+    if (cap == 0) hashes_host = nullptr, keys_host = nullptr;  // count-only query
     DeviceGuard g(s->device);
     touch(s);
     if (rsv_status st = flush_stage(s)) return st;
@@ -993,18 +1075,23 @@ rsv_status rsv_merge_log(rsv_sampler* s, const int64_t* hashes_host, const void*
     return RSV_OK;
 }
 
-static rsv_status check_packed(rsv_sampler* s) {
-    if (rsv_status st = check_open(s)) return st;
-    if (s->cfg.kind != RSV_KIND_ELEMENTS) return fail(RSV_E_UNSUPPORTED, "packed rows hold ELEMENTS samplers only");
+rsv_status rsv_retain_log(rsv_sampler* s, int32_t on) {
+    if (rsv_status st = check_distinct(s, "rsv_retain_log")) return st;
+    distinct_retain_log(s->distinct, on != 0);
     return RSV_OK;
 }
 
 rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev) {
-    if (rsv_status st = check_packed(s)) return st;
+    if (rsv_status st = check_open(s)) return st;
     if (!row_dev) return fail(RSV_E_NULL_POINTER, "row_dev is NULL");
     DeviceGuard g(s->device);
     touch(s);
     if (rsv_status st = flush_stage(s)) return st;
+    if (s->cfg.kind == RSV_KIND_DISTINCT) {
+        if (int rc = distinct_export_row(s->distinct, row_dev, s->count, s->stream)) return (rsv_status)rc;
+        if (s->own_stream) RSV_HIP_TRY(sync_stream(s));
+        return RSV_OK;
+    }
     if (rsv_status st = ensure_slots(s)) return st;
     RSV_HIP_TRY(launch_export_packed(s->slot_idx, s->slot_key, s->kw, s->k, row_dev, s->stream));
     if (s->own_stream) RSV_HIP_TRY(sync_stream(s));
@@ -1013,8 +1100,23 @@ rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev) {
 
 rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t parts, int64_t row_stride,
                             int64_t total_count) {
-    if (rsv_status st = check_packed(s)) return st;
+    if (rsv_status st = check_open(s)) return st;
     if (parts < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative parts");
+    if (s->cfg.kind == RSV_KIND_DISTINCT) {
+        if (row_stride < 2 * (int64_t)s->k + 6) return fail(RSV_E_ILLEGAL_ARGUMENT, "row_stride shorter than a packed row");
+        if (parts > 0 && !rows_dev) return fail(RSV_E_NULL_POINTER, "rows_dev is NULL");
+        DeviceGuard g(s->device);
+        touch(s);
+        if (rsv_status st = flush_stage(s)) return st;
+        if (int rc = distinct_merge_rows(s->distinct, rows_dev, parts, row_stride, s->stream)) return (rsv_status)rc;
+        if (total_count > s->count) s->count = total_count;
+        s->pub_valid = false;
+        if (s->own_stream) {  // the call returns with its work done: settle now, while the rows are the caller's
+            RSV_HIP_TRY(sync_stream(s));
+            if (int rc = distinct_settle(s->distinct, s->stream)) return (rsv_status)rc;
+        }
+        return RSV_OK;
+    }
     const int64_t row_min = (int64_t)s->k * (1 + (s->kw > 8 ? s->kw / 8 : 1));  // [idx(k) | keys]
     if (row_stride < row_min) return fail(RSV_E_ILLEGAL_ARGUMENT, "row_stride shorter than a packed row");
     if (parts > 0 && !rows_dev) return fail(RSV_E_NULL_POINTER, "rows_dev is NULL");
@@ -1056,9 +1158,6 @@ rsv_status rsv_sample_segmented(const void* keys_dev, const int64_t* offsets_dev
     if (num_streams < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative stream count");
     if (num_streams == 0) return RSV_OK;
     if (!offsets_dev || !out_dev || !counts_dev) return fail(RSV_E_NULL_POINTER, "NULL buffer");
-    const size_t lds = (size_t)segmented_waves_per_block((uint32_t)k) * ((size_t)k + 128) * 8;
-    if (lds > 160 * 1024)
-        return fail(RSV_E_UNSUPPORTED, "segmented sampling keeps each stream's k slots in LDS: k <= 20352");
     const DrawParams dp{seed, stream_base};
     RSV_HIP_TRY(launch_segmented(keys_dev, key_width, offsets_dev, num_streams, (uint32_t)k, dp, out_dev, counts_dev,
                                  (hipStream_t)hip_stream));

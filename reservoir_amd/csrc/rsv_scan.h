@@ -114,184 +114,9 @@ __device__ __forceinline__ void resolve_block(const DrawKey& dk, bool valid, uin
     enqueue_block(dk, w, i0, mask, cq, cqn, lane, k, hit);
 }
 
-// Push the U blocks of one iteration (has[u]: block g_begin + off[u] holds a candidate) with one
-// wave-uniform branch; whenever 64 blocks wait, all lanes resolve one each.  The queue holds
-// < 64 waiting + 64 U pushed entries.
-template <int U, class Hit>
-__device__ __forceinline__ void push_blocks(const bool (&has)[U], const uint32_t (&off)[U], uint32_t* q,
-                                            uint32_t& qn, uint64_t* cq, uint32_t& cqn, uint32_t lane,
-                                            const DrawKey& dk, uint64_t g_begin, uint64_t lo, uint64_t hi,
-                                            uint64_t dense_lim, uint32_t k, Hit& hit) {
-    unsigned long long bal[U], any = 0;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        bal[u] = __ballot(has[u]);
-        any |= bal[u];
-    }
-    if (any == 0) return;
-    const unsigned long long lt = lanemask_lt64();
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        if (has[u]) q[qn + __popcll(bal[u] & lt)] = off[u];
-        qn += (uint32_t)__popcll(bal[u]);
-    }
-    while (qn >= 64) {
-        qn -= 64;
-        __builtin_amdgcn_wave_barrier();
-        resolve_block(dk, true, g_begin + q[qn + lane], lo, hi, dense_lim, k, cq, cqn, lane, hit);
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-template <class Hit>
-__device__ __forceinline__ void drain_blocks(const uint32_t* q, uint32_t qn, uint64_t* cq, uint32_t& cqn,
-                                             uint32_t lane, const DrawKey& dk, uint64_t g_begin, uint64_t lo,
-                                             uint64_t hi, uint64_t dense_lim, uint32_t k, Hit& hit) {
-    __builtin_amdgcn_wave_barrier();
-    const bool valid = lane < qn;
-    resolve_block(dk, valid, g_begin + (valid ? q[lane] : 0u), lo, hi, dense_lim, k, cq, cqn, lane, hit);
-    drain_queue(dk, cq, cqn, lane, k, hit);
-}
-
-// K1 main loop, per-iteration pushes (the product launches k1_body_bits below; this form stays as
-// the A/B reference of tools/micro_k1.hip): grid-stride over level-0 blocks (16 indices each), U blocks per lane per
-// iteration; wave-uniform so the queue can run full-wave level-1 evaluations.  Hits (k ln(n/k) of
-// them) go straight to global atomicMax on the k-slot winner table: ~14k atomics per 1e9 indices
-// at k = 1024.  `q` = this wave's block queue (>= 63 + 64 U entries), `cq` its candidate queue
-// (kQueue entries).
-template <int U>
-__device__ __forceinline__ void k1_body(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
-                                        uint64_t n_groups, unsigned long long* __restrict__ win, uint32_t* q,
-                                        uint64_t* cq) {
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t qn = 0, cqn = 0;
-    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
-    const uint64_t dense_lim = 256ull * k;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * U;
-    for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U; base < n_groups;
-         base += stride) {
-        u32x4 w[U];
-        uint32_t off[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            off[u] = (uint32_t)(base + u * 64 + lane);  // n_groups < 2^32 per launch (host splits)
-            w[u] = level0(dk, g_begin + off[u]);
-        }
-        bool has[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)  // dense region (index < 256k): any block may hit
-            has[u] = (off[u] < n_groups) &  // bitwise: no short-circuit branches
-                     (((((g_begin + off[u]) << 4) + 1) < dense_lim) | any_zero_byte(w[u]));
-        push_blocks<U>(has, off, q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
-    }
-    drain_blocks(q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
-}
-
-// ---- K1 with deferred pushes -------------------------------------------------------------------
-// The per-iteration push above runs on ~every iteration (some lane of the wave nearly always holds
-// a candidate block) and cost ~28 us per 1e9 indices.  Here each lane only ORs one bit per block
-// into a register mask; every W = 32 / U iterations the wave pushes the set bits in rounds -- each
-// round every lane with bits left pushes its lowest one (ballot + prefix count), so a round is one
-// wave-uniform step and the queue needs room for just one round (64) beyond a partial batch.
-// The window's nb bits are shifted in oldest first (bits = bits * 2 + has: one v_lshl_or per block),
-// so bit b is window block idx = nb - 1 - b, the block at offset base0 + (idx / U) * stride +
-// (idx % U) * 64 + lane (all 32-bit: offsets < 2^31 per launch, stride * W < 2^32).
-template <int U, class Hit>
-__device__ __forceinline__ void push_bits(uint32_t bits, uint32_t nb, uint32_t base0, uint32_t stride, uint32_t* q,
-                                          uint32_t& qn, uint64_t* cq, uint32_t& cqn, uint32_t lane, const DrawKey& dk,
-                                          uint64_t g_begin, uint64_t lo, uint64_t hi, uint64_t dense_lim, uint32_t k,
-                                          Hit& hit) {
-    const unsigned long long lt = lanemask_lt64();
-    while (__any(bits != 0)) {
-        const bool has = bits != 0;
-        const unsigned long long bal = __ballot(has);
-        if (has) {
-            const uint32_t idx = nb - 1 - __builtin_ctz(bits);
-            bits &= bits - 1;
-            q[qn + __popcll(bal & lt)] = base0 + (idx / U) * stride + (idx % U) * 64u + lane;
-        }
-        qn += (uint32_t)__popcll(bal);
-        if (qn >= 64) {
-            qn -= 64;
-            __builtin_amdgcn_wave_barrier();
-            resolve_block(dk, true, g_begin + q[qn + lane], lo, hi, dense_lim, k, cq, cqn, lane, hit);
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-}
-
-template <int U>
-__device__ __forceinline__ void k1_body_bits(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi,
-                                             uint64_t g_begin, uint64_t n_groups,
-                                             unsigned long long* __restrict__ win, uint32_t* q, uint64_t* cq) {
-    constexpr int W = 32 / U;  // iterations per push window (one bit per block)
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t qn = 0, cqn = 0;
-    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
-    const uint64_t dense_lim = 256ull * k;
-    const uint32_t ng = (uint32_t)n_groups;  // < 2^31 per launch (host splits)
-    // first offset whose block lies wholly in the sparse region (16 g + 1 >= 256 k): from there on
-    // a block holds a candidate iff one of its 16 level-0 bytes is zero
-    const uint64_t g_sparse = (dense_lim + 14) >> 4;
-    const uint32_t off_sparse = g_sparse <= g_begin ? 0u : (uint32_t)std::min<uint64_t>(g_sparse - g_begin, ng);
-    const uint32_t stride = gridDim.x * blockDim.x * U;
-    uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
-    // per-lane level-0 counter kept in VGPRs and stepped by `stride` (rebuilding it from a
-    // scalar base every iteration made the compiler pad SALU->VALU hazards with 15 s_nop).  The
-    // launch never crosses a multiple of 2^32 blocks (launch_k1_last_writer splits there), so the
-    // counter's high word is one scalar for the whole launch: Philox round 0's first output and
-    // round 1's first product are then wave-uniform and leave the VALU (19 -> 18 v_mad_u64_u32 and
-    // 20 -> 19 v_bitop3 per block); only the low word is carried per lane.
-    const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g_begin >> 32));
-    uint32_t gl = (uint32_t)g_begin + base + lane;
-    while (base < ng) {  // wave-uniform
-        const uint32_t base0 = base;
-        uint32_t bits = 0, nb = 0;
-        for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride, nb += U) {
-            u32x4 w[U];
-            // block u's counter is gl + 64 u: the addend rides in the first product (no v_add)
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                w[u] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
-            if (base >= off_sparse && base + U * 64 <= ng) {  // steady state: zero-byte test only
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    // some b_e == 0 <=> the 16-bit OR of the planes' halves is not all ones
-                    const uint32_t x = w[u].x | w[u].y | w[u].z | w[u].w;
-                    uint32_t y;
-                    asm("v_or_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
-                        : "=v"(y) : "v"(x));
-                    const bool has = (uint16_t)y != 0xFFFFu;
-                    bits = bits + bits + (uint32_t)has;
-                }
-            } else {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t off = base + u * 64 + lane;
-                    const bool has =
-                        (off < ng) & (((((g_begin + off) << 4) + 1) < dense_lim) | any_zero_byte(w[u]));
-                    bits = (bits << 1) | (uint32_t)has;
-                }
-            }
-        }
-        push_bits<U>(bits, nb, base0, stride, q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
-    }
-    drain_blocks(q, qn, cq, cqn, lane, dk, g_begin, lo, hi, dense_lim, k, hit);
-}
-
-// ---- K1 with the zero-byte mask carried in the queue (k1_body_z) -------------------------------
-// k1_body_bits pushes a block's OFFSET, and the resolve recomputes its level-0 Philox to find the
-// candidate bytes.  In the sparse region (i + 1 >= 256 k) a candidate is exactly a zero byte, so
-// the 16-bit fold of the block's planes (y: bit e clear <=> b_e == 0) says everything the resolve
-// needs: the main loop leaves y in an LDS window beside the bit, the push packs it into the queue
-// entry, and the resolve goes straight to the level-1 draw with b = 0 -- no level-0 recompute, no
-// byte extraction.  Dense-region blocks (i < 256 k) carry y = 0 (all bytes zero is impossible for
-// a real block: probability 2^-128) and take the recomputing resolve.
 #ifndef RSV_K1P_COUNT
 #define RSV_K1P_COUNT(i, v)  // development counters (tools/micro_k1o.hip)
 #endif
-
-constexpr uint32_t kK1ZWin = 20;  // blocks per lane per window (W x U); 16..32 within 2 us, 20 best (r02ad)
 
 // the 16-bit OR of a block's plane halves: bit e clear <=> b_e == 0 (one SDWA op for the fold; the
 // wait state after it keeps a reader right behind from the gfx950 SDWA hazard, see fold_pair)
@@ -314,172 +139,8 @@ __device__ __forceinline__ u32x4 level1_b0_words(const DrawKey& dk, uint64_t i, 
     return philox4x32_10((uint32_t)g1, (uint32_t)(g1 >> 32) | kDomainLevel1, dk.s0, dk.s1, dk.k0, dk.k1);
 }
 
-template <int U, int WIN = kK1ZWin>
-__device__ __forceinline__ void k1_body_z(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
-                                          uint64_t n_groups, unsigned long long* __restrict__ win, uint64_t* q,
-                                          uint16_t* wy, uint32_t* tab, uint64_t* cq) {
-    static_assert(WIN % U == 0 && WIN <= 32, "the window's bits fit one 32-bit mask");
-    constexpr int W = WIN / U;
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t qn = 0, cqn = 0;
-    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
-    const uint64_t dense_lim = 256ull * k;
-    const uint32_t ng = (uint32_t)n_groups;  // < 2^31 per launch (host splits)
-    const uint64_t g_sparse = (dense_lim + 14) >> 4;
-    const uint32_t off_sparse = g_sparse <= g_begin ? 0u : (uint32_t)std::min<uint64_t>(g_sparse - g_begin, ng);
-    const uint32_t stride = gridDim.x * blockDim.x * U;
-    const uint32_t c1u = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(lo >> 33) | kDomainLevel1));
-    const bool hi_uniform = (lo >> 33) == ((hi - 1) >> 33);
-    const bool pre_ok = hi <= (1ull << 40);
-    const uint64_t k_hi = (uint64_t)k << 32;
-    uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
-    const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g_begin >> 32));
-    uint32_t gl = (uint32_t)g_begin + base + lane;
-    uint16_t* wyl = wy + lane;
-    // window row b holds slot s = WIN-1-b: block base0 + (s / U) stride + (s % U) 64 + lane
-    if (lane < WIN) tab[lane] = ((WIN - 1 - lane) / U) * stride + ((WIN - 1 - lane) % U) * 64u;
-    __builtin_amdgcn_wave_barrier();
-    // the steady branch holds blocks wholly inside [lo, hi) and the sparse region
-    const uint32_t off_steady =
-        __builtin_amdgcn_readfirstlane((int)std::max<uint32_t>(off_sparse, (lo & 15) ? 1u : 0u));
-    const uint32_t ng_steady = __builtin_amdgcn_readfirstlane((int)(ng - ((hi & 15) ? 1u : 0u)));
-
-    // all lanes take a queue entry (valid lanes only): its first zero byte gets the level-1 draw
-    // here; a block with more (~3 % of blocks) goes back on the block queue with that byte masked
-    // (y |= its bit), to be met again.  Clipped indices (outside [lo, hi)) were folded into y by
-    // the main loop, so no entry needs a clip.
-    auto resolve = [&](bool valid, uint64_t ent) {
-        const uint32_t off = (uint32_t)ent, y = (uint32_t)(ent >> 32);
-        const uint64_t g = g_begin + off, i0 = g << 4;
-        const bool dense = valid && y == 0;
-        if (__builtin_amdgcn_ballot_w64(dense)) resolve_block(dk, dense, g, lo, hi, dense_lim, k, cq, cqn, lane, hit);
-        const uint32_t zm = (valid && !dense) ? (~y & 0xFFFFu) : 0u;
-        uint32_t rest = 0;
-        if (zm) {
-            const uint32_t e = __builtin_ctz(zm);
-            rest = zm & (zm - 1);
-            const uint64_t i = i0 + e;
-            const u32x4 w = level1_b0_words(dk, i, hi_uniform, c1u);
-            const uint32_t Lh = (i & 1) ? w.z : w.x;
-            // j >= floor((Lh >> 8) (i + 1) / 2^32) (the top 24 of L >> 8's 56 bits): when that
-            // already reaches k the candidate loses (all but ~256 k / i of them); exact otherwise.
-            // Needs (Lh >> 8) (i + 1) < 2^64: i < 2^40 for the whole launch (pre_ok, uniform).
-            const bool maybe = !pre_ok || (uint64_t)(Lh >> 8) * (i + 1) < k_hi;
-            if (maybe) {
-                const uint64_t L = ((uint64_t)Lh << 32) | ((i & 1) ? w.w : w.y);
-                const uint64_t j = __umul64hi(L >> 8, i + 1);
-                if (j < k) hit((uint32_t)j, i);
-            }
-        }
-        const unsigned long long bal = __builtin_amdgcn_ballot_w64(rest != 0);
-        if (bal) {
-            if (rest) {
-                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                q[qn + pos] = (uint64_t)off | ((uint64_t)(~rest & 0xFFFFu) << 32);
-            }
-            qn += (uint32_t)__popcll(bal);
-        }
-    };
-
-    while (base < ng) {  // wave-uniform
-        const uint32_t base0 = base;
-        uint32_t bits = 0, nb = 0;
-        if (base0 >= off_steady && (uint64_t)base0 + (uint64_t)(W - 1) * stride + U * 64 <= ng_steady) {
-            // a whole window of steady iterations, unrolled: the window slot is an immediate LDS
-            // offset, and the bit is shifted in by the compare's carry (v_cmp + v_addc: bits = 2 bits
-            // + has) -- 5 VALU per block beside the Philox and one counter add per iteration
-#pragma unroll
-            for (int t = 0; t < W; ++t) {
-                u32x4 w[U];
-                const uint32_t gt = gl + t * stride;
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    w[u] = philox4x32_10_uniform_hi(gt, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t y = fold16(w[u]);
-                    asm("v_cmp_ne_u32_e32 vcc, 0xffff, %1\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
-                        : "+v"(bits)
-                        : "v"(y)
-                        : "vcc");
-                    wyl[(WIN - 1 - (t * U + u)) * 64] = (uint16_t)y;
-                }
-            }
-            base += W * stride;
-            gl += W * stride;
-            nb = W * U;
-        } else {  // a partial window (first, last, or where the dense / clipped blocks lie)
-            for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride, nb += U) {
-                u32x4 w[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    w[u] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
-                if (base >= off_steady && base + U * 64 <= ng_steady) {  // steady state: zero-byte test only
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint32_t y = fold16(w[u]);
-                        bits = bits + bits + (uint32_t)((uint16_t)y != 0xFFFFu);
-                        wyl[(WIN - 1 - (t * U + u)) * 64] = (uint16_t)y;
-                    }
-                } else {
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint32_t off = base + u * 64 + lane;
-                        const uint64_t i0 = (g_begin + off) << 4;
-                        const bool dense = i0 + 1 < dense_lim;
-                        // indices outside [lo, hi) count as nonzero bytes (never candidates)
-                        const uint32_t y = dense ? 0u : (fold16(w[u]) | (~clip_mask16(i0, lo, hi) & 0xFFFFu));
-                        const bool has = (off < ng) & (dense | ((uint16_t)y != 0xFFFFu));
-                        bits = bits + bits + (uint32_t)has;
-                        wyl[(WIN - 1 - (t * U + u)) * 64] = (uint16_t)y;
-                    }
-                }
-            }
-        }
-        // push the window's marked blocks: each round every lane with bits left pushes its lowest.
-        // Left-aligned, bit b is slot WIN-1-b: its fold is wy row b, its offset lbase + tab[b].
-        bits <<= WIN - nb;
-        const uint32_t lbase = base0 + lane;
-        __builtin_amdgcn_wave_barrier();
-        for (;;) {
-            const bool has = bits != 0;
-            const unsigned long long bal = __builtin_amdgcn_ballot_w64(has);
-            if (!bal) break;
-            const uint32_t b = __builtin_ctz(bits | (1u << (WIN - 1)));  // (any row for a lane with none)
-            bits &= bits - 1;
-            const uint32_t off = lbase + tab[b];
-            const uint32_t y = wyl[b * 64];
-            RSV_K1P_COUNT(6, __popcll(bal));
-            if (has) {
-                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                q[qn + pos] = (uint64_t)off | ((uint64_t)y << 32);
-            }
-            qn += (uint32_t)__popcll(bal);
-            while (qn >= 64) {  // a resolve may append (blocks with more zero bytes)
-                qn -= 64;
-                __builtin_amdgcn_wave_barrier();
-                const uint64_t ent = q[qn + lane];
-                __builtin_amdgcn_wave_barrier();
-                resolve(true, ent);
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-    }
-    while (qn > 0) {  // the last partial rounds (appends shrink geometrically)
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t nv = std::min<uint32_t>(qn, 64u);
-        qn -= nv;
-        const bool valid = lane < nv;
-        const uint64_t ent = valid ? q[qn + lane] : 0ull;
-        __builtin_amdgcn_wave_barrier();
-        resolve(valid, ent);
-    }
-    __builtin_amdgcn_wave_barrier();
-    drain_queue(dk, cq, cqn, lane, k, hit);
-}
-
 // ---- K1 with pair entries (k1_body_p) ----------------------------------------------------------
-// As k1_body_z, but a lane's two blocks of an iteration (offsets o and o + 64) share one window bit
+// As k1_body_z (round 3; now tools/k1_dev_bodies.h), but a lane's two blocks of an iteration (offsets o and o + 64) share one window bit
 // and one queue entry: the 32-bit fold z holds block o's 16-bit fold in its low half and block
 // o + 64's in its high half (bit e clear <=> byte e & 15 of block o + 64 (e >> 4) is zero), built
 // by two SDWA ops straight into the halves, and one compare marks the pair -- 4 VALU ops per block

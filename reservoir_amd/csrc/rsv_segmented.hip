@@ -26,24 +26,45 @@ namespace rsv {
 
 using namespace k2;
 
-size_t segmented_lds_bytes(uint32_t k) { return k2::lds_bytes(k); }
-
-hipError_t launch_segmented_v1(const void* keys, int key_width, const int64_t* offsets, int64_t S, uint32_t k,
-                               const DrawParams& dp, void* out, int64_t* counts, hipStream_t st);
+namespace {
+// global winner tables (k > 4416): scratch of k * 8 bytes per wave, at most this much per launch
+constexpr size_t kGtabBudget = 1ull << 30;
+}  // namespace
 
 hipError_t launch_segmented(const void* keys, int key_width, const int64_t* offsets, int64_t S, uint32_t k,
                             const DrawParams& dp, void* out, int64_t* counts, hipStream_t st) {
     if (S <= 0) return hipSuccess;
-    // RSV_K2=1 keeps the round-1 kernel (A/B measurements); it also serves tables too big for
-    // four waves' LDS here
-    static const int form = [] {
-        const char* e = std::getenv("RSV_K2");
-        return e ? std::atoi(e) : 0;
-    }();
-    const size_t lds = segmented_lds_bytes(k);
-    if (form == 1 || lds > 160 * 1024) return launch_segmented_v1(keys, key_width, offsets, S, k, dp, out, counts, st);
-    const uint32_t k0 = (uint32_t)dp.seed, k1 = (uint32_t)(dp.seed >> 32);
     const uint64_t blocks = ((uint64_t)S + kWaves - 1) / kWaves;
+    if (k2::lds_bytes(k) > k2::kLdsMax) {
+        // large k: the same kernel with each wave's k-slot table in global scratch (zeroed once;
+        // every stream leaves its slice zero again).  Grid: up to 16 workgroups per CU, fewer when
+        // their tables would pass kGtabBudget (k = 65536: 512 workgroups, 1 GiB)
+        const size_t per_wg = (size_t)kWaves * k * 8;
+        const uint64_t cap = std::max<uint64_t>(1, kGtabBudget / per_wg);
+        const unsigned grid = (unsigned)std::min<uint64_t>(std::min<uint64_t>(blocks, cap), 256ull * 16);
+        const size_t bytes = (size_t)grid * per_wg;
+        unsigned long long* gtab = nullptr;
+        hipError_t e = hipMallocAsync((void**)&gtab, bytes, st);
+        if (e != hipSuccess) return e;
+        e = hipMemsetAsync(gtab, 0, bytes, st);
+        const uint32_t k0 = (uint32_t)dp.seed, k1 = (uint32_t)(dp.seed >> 32);
+        const size_t lds = k2::lds_bytes(k, 0, true);
+        if (e == hipSuccess) {
+            if (key_width == 8)
+                hipLaunchKernelGGL((k2_segmented<int64_t, 0, true>), dim3(grid), dim3(64 * kWaves), lds, st,
+                                   (const int64_t*)keys, offsets, S, k, k0, k1, dp.stream, (int64_t*)out, counts,
+                                   k2::kQCap, gtab);
+            else
+                hipLaunchKernelGGL((k2_segmented<int32_t, 0, true>), dim3(grid), dim3(64 * kWaves), lds, st,
+                                   (const int32_t*)keys, offsets, S, k, k0, k1, dp.stream, (int32_t*)out, counts,
+                                   k2::kQCap, gtab);
+            e = hipGetLastError();
+        }
+        const hipError_t e2 = hipFreeAsync(gtab, st);
+        return e != hipSuccess ? e : e2;
+    }
+    const size_t lds = k2::lds_bytes(k);
+    const uint32_t k0 = (uint32_t)dp.seed, k1 = (uint32_t)(dp.seed >> 32);
     // up to 128 four-wave workgroups per CU over the launch (C3: 8 streams per wave): tools/micro_k2 G
     // (r03ai) 1.78 ms at 4096 workgroups, 1.71 at 16384, 1.65 at 32768, 1.66-1.68 at 65536, 1.84 at
     // one stream per wave (262144: every workgroup rebuilds the threshold table)

@@ -40,23 +40,29 @@ def shard_streams(offsets, rank: int, world: int):
 
 
 def sample_shard(sampler, keys_local, global_offset: int) -> None:
-    """Sample this rank's shard of one stream (keys at [global_offset, +len))."""
+    """Sample this rank's shard of one stream (keys at [global_offset, +len)).  An ordered distinct
+    sampler retains its candidate log from its first shard on (combine's exact replay reads it)."""
     if not sampler.is_distinct:
         sampler.seek(global_offset)
+    elif sampler.is_ordered and sampler.count == 0 and hasattr(sampler, "retain_log"):
+        sampler.retain_log(True)
     sampler.sample_all(keys_local)
 
 
 def combine(sampler, group=None, device=None, total_count: int | None = None) -> bool:
     """All-gather the partial states of every rank and merge them into ``sampler`` (on all ranks).
 
-    One collective: each rank packs its partial state into one int64 row -- element samplers
-    ``[idx(k) | keys(k)]`` (16 KB at k = 1024), distinct samplers ``[keys(k) | hashes(k) | meta]``
-    -- so the exchange pays one RCCL latency.  ``total_count`` (the global stream length) saves a
-    second exchange for element samplers; without it the per-rank counts ride along in the row.
+    One collective: each rank packs its partial state into one int64 row (rsv_export_packed) --
+    element samplers ``[idx(k) | keys(k)]`` (16 KB at k = 1024), distinct samplers ``[keys(k) |
+    hashes(k) | meta]`` -- so the exchange pays one RCCL latency, and one device merge
+    (rsv_merge_packed) folds the gathered rows in, stream-ordered: a set-mode distinct or element
+    combine never waits on the host.  ``total_count`` (the global stream length) saves reading the
+    per-rank counts back.
 
-    Ordered distinct samplers (the reference's default ``hashCode``) whose merged boundary hash
-    bucket is oversubscribed take one more exchange, the exact replay: rank r holds the r-th piece
-    of the stream, and the result is the reference's sequential set.  Returns whether it ran.
+    Ordered distinct samplers (the reference's default ``hashCode``) read the merged state back
+    once; when its boundary hash bucket is oversubscribed they take one more exchange, the exact
+    replay: rank r holds the r-th piece of the stream, and the result is the reference's
+    sequential set (every rank needs ``retain_log``).  Returns whether the replay ran.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -65,108 +71,90 @@ def combine(sampler, group=None, device=None, total_count: int | None = None) ->
     if not sampler.is_distinct:
         _combine_elements(sampler, world, group, device, total_count)
         return False
-    row = _distinct_row(sampler, device)
-    flat = torch.empty(world * row.numel(), dtype=torch.int64, device=row.device)
+    width = sampler.packed_width
+    row = torch.empty(width, dtype=torch.int64, device=device)
+    sampler.export_packed(row)
+    flat = torch.empty(world * width, dtype=torch.int64, device=device)
     dist.all_gather_into_tensor(flat, row, group=group)  # flat output: gloo and RCCL both accept
-    rows = flat.view(world, row.numel())
-    meta = _merge_distinct_rows(sampler, rows, total_count)
-    if _ordered_replay_needed(sampler, meta):
-        bounds = replay_bounds(rows, meta, sampler.max_sample_size)
-        h, keys = sampler.export_log(bounds[rank])
-        part = torch.from_numpy(np.concatenate([h, keys.astype(np.int64)])).to(row.device)
-        sizes = torch.empty(world, dtype=torch.int64, device=row.device)
-        dist.all_gather_into_tensor(sizes, torch.tensor([h.size], dtype=torch.int64).to(row.device), group=group)
-        sz = sizes.cpu().numpy()
-        mx = int(sz.max())
-        buf = torch.zeros(2 * mx, dtype=torch.int64, device=row.device)
-        buf[: h.size] = part[: h.size]
-        buf[mx: mx + h.size] = part[h.size:]
-        logs = torch.empty(world * 2 * mx, dtype=torch.int64, device=row.device)
-        dist.all_gather_into_tensor(logs, buf, group=group)
-        lg = logs.view(world, 2 * mx).cpu().numpy()
-        _merge_logs(sampler, [(lg[r, : sz[r]], lg[r, mx: mx + sz[r]]) for r in range(world)], meta)
-        return True
-    return False
+    rows = flat.view(world, width)
+    k = sampler.max_sample_size
+    total = int(rows[:, 2 * k + 1].sum().item()) if total_count is None else int(total_count)
+    sampler.merge_packed(rows, total)
+    if not sampler.is_ordered:
+        return False
+    meta = _ordered_replay_meta(sampler, rows)
+    if meta is None:
+        return False
+    bounds = replay_bounds(rows, meta, k)
+    h, keys = sampler.export_log(bounds[rank])
+    part = torch.from_numpy(np.concatenate([h, keys.astype(np.int64)])).to(device)
+    sizes = torch.empty(world, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(sizes, torch.tensor([h.size], dtype=torch.int64).to(device), group=group)
+    sz = sizes.cpu().numpy()
+    parts = []
+    for r in range(world):  # exact sizes, one broadcast per rank (no padding to the largest log)
+        buf = part if r == rank else torch.empty(2 * int(sz[r]), dtype=torch.int64, device=device)
+        if sz[r]:
+            dist.broadcast(buf, src=dist.get_global_rank(group, r) if group is not None else r, group=group)
+        lg = buf.cpu().numpy()
+        parts.append((lg[: sz[r]], lg[sz[r]:]))
+    _merge_logs(sampler, parts)
+    return True
 
 
 def merge_local(target, shards, total_count: int | None = None) -> bool:
     """``combine`` without a process group: ``shards`` are samplers that each saw one contiguous
     piece of a stream, in order (shard r = rank r), all on one device; their merged state goes into
-    ``target`` (a fresh sampler, or one of the shards).  Same rows, merge calls and exact ordered
+    ``target`` (a fresh sampler, or one of the shards).  Same rows, merge kernels and exact ordered
     replay as ``combine`` -- e.g. C4's 8-way split rehearsed on one GPU.  Returns whether the exact
     ordered replay ran."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+    rows = torch.empty((len(shards), target.packed_width), dtype=torch.int64, device=dev)
+    for r, s in enumerate(shards):
+        s.export_packed(rows[r])
     if not target.is_distinct:
-        k = target.max_sample_size
-        kw = getattr(target, "key_width", 8)
-        body = k * (1 + (kw // 8 if kw > 8 else 1))
-        dev = torch.device("cuda", torch.cuda.current_device())
-        rows = torch.empty((len(shards), body), dtype=torch.int64, device=dev)
-        for r, s in enumerate(shards):
-            s.export_packed(rows[r])
         total = sum(s.count for s in shards) if total_count is None else int(total_count)
         target.merge_packed(rows, total)
         return False
-    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
-    rows = torch.stack([_distinct_row(s, dev) for s in shards])
-    meta = _merge_distinct_rows(target, rows, total_count)
-    if _ordered_replay_needed(target, meta):
-        bounds = replay_bounds(rows, meta, target.max_sample_size)
-        parts = []
-        for r, s in enumerate(shards):
-            h, keys = s.export_log(bounds[r])
-            parts.append((h, keys.astype(np.int64)))
-        _merge_logs(target, parts, meta)
-        return True
-    return False
+    k = target.max_sample_size
+    total = int(rows[:, 2 * k + 1].sum().item()) if total_count is None else int(total_count)
+    target.merge_packed(rows, total)
+    if not target.is_ordered:
+        return False
+    meta = _ordered_replay_meta(target, rows)
+    if meta is None:
+        return False
+    bounds = replay_bounds(rows, meta, k)
+    parts = []
+    for r, s in enumerate(shards):
+        h, keys = s.export_log(bounds[r])
+        parts.append((h, keys.astype(np.int64)))
+    _merge_logs(target, parts)
+    return True
 
 
-# distinct row: [keys(k) | hashes(k) | n, count, tied, max_hash, log_retained, ordered]
+# distinct row (rsv_export_packed): [keys(k) | hashes(k) | n, count, tied, max_hash, log_retained, ordered]
 _META = 6
 
 
-def _distinct_row(sampler, device) -> torch.Tensor:
-    info = sampler.distinct_info()
-    idx, keys, hashes, n = sampler.export_state(device)
-    k = keys.numel()
-    row = torch.empty(2 * k + _META, dtype=torch.int64, device=idx.device)
-    row[:k] = keys.to(torch.int64)
-    row[k:2 * k] = hashes
-    meta = [n, sampler.count, info["tied"], info["max_hash"], info["log_retained"], info["ordered"]]
-    row[2 * k:] = torch.tensor(meta, dtype=torch.int64).to(idx.device, non_blocking=True)
-    return row
-
-
-def _merge_distinct_rows(sampler, rows, total_count):
-    """Bottom-k of the union by (hash, key) (rsv_merge_state); returns the per-rank meta (host)."""
+def _ordered_replay_meta(sampler, rows):
+    """After the device merge of an ordered sampler: the per-rank meta (host) when the exact replay
+    is needed, else None.  The merged set is the reference's unless more distinct elements share its
+    maximum hash than it keeps -- seen in the union, or inside one rank whose own boundary bucket
+    was oversubscribed at that maximum (the engine folds both into ``tied``)."""
+    info = sampler.distinct_info()  # settles the merge: one wait for its published words
+    if not info["tied"]:
+        return None
     k = sampler.max_sample_size
-    world = rows.shape[0]
-    dtype = torch.int64 if sampler.key_width == 8 else torch.int32
     meta = rows[:, 2 * k:].cpu().numpy()
-    total = int(meta[:, 1].sum()) if total_count is None else int(total_count)
-    sampler.merge_state(torch.empty((world, k), dtype=torch.int64, device=rows.device),
-                        rows[:, :k].to(dtype).contiguous(), rows[:, k:2 * k].contiguous(),
-                        meta[:, 0].tolist(), total)
-    return meta
-
-
-def _ordered_replay_needed(sampler, meta) -> bool:
-    """Ordered samplers only: the merged set is the reference's unless more distinct elements share
-    the merged maximum hash than it keeps -- seen in the union (``tied`` after the merge) or inside
-    one rank whose own set was tied at that maximum (it exported only part of its bucket)."""
     if not all(int(m[5]) for m in meta):
-        return False
-    info = sampler.distinct_info()
-    k = sampler.max_sample_size
-    if info["size"] < k:
-        return False  # fewer than k distinct elements overall: the set holds all of them
-    M = info["max_hash"]
-    need = bool(info["tied"]) or any(int(m[2]) and int(m[3]) == M and int(m[0]) == k for m in meta)
-    if need and not all(int(m[4]) for m in meta):
-        warnings.warn("ordered distinct combine: a rank did not retain its candidate log; the merged set "
-                      "resolves the boundary hash bucket by (hash, key) instead of arrival order",
+        return None  # some rank ran in set mode: the (hash, key) set is the defined result
+    if not all(int(m[4]) for m in meta):
+        warnings.warn("ordered distinct combine: a rank did not retain its candidate log (retain_log); the "
+                      "merged set resolves the boundary hash bucket by (hash, key) instead of arrival order",
                       RuntimeWarning)
-        return False
-    return need
+        return None
+    return meta
 
 
 def replay_bounds(rows, meta, k: int) -> list:
@@ -191,7 +179,7 @@ def replay_bounds(rows, meta, k: int) -> list:
     return bounds
 
 
-def _merge_logs(sampler, parts, meta) -> None:
+def _merge_logs(sampler, parts) -> None:
     """Exact ordered merge: every rank's exported candidates, concatenated in rank order, through a
     fresh replica of the reference's RandomValues (rsv_merge_log)."""
     h = np.concatenate([np.asarray(p[0], dtype=np.int64) for p in parts]) if parts else np.empty(0, np.int64)

@@ -29,11 +29,20 @@ Extensions (keyword-only, defaulted so reference-style calls are unchanged):
     order     distinct only: "auto" (default), "set" or "ordered" -- how hash ties are resolved
               (include/reservoir_hip.h rsv_distinct_order): "ordered" reproduces the reference's
               sequential heap for any hash, "set" is the order-independent bottom-k by (hash, key)
+    retain_log  distinct "ordered" only: keep the replayed candidates on the host for the exact
+              multi-rank merge (export_log; reservoir_amd.distributed.combine needs it on every
+              rank whose boundary hash bucket may tie)
+
+sample_all over an indexable host sequence (a list, tuple, range or host numpy array -- the
+reference's IndexedSeq) samples by index first and maps only the elements that end in the
+reservoir, as the reference's sampleIndexed does (Sampler.scala:261-273): no key crosses PCIe but
+the <= k winners (rsv_sample_indexed / rsv_fill_slots).
 """
 from __future__ import annotations
 
 import ctypes as C
 import os
+from collections.abc import Sequence
 from typing import Any, Callable, Iterable
 
 import numpy as np
@@ -93,6 +102,17 @@ def _is_torch_cuda(x) -> bool:
     return t.__module__.startswith("torch") and t.__name__ == "Tensor" and getattr(x, "is_cuda", False)
 
 
+def _indexed(elements) -> bool:
+    """The reference's IndexedSeq with a known size (Sampler.scala:294-307): a host sequence with
+    len() and O(1) indexing -- not a string, not bytes, not a torch tensor (those take the batch
+    paths)."""
+    if isinstance(elements, np.ndarray):
+        return elements.ndim == 1
+    if isinstance(elements, (str, bytes, bytearray)) or type(elements).__module__.startswith("torch"):
+        return False
+    return isinstance(elements, (range, list, tuple, Sequence))
+
+
 def _current_raw_stream(torch, t) -> int:
     """torch's current HIP stream on t's device as an integer handle (cheap form when available)."""
     raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
@@ -107,7 +127,8 @@ class GpuSampler:
     def __init__(self, kind: int, max_sample_size: int, map_fn: Callable, *, reusable: bool,
                  pre_allocate: bool = False, hash_fn=None, hash_kind: int = N.HASH_DEFAULT,
                  key_type: str = "long", engine: str = "philox_r", seed: int | None = None,
-                 stream_id: int = 0, device: int | None = None, order: str = "auto"):
+                 stream_id: int = 0, device: int | None = None, order: str = "auto",
+                 retain_log: bool = False):
         if key_type not in _KEY and not _wide_width(key_type):
             raise IllegalArgumentException(f"key_type must be one of {sorted(_KEY)} or 'bytesN'")
         if engine not in _ENGINE:
@@ -143,12 +164,19 @@ class GpuSampler:
         self._h = h
         self._stream = int(self._L.rsv_get_stream(h) or 0)
         self._precomputed = hash_kind == N.HASH_PRECOMPUTED
+        self._rows = None  # the last merge_packed's rows (a distinct merge reads them until it settles)
+        self._ordered = False
+        if kind == N.KIND_DISTINCT:
+            self._ordered = bool(self.distinct_info()["ordered"])  # no device work at creation
+            if retain_log:
+                N.check(self._L.rsv_retain_log(h, 1))
 
     # -- lifecycle ----------------------------------------------------------------------------
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._L.rsv_destroy(self._h)
             self._h = None
+        self._rows = None
 
     def __del__(self):
         try:
@@ -230,6 +258,9 @@ class GpuSampler:
             return
         if not self._L.rsv_is_open(self._h):
             raise IllegalStateException("use of sampler after calling `result()`")
+        if self._kind == N.KIND_ELEMENTS and self._width <= 8 and _indexed(elements):
+            self._sample_indexed(elements)
+            return
         if self._width > 8:
             keys = self._wide_keys(elements)
         elif isinstance(elements, np.ndarray) and self._map is identity:
@@ -246,6 +277,23 @@ class GpuSampler:
             hashes.ctypes.data_as(C.c_void_p) if hashes is not None else None))
 
     sampleAll = sample_all
+
+    def _sample_indexed(self, seq) -> None:
+        """sampleAll over an IndexedSeq (Sampler.scala:289-312 -> sampleIndexed :261-273): the engine
+        samples the len(seq) indices, and only the elements that now hold a slot are mapped."""
+        n = len(seq)
+        offs = np.empty(self._k, dtype=np.int64)
+        N.check(self._L.rsv_sample_indexed(self._h, n, offs.ctypes.data_as(C.c_void_p)))
+        if n == 0:
+            return
+        sel = np.flatnonzero(offs >= 0)
+        keys = np.zeros(self._k, dtype=self._dtype)
+        if isinstance(seq, np.ndarray) and self._map is identity:
+            keys[sel] = seq[offs[sel]]
+        else:
+            for j in sel.tolist():
+                keys[j] = self._map(seq[int(offs[j])])
+        N.check(self._L.rsv_fill_slots(self._h, keys.ctypes.data_as(C.c_void_p)))
 
     def _wide_keys(self, elements) -> np.ndarray:
         """Host batch of fixed-width byte keys as a contiguous array of dtype VN."""
@@ -331,17 +379,30 @@ class GpuSampler:
                                          C.byref(n)))
         return idx, keys, hashes, n.value
 
+    @property
+    def packed_width(self) -> int:
+        """Length of this sampler's rsv_export_packed row (int64 words)."""
+        if self.is_distinct:
+            return 2 * self._k + 6
+        return self._k * (1 + (self._width // 8 if self._width > 8 else 1))
+
     def export_packed(self, row) -> None:
-        """Element samplers: write ``[idx(k) | keys as int64 (k)]`` into the int64 device tensor
-        ``row`` (one kernel, stream-ordered on a caller stream)."""
+        """Write the packed row (include/reservoir_hip.h rsv_export_packed) into the int64 device
+        tensor ``row``: ``[idx(k) | keys as int64 (k)]`` for element samplers, ``[keys (k) | hashes
+        (k) | n, count, tied, max_hash, log_retained, ordered]`` for distinct ones (one kernel,
+        stream-ordered on a caller stream)."""
         self._order_after_torch(row)
         N.check(self._L.rsv_export_packed(self._h, C.c_void_p(row.data_ptr())))
 
     def merge_packed(self, rows, total_count: int) -> None:
-        """Element samplers: merge the packed rows of a ``[parts, width]`` int64 device tensor."""
+        """Merge the packed rows of a ``[parts, width]`` int64 device tensor: per slot the last
+        writer (elements), the bottom-k of the union (distinct: on the device, no host wait; the
+        rows are kept referenced until the next merge, as the engine may re-read them)."""
         if rows.dim() != 2 or not rows.is_contiguous():
             raise IllegalArgumentException("rows must be a contiguous [parts, width] tensor")
         self._order_after_torch(rows)
+        if self.is_distinct:
+            self._rows = rows
         N.check(self._L.rsv_merge_packed(self._h, C.c_void_p(rows.data_ptr()), int(rows.shape[0]),
                                          int(rows.shape[1]), int(total_count)))
 
@@ -355,17 +416,25 @@ class GpuSampler:
 
     @property
     def is_ordered(self) -> bool:
-        return self.is_distinct and bool(self.distinct_info()["ordered"])
+        """RSV_DISTINCT_ORDERED semantics (fixed at creation: no device state is read)."""
+        return self._ordered
+
+    def retain_log(self, on: bool = True) -> None:
+        """Ordered distinct samplers: keep the candidate log for export_log (before sampling)."""
+        N.check(self._L.rsv_retain_log(self._h, 1 if on else 0))
 
     def export_log(self, bound: int = 2**63 - 1):
         """Ordered distinct samplers: every logged candidate with hash < ``bound`` in arrival order
         as host arrays (hashes int64, keys of the key type)."""
         n = C.c_int64(0)
-        cap = self.distinct_info()["log_entries"]
+        # count first (cap 0): the buffers are sized for what the bound keeps, not the whole log
+        N.check(self._L.rsv_export_log(self._h, int(bound), None, None, 0, C.byref(n)))
+        cap = n.value
         h = np.empty(max(cap, 1), dtype=np.int64)
         k = np.empty(max(cap, 1), dtype=self._dtype)
-        N.check(self._L.rsv_export_log(self._h, int(bound), h.ctypes.data_as(C.c_void_p),
-                                       k.ctypes.data_as(C.c_void_p), cap, C.byref(n)))
+        if cap:
+            N.check(self._L.rsv_export_log(self._h, int(bound), h.ctypes.data_as(C.c_void_p),
+                                           k.ctypes.data_as(C.c_void_p), cap, C.byref(n)))
         return h[: n.value].copy(), k[: n.value].copy()
 
     def merge_log(self, hashes, keys, total_count: int) -> None:
@@ -427,7 +496,7 @@ def distinct(max_sample_size: int, reusable: bool = False, **ext):
     """
 
     def make(map_fn: Callable = identity, hash=_DEFAULT_HASH) -> GpuSampler:
-        _validate_shared(max_sample_size, map_fn)
+        _validate_shared(max_sample_size, map_fn)  # validateDistinctParams :90-95
         hk, hf = _resolve_hash(hash)
         return GpuSampler(N.KIND_DISTINCT, max_sample_size, map_fn, reusable=reusable,
                           hash_fn=hf, hash_kind=hk, **ext)

@@ -7,6 +7,10 @@
 //   jni   bindings/jvm/rsv_jvm.c, the session logic every JNI native method of
 //         bindings/jni/reservoir_jni.c consists of (sample per element, sampleAll over arrays)
 //   abi   per-element rsv_sample (the engine's own staging), for the akka path at C5's k = 1 Mi
+//   fidx  FfmSampler.sampleAll over an IndexedSeq (rsv_sample_indexed + rsv_fill_slots): a few
+//         elements per element first, then the rest of the sequence by index -- map (here: the
+//         key of offset i) runs only for the slots' new holders, no key buffer for the sequence
+//   jidx  the same through rsv_jvm (JniSampler.sampleAll's natives)
 // Each case line of argv[1] names the sampler, its keys (splitmix64(base + i), or a binary key file)
 // and a binary file with the oracle's expected result (tests/test_gpu_ffm.py writes them);
 // distinct results compare as sets.
@@ -83,6 +87,31 @@ struct FfmMirror {
         std::memcpy(stage + filled * width, key, (size_t)width);
         if (precomputed) stage_hash[filled] = hash;
         filled += 1;
+    }
+    // sampleAll over an IndexedSeq of n elements; key_at(i, dst) is `map(seq(i))`.  Returns the
+    // number of elements mapped.
+    template <class KeyAt>
+    int64_t sample_all_indexed(int64_t n, KeyAt key_at) {
+        if (!open) throw JvmException(RSV_E_ILLEGAL_STATE, "use of sampler after calling `result()`");
+        if (filled > 0) {  // the staged keys come first in index order
+            const int64_t f = filled;
+            filled = 0;
+            check(rsv_stage_commit(handle, f));
+        }
+        cap = 0;
+        std::vector<int64_t> offsets((size_t)k);
+        check(rsv_sample_indexed(handle, n, offsets.data()));
+        std::vector<uint8_t> ks((size_t)k * width);
+        int64_t mapped = 0;
+        for (int j = 0; j < k; ++j) {
+            const int64_t o = offsets[(size_t)j];
+            if (o >= 0) {
+                key_at(o, ks.data() + (size_t)j * width);
+                ++mapped;
+            }
+        }
+        check(rsv_fill_slots(handle, ks.data()));
+        return mapped;
     }
     std::vector<uint8_t> result(int64_t* n_out) {
         if (!open) throw JvmException(RSV_E_ILLEGAL_STATE, "use of sampler after calling `result()`");
@@ -286,6 +315,57 @@ static void run_abi(const Case& c) {  // per-element rsv_sample: the engine stag
     rsv_destroy(h);
 }
 
+// sampleAll over an IndexedSeq: the first `pre` elements per element, the rest by index.  The
+// sequence is virtual (key i = make_key(c, i)): no key buffer exists for it.
+static void run_indexed(const Case& c, bool ffm) {
+    const int64_t pre = std::min<int64_t>(c.n, 5);
+    uint8_t key[8];
+    int64_t mapped = 0;
+    std::vector<uint8_t> out;
+    int64_t n = 0;
+    if (ffm) {
+        FfmMirror s(config_of(c));
+        for (int64_t i = 0; i < pre; ++i) {
+            const int64_t h = make_key(c, i, key);
+            s.sample(key, h);
+        }
+        mapped = s.sample_all_indexed(c.n - pre, [&](int64_t o, uint8_t* dst) { make_key(c, pre + o, dst); });
+        out = s.result(&n);
+    } else {
+        rsv_jvm s;
+        const rsv_config cfg = config_of(c);
+        rsv_status st = rsv_jvm_create(&s, &cfg);
+        EXPECT(st == RSV_OK, c.name.c_str());
+        if (st != RSV_OK) return;
+        for (int64_t i = 0; i < pre; ++i) {
+            const int64_t h = make_key(c, i, key);
+            EXPECT(rsv_jvm_sample(&s, key, h) == RSV_OK, c.name.c_str());
+        }
+        std::vector<int64_t> offsets((size_t)c.k);
+        EXPECT(rsv_jvm_sample_indexed(&s, c.n - pre, offsets.data()) == RSV_OK, c.name.c_str());
+        // a call before the owed keys arrive is an IllegalStateException; the sampler is unharmed
+        std::vector<uint8_t> probe((size_t)c.k * c.kw);
+        int64_t pn = 0;
+        EXPECT(rsv_jvm_result(&s, probe.data(), c.k, &pn) == RSV_E_ILLEGAL_STATE, c.name.c_str());
+        std::vector<uint8_t> ks((size_t)c.k * c.kw);
+        for (int j = 0; j < c.k; ++j)
+            if (offsets[(size_t)j] >= 0) {
+                make_key(c, pre + offsets[(size_t)j], ks.data() + (size_t)j * c.kw);
+                ++mapped;
+            }
+        EXPECT(rsv_jvm_fill_slots(&s, ks.data()) == RSV_OK, c.name.c_str());
+        EXPECT(rsv_jvm_fill_slots(&s, ks.data()) == RSV_E_ILLEGAL_STATE, c.name.c_str());  // nothing owed now
+        out.resize((size_t)c.k * c.kw);
+        EXPECT(rsv_jvm_result(&s, out.data(), c.k, &n) == RSV_OK, c.name.c_str());
+        out.resize((size_t)n * c.kw);
+        rsv_jvm_destroy(&s);
+    }
+    EXPECT(same(c, out, n), c.name.c_str());
+    EXPECT(mapped <= c.k, c.name.c_str());  // map ran only for the reservoir's new holders
+    std::printf("  %s: %lld of %lld indexed elements mapped\n", c.name.c_str(), (long long)mapped,
+                (long long)(c.n - pre));
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s cases.txt\n", argv[0]);
@@ -315,6 +395,8 @@ int main(int argc, char** argv) {
             if (c.path == "ffm") run_ffm(c);
             else if (c.path == "jni") run_jni(c);
             else if (c.path == "abi") run_abi(c);
+            else if (c.path == "fidx") run_indexed(c, true);
+            else if (c.path == "jidx") run_indexed(c, false);
             else throw std::runtime_error("unknown path " + c.path);
         } catch (const std::exception& e) {
             std::printf("FAIL %s: exception %s\n", c.name.c_str(), e.what());

@@ -51,7 +51,9 @@ def test_ffm_mirror_call_sequences_match_scala():
     mirror = _body(cpp, "struct FfmMirror {")
     pairs = [("private[this] def nextStage(): Unit = {", "void next_stage() {"),
              ("def sample(element: A): Unit = {", "void sample(const void* key, int64_t hash) {"),
-             ("def result(): IndexedSeq[B] = {", "std::vector<uint8_t> result(int64_t* n_out) {")]
+             ("def result(): IndexedSeq[B] = {", "std::vector<uint8_t> result(int64_t* n_out) {"),
+             ("override def sampleAll(elements: IterableOnce[A]): Unit = elements match {",
+              "int64_t sample_all_indexed(int64_t n, KeyAt key_at) {")]
     for s_head, c_head in pairs:
         s_calls = _scala_calls(_body(scala, s_head))
         c_calls = _cpp_calls(_body(mirror, c_head))

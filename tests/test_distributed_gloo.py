@@ -1,9 +1,10 @@
 """N > 1 path of reservoir_amd.distributed on CPU: world_size-2 gloo, oracle-backed shard samplers.
 
 The shard samplers here are CPU stand-ins built on the oracle (they implement the same
-seek / sample_all / export_state / merge_state protocol as GpuSampler); what is under test is the
-sharding arithmetic and the one-collective combine of reservoir_amd.distributed.  The engine's
-own merge kernel is covered on the GPU (test_gpu_elements / test_gpu_distinct *_merge tests).
+seek / sample_all / export_packed / merge_packed protocol as GpuSampler -- the packed rows of
+include/reservoir_hip.h rsv_export_packed); what is under test is the sharding arithmetic and the
+one-collective combine of reservoir_amd.distributed.  The engine's own merge kernels are covered on
+the GPU (test_gpu_elements / test_gpu_distinct *_merge tests, test_gpu_distributed).
 """
 import os
 import socket
@@ -59,6 +60,10 @@ class OracleElements:
     def max_sample_size(self):
         return self.k
 
+    @property
+    def packed_width(self):
+        return 2 * self.k
+
     def export_packed(self, row):
         row[: self.k] = torch.from_numpy(self.idx)
         row[self.k: 2 * self.k] = torch.from_numpy(self.res)
@@ -71,8 +76,30 @@ class OracleElements:
         return self.res[: min(self.count, self.k)].copy()
 
 
+def _write_row(row, k, keys, hs, meta):
+    """A distinct packed row: [keys(k) | hashes(k) | n, count, tied, max_hash, log_retained, ordered]."""
+    n = keys.size
+    row[:] = 0
+    row[k: 2 * k] = 2**63 - 1
+    row[:n] = torch.from_numpy(np.asarray(keys, dtype=np.int64))
+    row[k: k + n] = torch.from_numpy(np.asarray(hs, dtype=np.int64))
+    row[2 * k:] = torch.tensor(meta, dtype=torch.int64)
+
+
+def _row_entries(rows, k):
+    """(h, key) entries of every gathered row and each row's meta."""
+    ents, metas = set(), []
+    for r in range(rows.shape[0]):
+        meta = rows[r, 2 * k:].tolist()
+        n = meta[0]
+        ents |= set(zip(rows[r, k: k + n].tolist(), rows[r, :n].tolist()))
+        metas.append(meta)
+    return sorted(ents), metas
+
+
 class OracleDistinct:
     is_distinct = True
+    is_ordered = False
     key_width = 8
     key_dtype = np.int64
 
@@ -92,22 +119,19 @@ class OracleDistinct:
     def max_sample_size(self):
         return self.k
 
-    def distinct_info(self):  # set mode: the exact ordered replay never applies
-        keys, hs = self.d.result()
-        return {"ordered": 0, "tied": 0, "log_retained": 0, "size": keys.size,
-                "max_hash": int(hs.max()) if keys.size else -2**63, "log_entries": 0}
+    @property
+    def packed_width(self):
+        return 2 * self.k + 6
 
-    def export_state(self, device):
+    def export_packed(self, row):
         keys, hs = self.d.result()
-        n = keys.size
-        pad = lambda a: torch.from_numpy(np.concatenate([a, np.zeros(self.k - n, dtype=np.int64)]))
-        return torch.full((self.k,), -1, dtype=torch.int64), pad(keys), pad(hs), n
+        o = np.lexsort((keys, hs))
+        keys, hs = keys[o], hs[o]
+        _write_row(row, self.k, keys, hs, [keys.size, self.count, 0, int(hs[-1]) if keys.size else -2**63, 0, 0])
 
-    def merge_state(self, idx, keys, hashes, part_n, total):
-        ents = set()
-        for p, n in enumerate(part_n):
-            ents |= set(zip(hashes[p, :n].tolist(), keys[p, :n].tolist()))
-        self.entries = sorted(ents)[: self.k]
+    def merge_packed(self, rows, total):
+        ents, _ = _row_entries(rows, self.k)
+        self.entries = ents[: self.k]
         self.count = total
 
     def result(self):
@@ -127,6 +151,7 @@ class OracleOrdered:
     superset of what any sequential run admits from it (the engine logs fewer)."""
 
     is_distinct = True
+    is_ordered = True
     key_width = 8
     key_dtype = np.int64
 
@@ -168,19 +193,24 @@ class OracleOrdered:
         return {"ordered": 1, "tied": int(tied), "log_retained": 1, "size": m, "max_hash": mx,
                 "log_entries": self.seen.size}
 
-    def export_state(self, device):
-        keys, hs = self._state()
-        n = keys.size
-        pad = lambda a: torch.from_numpy(np.concatenate([a, np.zeros(self.k - n, dtype=np.int64)]))
-        return torch.full((self.k,), -1, dtype=torch.int64), pad(keys), pad(hs), n
+    @property
+    def packed_width(self):
+        return 2 * self.k + 6
 
-    def merge_state(self, idx, keys, hashes, part_n, total):
-        ents = set()
-        for p, n in enumerate(part_n):
-            ents |= set(zip(hashes[p, :n].tolist(), keys[p, :n].tolist()))
-        ents = sorted(ents)
+    def export_packed(self, row):
+        keys, hs = self._state()
+        info = self.distinct_info()
+        _write_row(row, self.k, keys, hs, [keys.size, self.count, info["tied"], info["max_hash"], 1, 1])
+
+    def merge_packed(self, rows, total):
+        """As the engine's device merge: the (h, key) bottom-k of the union; tied when the union
+        oversubscribes the merged maximum's bucket or a full rank was tied at it."""
+        ents, metas = _row_entries(rows, self.k)
         top = ents[: self.k]
-        self.tied_merge = len(top) == self.k and sum(1 for h, _ in ents if h <= top[-1][0]) > self.k
+        full = len(top) == self.k
+        M = top[-1][0] if top else None
+        self.tied_merge = full and (sum(1 for h, _ in ents if h <= M) > self.k or
+                                    any(m[2] and m[0] == self.k and m[3] == M for m in metas))
         self.merged = (np.array([v for _, v in top], dtype=np.int64), np.array([h for h, _ in top], dtype=np.int64))
         self.count = total
 

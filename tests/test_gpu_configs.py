@@ -186,8 +186,8 @@ def test_c4_share_set_mode_identity(cuda, oracle):
 def test_c4_full_workload_8way(cuda, oracle):
     """C4 at its own workload (BASELINE.json configs[3]): 4e9 Long keys, 30 % duplicates,
     k = 65536, split 8 ways -- 8 distinct samplers on one GPU, each fed one contiguous 5e8 piece
-    (= one rank of the 8-GPU run), merged with distributed.merge_local (export_state -> merge_state,
-    plus the exact ordered replay for the default hash).  Also one sampler fed the whole stream in
+    (= one rank of the 8-GPU run), merged with distributed.merge_local (export_packed -> the device
+    merge_packed, plus the exact ordered replay for the default hash).  Also one sampler fed the whole stream in
     two batches of >= 2^31 keys (the chunk loop).  Both hashes vs the oracle's sequential
     RandomValues over all 4e9 keys (Sampler.scala:383-412)."""
     import threading
@@ -215,7 +215,7 @@ def test_c4_full_workload_8way(cuda, oracle):
     cut = (1 << 31) + 12_345
     for name, ref in refs.items():
         want = np.sort(ref.result()[0])
-        mk = Sampler.distinct(k, seed=seed)
+        mk = Sampler.distinct(k, seed=seed, retain_log=name == "default")
         make = (lambda: mk(hash="identity")) if name == "identity" else (lambda: mk())
         shards = []
         for r in range(parts):

@@ -582,7 +582,7 @@ def test_ordered_exact_shard_merge(cuda, oracle, shards, k, n, buckets, int_keys
         for into_shard in (False, True):
             ss = []
             for piece in np.array_split(vals, shards):
-                s = Sampler.distinct(k, seed=seed, key_type=kt, order="ordered")()
+                s = Sampler.distinct(k, seed=seed, key_type=kt, order="ordered", retain_log=True)()
                 s.sample_all(torch.from_numpy(piece).to(dt).to(cuda))
                 ss.append(s)
             target = ss[0] if into_shard else Sampler.distinct(k, seed=seed, key_type=kt, order="ordered")()
@@ -612,7 +612,7 @@ def test_ordered_exact_merge_archived_log(cuda, oracle, monkeypatch):
         want[seed] = ref.result()[0].tolist()
         ss = []
         for piece in np.array_split(vals, 3):
-            s = Sampler.distinct(250, seed=seed)()
+            s = Sampler.distinct(250, seed=seed, retain_log=True)()
             for sub in np.array_split(piece, 4):
                 s.sample_all(torch.from_numpy(sub).to(cuda))
             ss.append(s)

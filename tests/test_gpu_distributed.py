@@ -2,7 +2,7 @@
 
 Each rank samples its index range of one stream with a GpuSampler (seek + sample_all on device
 keys), then distributed.combine runs the one-collective exchange: export_packed -> all_gather ->
-merge_packed for element samplers, export_state -> all_gather -> merge_state for distinct ones.
+merge_packed, for element and distinct samplers alike (the distinct merge runs on the device).
 Every rank must end with the oracle's single-stream result (oracle.algo_r, oracle.Distinct) --
 including default-hash (ordered) distinct samplers whose boundary hash bucket is oversubscribed,
 which take combine's exact replay (export_log -> all_gather -> merge_log).
@@ -77,7 +77,7 @@ def _worker(rank, world, port, q):
         for seed in range(3):
             cv = _colliding_vals(seed)
             clo, chi = D.shard_range(cv.size, rank, world)
-            o = Sampler.distinct(300, seed=seed)()
+            o = Sampler.distinct(300, seed=seed, retain_log=True)()
             o.sample_all(torch.from_numpy(cv[clo:chi]).to(dev))
             replayed = D.combine(o, device=dev)
             out[f"ordered{seed}"] = (o.result().tolist(), o.count, bool(replayed))

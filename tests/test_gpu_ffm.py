@@ -108,3 +108,47 @@ def test_ffm_and_jni_call_sequences(tmp_path, cuda, oracle):
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("PASS") == len(cases), r.stdout
+
+
+@pytest.mark.gpu
+def test_indexed_sample_all_through_the_bindings(tmp_path, cuda, oracle):
+    """sampleAll over an IndexedSeq through both JVM paths (FfmSampler.sampleAll's downcalls and
+    JniSampler's natives over rsv_jvm): rsv_sample_indexed + rsv_fill_slots, the sequence virtual
+    (no key buffer: the harness computes key i only when the engine names offset i).  At C2's shape
+    -- a 1e9-element sequence, k = 1024 -- the reservoir must equal the oracle's last writers
+    (philox_r) and the oracle's own sampleIndexed walk of Algorithm L (java_l, Sampler.scala:261-273),
+    with map run for at most k elements.  Small cases cover n < k, n = k and Int keys."""
+    exe = build(tmp_path)
+    sm = oracle.lib().or_splitmix64
+    cases = []
+
+    def key_of(base, i, kw):
+        v = np.array([sm(base + int(i))], dtype=np.uint64).view(np.int64)[0]
+        return int(v) if kw == 8 else int(v) >> 33
+
+    def add(name, path, k, kw, engine, seed, stream, n, base, idx):
+        want = np.array([key_of(base, i, kw) for i in idx.tolist()], dtype=np.int64 if kw == 8 else np.int32)
+        f = tmp_path / f"{name}.bin"
+        want.tofile(f)
+        cases.append(f"{name} {path} 0 {k} {kw} 0 0 0 {engine} {seed} {stream} {n} {base} {f}")
+
+    n = 1_000_000_000
+    win = oracle.algo_r_last_writers(0xC0FFEE, 0x5A5A, 1024, 0, n)
+    assert (win >= 0).all()
+    ref = oracle.AlgoL(1000, 0)
+    ref.sample_all_iota(0, n)
+    for path in ("fidx", "jidx"):
+        add(f"{path}_c2_philox", path, 1024, 8, 0, 0xC0FFEE, 0x5A5A, n, 0x5EED0000, win)
+        add(f"{path}_c2_java_l", path, 1000, 8, 1, 0, 0, n, 0x5EED0000, ref.result())
+    for n_small, k in ((500, 1024), (1024, 1024), (70_001, 64)):
+        w = oracle.algo_r_last_writers(7, 8, k, 0, n_small)
+        add(f"jidx_small_{n_small}_{k}", "jidx", k, 4, 0, 7, 8, n_small, 99, w[w >= 0])
+        r = oracle.AlgoL(k, 3)
+        r.sample_all_iota(0, n_small)
+        add(f"fidx_small_java_l_{n_small}_{k}", "fidx", k, 8, 1, 3, 0, n_small, 5, r.result())
+    f = tmp_path / "cases.txt"
+    f.write_text("\n".join(cases) + "\n")
+    r = subprocess.run([str(exe), str(f)], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("PASS") == len(cases), r.stdout

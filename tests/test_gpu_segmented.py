@@ -9,15 +9,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("k", [1, 5, 64, 100, 1024, 3000, 4400])
+@pytest.mark.parametrize("k", [1, 5, 64, 100, 1024, 3000, 4400, 4416, 4417, 8192, 65536])
 def test_ragged_parity(cuda, oracle, k):
-    """k = 3000 / 4400: the winner table exceeds 64 KB of dynamic LDS (k2::lds_bytes)."""
+    """k = 3000 / 4400: the winner table exceeds 64 KB of dynamic LDS (k2::lds_bytes); 4416 is the
+    largest k whose four tables fit one workgroup's 160 KB; from 4417 on every wave's table is a
+    slice of global scratch (k2_segmented<..., GT = true>, rsv_segmented.hip)."""
     import torch
 
     from reservoir_amd import batch
 
     rng = np.random.default_rng(k)
-    lens = rng.integers(0, 5000, size=300)
+    big = k > 4096
+    lens = rng.integers(0, 4 * k + 5000 if big else 5000, size=60 if big else 300)
     lens[:6] = [0, 1, k - 1 if k > 1 else 0, k, k + 1, 4096]
     offs = np.r_[0, np.cumsum(lens)].astype(np.int64)
     keys = oracle.splitmix_keys(k, int(offs[-1]))
@@ -85,7 +88,7 @@ def test_long_streams_sparse_region(cuda, oracle, k):
     assert np.array_equal(out.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("k", [64, 1000])
+@pytest.mark.parametrize("k", [64, 1000, 8192])
 def test_streams_past_2pow27(cuda, oracle, k):
     """Streams of >= 2^27 keys take K2's 64-bit path (u64 LDS winner table, full Philox counter
     words, 64-bit index rebuild in resolve_round).  keys = arange, so each output key is its global
@@ -94,7 +97,7 @@ def test_streams_past_2pow27(cuda, oracle, k):
 
     from reservoir_amd import batch
 
-    lens = [(1 << 27) + 12_345, 1000, (1 << 27) + 1]
+    lens = [(1 << 27) + 12_345, max(1000, k + 808), (1 << 27) + 1]
     offs = np.r_[0, np.cumsum(lens)].astype(np.int64)
     keys = torch.arange(int(offs[-1]), dtype=torch.int64, device=cuda)
     out, cnt = batch.sample_segmented(keys, torch.from_numpy(offs).to(cuda), k, seed=41, stream_base=9)

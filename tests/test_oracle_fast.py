@@ -34,3 +34,24 @@ def test_segmented_timer_runs_reference_samplers(oracle):
             a = oracle.AlgoL(k, s)
             a.sample_all(keys[s * L:(s + 1) * L])
             assert np.array_equal(out[s * k:(s + 1) * k], a.result())
+
+
+@pytest.mark.parametrize("k,base,n", [(20, 1, 3000), (1, 0, 10), (100, -5, 1_000_000), (1024, 7, 500)])
+def test_iota_walk_equals_indexed_walk(oracle, k, base, n):
+    """or_algo_l_sample_all_iota (the sampleIndexed walk over a Range, no element array) reads the
+    elements or_algo_l_sample_all_indexed reads: same reservoir, in one call and in three; for
+    SamplerTest.scala:117-142's setup (k = 20, 1 to 3000, Random(0)) the survey's vector."""
+    a = oracle.AlgoL(k, 3)
+    a.sample_all(np.arange(base, base + n, dtype=np.int64))
+    b = oracle.AlgoL(k, 3)
+    b.sample_all_iota(base, n)
+    c = oracle.AlgoL(k, 3)
+    cuts = [0, n // 3, n // 2, n]
+    for lo, hi in zip(cuts, cuts[1:]):
+        c.sample_all_iota(base + lo, hi - lo)
+    assert np.array_equal(a.result(), b.result()) and np.array_equal(a.result(), c.result())
+    if (k, base, n) == (20, 1, 3000):
+        d = oracle.AlgoL(20, 0)
+        d.sample_all_iota(1, 3000)
+        assert d.result().tolist() == [1335, 1173, 2365, 2555, 705, 392, 612, 786, 1639, 2529, 2575, 2058,
+                                       176, 780, 339, 607, 1147, 1511, 1218, 222]

@@ -4,6 +4,10 @@
   C4g distinct, one GPU's share of C4: 5e8 int64 keys, 30 % duplicates, k = 65536, identity hash
       (K3 filter + merge); also the default Long.hashCode
   C2L the reference's Algorithm L (engine java_l) on C2: 1e9 keys, k = 1024 (K1' replay)
+  C2I C2 through the boundary as the JVM binding's sampleAll(IndexedSeq): a 1e9-element host
+      sequence sampled by index (rsv_sample_indexed), map + keys only for the <= 1024 winners
+  C4M C4's combine on one GPU: 8 shard sets of k = 65536 merged by distributed.merge_local
+      (8 x rsv_export_packed + the device rsv_merge_packed), both hashes
 
 Prints one JSON line per config with the kernel time (HIP events on the launch stream) and the
 8-B-per-element HBM roofline fraction.  Usage: python tools/bench_paths.py [--only c3,c4,c2l]
@@ -168,6 +172,74 @@ def c2l(dev):
             "elements": n, "seconds": t, "Gelem_s": n / t / 1e9}
 
 
+def c2_indexed(dev):
+    """sampleAll over a 1e9-element IndexedSeq through the C ABI (the FFM/JNI bindings' override):
+    K1 over the indices, k x 8 B of slot offsets back, the winners' keys forward -- no key buffer."""
+    from reservoir_amd import Sampler
+
+    n, k = 1_000_000_000, 1024
+    seq = range(n)
+    ts = []
+    for rep in range(12):
+        s = Sampler(k, seed=0xC0FFEE, stream_id=0x5A5A)()
+        t0 = time.perf_counter()
+        s.sample_all(seq)
+        s.result()
+        ts.append(time.perf_counter() - t0)
+        s.close()
+    t = sorted(ts[2:])[len(ts[2:]) // 2]
+    return {"config": "C2 as sampleAll(IndexedSeq) through the ABI (rsv_sample_indexed + rsv_fill_slots): "
+                      "1e9-element host sequence, no key buffer, map on the winners only",
+            "elements": n, "seconds": t, "Gelem_s": n / t / 1e9}
+
+
+def c4_merge(dev, parts=8, k=65536, per_shard=20_000_000):
+    """The C4 combine's merge on one GPU: `parts` shard sets (k = 65536 each, from consecutive
+    slices of C4-distributed keys) merged into a fresh sampler by distributed.merge_local -- the
+    rows and the device merge of distributed.combine without the all-gather.  Time per merge
+    (HIP events on the caller stream, and host wall clock including the result publication)."""
+    from reservoir_amd import Sampler
+    from reservoir_amd import distributed as D
+
+    data = c4_data(parts * per_shard, dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    out = []
+    for hash_kind in ("identity", "default"):
+        mk = Sampler.distinct(k, seed=7, retain_log=hash_kind == "default")
+        make = (lambda: mk(hash="identity")) if hash_kind == "identity" else (lambda: mk())
+        shards = []
+        for r in range(parts):
+            s = make()
+            s.set_stream(stream)
+            s.sample_all(data[r * per_shard:(r + 1) * per_shard])
+            shards.append(s)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        gpu, wall = [], []
+        for rep in range(25):
+            t = make()
+            t.set_stream(stream)
+            torch.cuda.synchronize()
+            w0 = time.perf_counter()
+            e0.record()
+            D.merge_local(t, shards, total_count=parts * per_shard)
+            e1.record()
+            t.result()
+            wall.append(time.perf_counter() - w0)
+            e1.synchronize()
+            gpu.append(e0.elapsed_time(e1) / 1e3)
+            t.close()
+        gpu, wall = sorted(gpu[5:]), sorted(wall[5:])
+        out.append({"config": f"C4 combine: {parts} shard sets of k={k} merged (merge_local = {parts} x "
+                              f"export_packed + device merge_packed), hash={hash_kind}",
+                    "rows": parts, "k": k, "merge_gpu_seconds": gpu[len(gpu) // 2],
+                    "merge_wall_seconds_incl_result": wall[len(wall) // 2]})
+        for s in shards:
+            s.close()
+    del data
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="c3,c4,c2l")
@@ -191,6 +263,11 @@ def main():
         print(json.dumps(c4(dev, "identity")), flush=True)
     if "c2l" in todo:
         print(json.dumps(c2l(dev)), flush=True)
+    if "c2i" in todo:
+        print(json.dumps(c2_indexed(dev)), flush=True)
+    if "c4m" in todo:
+        for r in c4_merge(dev):
+            print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":

@@ -7,7 +7,7 @@
 #include <vector>
 
 #include "../reservoir_amd/csrc/rsv_device.h"
-#include "../reservoir_amd/csrc/rsv_scan.h"
+#include "k1_dev_bodies.h"
 
 using namespace rsv;
 

@@ -16,7 +16,7 @@ __device__ unsigned long long g_dbg[8];
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_dbg[i], (unsigned long long)(v))
 #endif
 #include "../reservoir_amd/csrc/rsv_device.h"
-#include "../reservoir_amd/csrc/rsv_scan.h"
+#include "k1_dev_bodies.h"
 
 using namespace rsv;
 

@@ -60,7 +60,8 @@ int main(int argc, char** argv) {
         for (int rep = 0; rep < 45; ++rep) {
             CK(hipEventRecord(e0));
             hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * k2::kWaves), lds_run, 0, (const int64_t*)keys,
-                               (const int64_t*)offs, S, k, 1u, 0u, 0ull, out, cnt, 0xFFFFFFFFu);
+                               (const int64_t*)offs, S, k, 1u, 0u, 0ull, out, cnt, 0xFFFFFFFFu,
+                               (unsigned long long*)nullptr);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms;
