@@ -235,22 +235,24 @@ def c4_leg(args, rank: int, world: int, dev, backend: str) -> dict:
 
     for hash_kind in ("identity", "default"):
         replays = 0
-        marks = []  # per timed step: events before sampling / before the combine / after it
+        marks = []  # per timed step: events before sampling / before the combine / inside it / after it
 
         def step(mark=False):
             nonlocal replays
             s = make(hash_kind)
             s.set_stream(stream)
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if mark else None
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if mark else None
             if ev:
                 ev[0].record()
             s.sample_all(keys)
             if ev:
                 ev[1].record()
-            replays += D.combine(s, device=dev, total_count=total)
+            inner = [] if mark else None  # after the export / the all-gather / the device merge
+            replays += D.combine(s, device=dev, total_count=total, marks=inner)
             if ev:
+                ev.append(torch.cuda.Event(enable_timing=True))
                 ev[2].record()
-                marks.append(ev)
+                marks.append(ev + inner)
             r = s.result()
             s.close()
             return r
@@ -274,13 +276,18 @@ def c4_leg(args, rank: int, world: int, dev, backend: str) -> dict:
         elapsed = float(el.item())
         # the step split on the stream's own clock (events around sample_all and around combine:
         # the all-gather, the device merge, and for the default hash its one host read-back)
-        samp = statistics.median(a.elapsed_time(b) for a, b, _ in marks)
-        comb = statistics.median(b.elapsed_time(c) for _, b, c in marks)
+        samp = statistics.median(m[0].elapsed_time(m[1]) for m in marks)
+        comb = statistics.median(m[1].elapsed_time(m[2]) for m in marks)
+        gather = statistics.median(m[3].elapsed_time(m[4]) for m in marks)
+        merge = statistics.median(m[4].elapsed_time(m[5]) for m in marks)
+        export = statistics.median(m[1].elapsed_time(m[3]) for m in marks)
         leg = {"hash": hash_kind + (" (Long.hashCode, ordered: exact sequential set)" if hash_kind == "default"
                                     else " (set mode, bit-exact bottom-k)"),
                "steps": args.c4_steps, "ms_per_step": round(elapsed / args.c4_steps * 1e3, 4),
                "Gelem_s": round(total * args.c4_steps / elapsed / 1e9, 3), "exact_replays": replays,
                "sample_ms_median": round(samp, 4), "combine_ms_median": round(comb, 4),
+               "combine_split_ms": {"export_row": round(export, 4), "all_gather": round(gather, 4),
+                                    "device_merge": round(merge, 4)},
                "split_clock": "HIP events on the sampler's (torch's) stream, this rank"}
         if rank == 0:  # the merged set vs one sampler over the whole stream (same seed, same hash)
             full = workloads.c4_slice(total, 0, total, dev)

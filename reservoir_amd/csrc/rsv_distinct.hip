@@ -1107,38 +1107,41 @@ struct Runs {
     __device__ __forceinline__ bool ordered(int r) const { return rows[(int64_t)(r - 1) * stride + 2 * k + 5] != 0; }
 };
 
-// the cut and its tie flag (thread-local; every workgroup of rows_bounds computes it, <= 64 runs).
-// T = the smallest maximum of a full run; tiedT: a full run whose own boundary bucket was
-// oversubscribed sits at T (its export holds only part of that bucket -- with the merged maximum at
-// T the union's tie word cannot see it)
+// the cut and its tie flag, computed by one wave (every workgroup of rows_bounds does: <= 64 rows,
+// lane r - 1 reads row r's meta -- one load latency instead of a chain of 4 per row, which made the
+// pass 111 us at 8 rows).  T = the smallest maximum of a full run; tiedT: a full run whose own
+// boundary bucket was oversubscribed sits at T (its export holds only part of that bucket -- with
+// the merged maximum at T the union's tie word cannot see it).  Wave-uniform results.
 template <typename KeyT>
 __device__ __forceinline__ void runs_top(const Runs<KeyT>& R, int parts, int64_t set_max, bool set_over,
                                          int64_t* top, int64_t* T_out, bool* tiedT, bool* all_ordered) {
-    int64_t T = R.m == R.k ? set_max : INT64_MAX;
-    int64_t mx = R.m > 0 ? set_max : INT64_MIN;
-    bool tt = R.m == R.k && set_over, ord = true;
-    for (int r = 1; r <= parts; ++r) {
-        const int64_t n = R.n(r), mh = R.max_h(r);
-        ord = ord && R.ordered(r);
-        if (n > 0) mx = std::max(mx, mh);
-        if (n == R.k) {
-            const bool t = R.tied(r);
-            if (mh < T) {
-                T = mh;
-                tt = t;
-            } else if (mh == T) {
-                tt = tt || t;
-            }
-        }
+    const int lane = (int)(threadIdx.x & 63);
+    const bool on = lane < parts;
+    const int64_t n = on ? R.n(lane + 1) : 0;
+    const int64_t mh = on ? R.max_h(lane + 1) : INT64_MIN;
+    const bool t = on && R.tied(lane + 1), ord = !on || R.ordered(lane + 1);
+    const bool full = n == R.k;
+    int64_t T = full ? mh : INT64_MAX, mx = n > 0 ? mh : INT64_MIN;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        T = std::min(T, shfl_xor_any(T, off));
+        mx = std::max(mx, shfl_xor_any(mx, off));
     }
+    if (R.m == R.k) T = std::min(T, set_max);
+    if (R.m > 0) mx = std::max(mx, set_max);
+    const bool tt = (R.m == R.k && set_over && set_max == T) || __ballot(full && t && mh == T) != 0;
     *top = std::min(T, mx);
     *T_out = T;
     *tiedT = tt;
-    *all_ordered = ord;
+    *all_ordered = __ballot(!ord) == 0;
 }
 
 // start[r * (B + 1) + b] = first index of run r whose bucket is >= b (entries above top: bucket B).
-// One thread per index i in [0, n_r] (i = n_r closes the run); grid (x, parts + 1), y = run.
+// One thread per index i in [0, n_r] (i = n_r closes the run); grid (x, parts + 1), y = run.  Each
+// bucket's first entry stores its index (one store per non-empty bucket); the buckets a run skips
+// keep the all-ones fill and rows_fill gives them the next bucket's start (a run sparse in the
+// buckets -- an empty one, or a shard with few elements under the cut -- would otherwise leave one
+// thread storing every skipped bucket in turn: 128 us at 8 rows with an empty target).
 template <typename KeyT>
 __global__ __launch_bounds__(kBlock) void rows_bounds(Runs<KeyT> R, int32_t parts, int64_t set_max, int32_t set_over,
                                                       uint32_t lb, int64_t* __restrict__ ctl, int32_t log_bmax,
@@ -1146,17 +1149,19 @@ __global__ __launch_bounds__(kBlock) void rows_bounds(Runs<KeyT> R, int32_t part
     __shared__ int64_t s_top;
     __shared__ uint64_t s_q;
     const int r = (int)blockIdx.y;
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {
         int64_t top, T;
         bool tiedT, ord;
         runs_top(R, parts, set_max, set_over != 0, &top, &T, &tiedT, &ord);
-        const uint64_t span = (uint64_t)top - (uint64_t)INT64_MIN;
-        s_top = top;
-        s_q = span == UINT64_MAX ? 1ull : UINT64_MAX / (span + 1);
-        if (blockIdx.x == 0 && r == 0) {
-            ctl[5] = 0;  // bucket_emit's tie word
-            ctl[6] = (tiedT ? 2 : 0) | (ord ? 1 : 0);
-            ctl[7] = T;
+        if (threadIdx.x == 0) {
+            const uint64_t span = (uint64_t)top - (uint64_t)INT64_MIN;
+            s_top = top;
+            s_q = span == UINT64_MAX ? 1ull : UINT64_MAX / (span + 1);
+            if (blockIdx.x == 0 && r == 0) {
+                ctl[5] = 0;  // bucket_emit's tie word
+                ctl[6] = (tiedT ? 2 : 0) | (ord ? 1 : 0);
+                ctl[7] = T;
+            }
         }
     }
     if (blockIdx.x == 0 && r == 0) zero_bucket_groups(ctl, log_bmax);
@@ -1178,7 +1183,37 @@ __global__ __launch_bounds__(kBlock) void rows_bounds(Runs<KeyT> R, int32_t part
             const int64_t h = R.h(r, i - 1);
             bp = h <= top ? (int64_t)map(h) : (int64_t)B;
         }
-        for (int64_t b = bp + 1; b <= (int64_t)bi; ++b) st[b] = (uint32_t)i;
+        if ((int64_t)bi != bp) st[bi] = (uint32_t)i;
+    }
+}
+
+// the skipped buckets of every run: start[b] = min(start[b], start[b + 1]) from the top bucket down
+// (a suffix minimum; unwritten entries are all ones).  One workgroup per run, each thread a
+// contiguous piece, a workgroup scan of the pieces' minima for the carries.
+__global__ __launch_bounds__(1024) void rows_fill(uint32_t lb, uint32_t* __restrict__ start) {
+    __shared__ uint32_t s_min[1024 / 64];
+    const uint32_t B1 = (1u << lb) + 1;
+    uint32_t* st = start + (size_t)blockIdx.x * B1;
+    const uint32_t per = (B1 + blockDim.x - 1) / blockDim.x;
+    const uint32_t a = threadIdx.x * per, e = std::min(B1, a + per);
+    uint32_t m = 0xFFFFFFFFu;
+    for (uint32_t b = e; b-- > a;) m = std::min(m, st[b]);  // this piece's minimum
+    // exclusive suffix minimum over the pieces after this one: within the wave, then across waves
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t incl = m;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_down((int)incl, off);
+        if (lane + off < 64) incl = std::min(incl, v);
+    }
+    if (lane == 0) s_min[w] = incl;
+    __syncthreads();
+    uint32_t carry = (uint32_t)__shfl_down((int)incl, 1);
+    if (lane == 63) carry = 0xFFFFFFFFu;
+    for (uint32_t x = w + 1; x < blockDim.x / 64; ++x) carry = std::min(carry, s_min[x]);
+    for (uint32_t b = e; b-- > a;) {
+        carry = std::min(carry, st[b]);
+        st[b] = carry;
     }
 }
 
@@ -2694,10 +2729,12 @@ static int merge_rows_impl(DistinctState* d, const int64_t* rows, int32_t parts,
         d->mstart_cap = need;
     }
     const Runs<KeyT> R{rows, stride, k, d->set_h, (const KeyT*)d->set_k, d->m};
+    RSV_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d->mstart, 0xFFFFFFFFu, (size_t)need, st));
     const int64_t longest = std::max<int64_t>(d->m, k) + 1;
     const dim3 bgrid((unsigned)std::min<int64_t>((longest + kBlock - 1) / kBlock, 1024), (unsigned)(parts + 1));
     hipLaunchKernelGGL(rows_bounds<KeyT>, bgrid, dim3(kBlock), 0, st, R, parts, d->m ? d->set_top : INT64_MIN,
                        (int32_t)(d->m == k && d->over), (uint32_t)lb, d->sctl, d->log_bmax_s, d->mstart);
+    hipLaunchKernelGGL(rows_fill, dim3((unsigned)(parts + 1)), dim3(1024), 0, st, (uint32_t)lb, d->mstart);
     KeyT* bk = (KeyT*)d->sbk;
     hipLaunchKernelGGL(rows_sort<KeyT>, dim3((B + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, R, parts,
                        (uint32_t)lb, (const uint32_t*)d->mstart, d->sctl, d->log_bmax_s, d->sbh, bk);

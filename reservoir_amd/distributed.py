@@ -49,7 +49,14 @@ def sample_shard(sampler, keys_local, global_offset: int) -> None:
     sampler.sample_all(keys_local)
 
 
-def combine(sampler, group=None, device=None, total_count: int | None = None) -> bool:
+def _mark(marks) -> None:
+    if marks is not None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        marks.append(ev)
+
+
+def combine(sampler, group=None, device=None, total_count: int | None = None, marks: list | None = None) -> bool:
     """All-gather the partial states of every rank and merge them into ``sampler`` (on all ranks).
 
     One collective: each rank packs its partial state into one int64 row (rsv_export_packed) --
@@ -63,6 +70,7 @@ def combine(sampler, group=None, device=None, total_count: int | None = None) ->
     once; when its boundary hash bucket is oversubscribed they take one more exchange, the exact
     replay: rank r holds the r-th piece of the stream, and the result is the reference's
     sequential set (every rank needs ``retain_log``).  Returns whether the replay ran.
+    ``marks`` (a list): CUDA events are appended after the export, the all-gather and the merge.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -74,12 +82,15 @@ def combine(sampler, group=None, device=None, total_count: int | None = None) ->
     width = sampler.packed_width
     row = torch.empty(width, dtype=torch.int64, device=device)
     sampler.export_packed(row)
+    _mark(marks)
     flat = torch.empty(world * width, dtype=torch.int64, device=device)
     dist.all_gather_into_tensor(flat, row, group=group)  # flat output: gloo and RCCL both accept
+    _mark(marks)
     rows = flat.view(world, width)
     k = sampler.max_sample_size
     total = int(rows[:, 2 * k + 1].sum().item()) if total_count is None else int(total_count)
     sampler.merge_packed(rows, total)
+    _mark(marks)
     if not sampler.is_ordered:
         return False
     meta = _ordered_replay_meta(sampler, rows)
