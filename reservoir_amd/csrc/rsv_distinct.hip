@@ -685,6 +685,7 @@ struct SchedDev {
     uint64_t lo_mult;           // low region: bucket = umulhi(h - MIN, lo_mult * B_lo)
     float hi_a[kMaxRanges];     // high region, piece p (t[p + 1] < h <= t[p]): pos = a u + c, u = (h - MIN) / 2^64
     float hi_c[kMaxRanges];
+    int64_t off;                // the pass's log entries start `off` past the base it is given
 };
 
 // bucket of h for the scheduled merge: B_lo buckets map [MIN, t_lo] linearly (monotone: the
@@ -742,22 +743,33 @@ __global__ __launch_bounds__(kBlock) void sched_filter(const KeyT* __restrict__ 
                                                        int64_t n, int64_t r0, int64_t r1, const SchedDev* __restrict__ sd,
                                                        int64_t* __restrict__ cand_h, KeyT* __restrict__ cand_k,
                                                        uint32_t* __restrict__ cand_i, int64_t* __restrict__ ctl,
-                                                       int64_t cap, int32_t log_bmax) {
+                                                       int64_t cap, int32_t log_bmax, int* __restrict__ vacc_zero) {
     __shared__ int64_t sb[kMaxRanges + 1], stt[kMaxRanges];
+    if (vacc_zero) {  // freshly allocated merge area (the fused pass; ctl_plan zeroed the ctl words)
+        const size_t words = (size_t)kCountStride << log_bmax, stride = (size_t)gridDim.x * blockDim.x;
+        uint32_t* cnt = bucket_count(ctl);
+        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) cnt[i] = 0;
+        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)kVerifyCopies * (kMaxRanges + 1);
+             i += stride)
+            vacc_zero[i] = 0;
+    }
+    const int nr = sd->nr;
+    if (nr < 2) return;  // no pass (ctl_plan found none)
     // (the plan is NOT a kernel argument: 8192 workgroups reading ~1.6 KB of kernarg memory each
     // made the pass 709 -> 769 us; a device copy, read through L2, costs one small copy dispatch)
     if (blockIdx.x == 0) {  // the merge's tie word and group sums (bucket_sort adds, bucket_emit sets)
         if (threadIdx.x == 0) ctl[5] = 0;
         zero_bucket_groups(ctl, log_bmax);
     }
-    const int nr = sd->nr;
     for (int i = threadIdx.x; i <= nr; i += blockDim.x) {
         sb[i] = sd->b[i];
         if (i < nr) stt[i] = sd->t[i];
     }
     __syncthreads();
     RangeBound rb{sb, stt, 0, 0, 0};
-    k3_filter_body<KeyT, HASH, true>(keys, hashes, n, r0, r1, rb, cand_h, cand_k, (unsigned long long*)ctl, cap, cand_i);
+    const int64_t off = sd->off;
+    k3_filter_body<KeyT, HASH, true>(keys, hashes, n, r0, r1, rb, cand_h + off, cand_k + off, (unsigned long long*)ctl,
+                                     cap, cand_i + off);
 }
 
 // the scheduled merge's bucket filing, after the pass: the set's members (tag 0; backed up first,
@@ -772,6 +784,11 @@ __global__ __launch_bounds__(kBlock) void sched_file(const SchedDev* __restrict_
                                                      int64_t* __restrict__ bak_h, KeyT* __restrict__ bak_k) {
     __shared__ int64_t stt[kMaxRanges];
     const int nr = sd->nr;
+    if (nr < 2) return;
+    const int64_t off = sd->off;
+    cand_h += off;
+    cand_k += off;
+    cand_i += off;
     for (int i = threadIdx.x; i < nr; i += blockDim.x) stt[i] = sd->t[i];
     __syncthreads();
     const uint32_t B_lo = sd->B_lo;
@@ -793,6 +810,175 @@ __global__ __launch_bounds__(kBlock) void sched_file(const SchedDev* __restrict_
             sink.put(cand_h[e], cand_k[e], cand_i[e] + 1u);
         }
     }
+}
+
+// ---- the plan (host: sched_sample; device: ctl_plan, the fused first chunk + pass) ------------
+__host__ __device__ inline double sched_ufrac(int64_t t) {  // fraction of the hash range at or below t
+    return ((double)((uint64_t)t - (uint64_t)INT64_MIN) + 1.0) / 18446744073709551616.0;
+}
+__host__ __device__ inline int64_t sched_bound_at(double frac) {  // largest t with ufrac(t) <= frac
+    if (frac >= 1.0) return INT64_MAX;
+    const double x = floor(frac * 18446744073709551616.0) - 1.0;
+    return x < 0 ? INT64_MIN : (int64_t)((uint64_t)x ^ 0x8000000000000000ull);
+}
+
+// Range starts and bounds of a pass over n elements after S0 seen, current bound t0 (see
+// sched_sample); returns the expected candidate count, or -1 for fewer than two ranges.
+__host__ __device__ inline double sched_plan_ranges(SchedDev* sp, double S0, int64_t t0, int64_t n, int64_t k,
+                                                    double beta) {
+    S0 = S0 > 1.0 ? S0 : 1.0;
+    const double D0 = fmax((double)k, (double)k / sched_ufrac(t0));
+    const double dfr = fmin(1.0, fmax(0.5, D0 / S0));
+    const double g = fmax(1.08, pow((S0 + (double)n) / S0, 1.0 / (kMaxRanges - 2)));
+    int nr = 0;
+    sp->b[0] = 0;
+    sp->t[0] = t0;
+    for (double P = S0 * g;; P *= g) {
+        ++nr;
+        int64_t bn = ((int64_t)(P - S0) + 15) & ~(int64_t)15;
+        if (bn >= n - 16 || nr == kMaxRanges) {
+            sp->b[nr] = n;
+            break;
+        }
+        bn = bn > sp->b[nr - 1] + 16 ? bn : sp->b[nr - 1] + 16;
+        sp->b[nr] = bn;
+        const double D = D0 + dfr * (double)bn;
+        const int64_t tb = sched_bound_at(beta * (double)k / D);
+        sp->t[nr] = tb < sp->t[nr - 1] ? tb : sp->t[nr - 1];
+    }
+    sp->nr = nr;
+    if (nr < 2) return -1.0;
+    double c_pred = 0;
+    for (int r = 0; r < nr; ++r) c_pred += (double)(sp->b[r + 1] - sp->b[r]) * fmin(1.0, sched_ufrac(sp->t[r]));
+    return c_pred;
+}
+
+// The merge's bucket map for 2^lb buckets.  Its entries are uniform in h below their range's
+// bound: F(h) = sum_r len_r min(u, u_r) (u = fraction of the hash range below h); the set's k
+// members count as range 0 elements (uniform below t[0]: k / u_0 of them per unit of u)
+__host__ __device__ inline void sched_plan_map(SchedDev* sp, int64_t k, int32_t lb) {
+    const int nr = sp->nr;
+    auto flen = [&](int r) {
+        return (double)(sp->b[r + 1] - sp->b[r]) + (r == 0 ? (double)k / sched_ufrac(sp->t[0]) : 0.0);
+    };
+    double F_top = 0, L_all = 0;
+    for (int r = 0; r < nr; ++r) {
+        F_top += flen(r) * sched_ufrac(sp->t[r]);
+        L_all += flen(r);
+    }
+    sp->lb = (uint32_t)lb;
+    sp->B = 1u << lb;
+    const int64_t t_lo = sp->t[nr - 1];
+    const double F_lo = L_all * sched_ufrac(t_lo);
+    const double lo_frac = fmin(0.9, fmax(0.02, F_lo / F_top));
+    const uint32_t blo = (uint32_t)(lo_frac * sp->B);
+    sp->B_lo = blo < 1 ? 1u : (blo > sp->B - 1 ? sp->B - 1 : blo);
+    const uint64_t span_lo = (uint64_t)t_lo - (uint64_t)INT64_MIN;
+    sp->lo_mult = span_lo == UINT64_MAX ? 1ull : UINT64_MAX / (span_lo + 1);
+    const double inv = 1.0 / fmax(F_top - F_lo, 1e-30);
+    double A = 0, FU = 0;  // piece p: A = sum_{r <= p} len_r, and the ranges above it at their bounds
+    for (int p = 0; p + 1 < nr; ++p) {
+        A += flen(p);
+        FU += flen(p) * sched_ufrac(sp->t[p]);
+        sp->hi_a[p] = (float)(A * inv);
+        sp->hi_c[p] = (float)((F_top - FU - F_lo) * inv);
+    }
+}
+
+// wave-wide inclusive scans / reductions (one wave; every lane takes part)
+template <typename T, typename F>
+__device__ __forceinline__ T wave_scan(T v, F op) {
+    const int lane = threadIdx.x & 63;
+    for (int d = 1; d < 64; d <<= 1) {
+        const T o = __shfl_up(v, d);
+        if (lane >= d) v = op(v, o);
+    }
+    return v;
+}
+
+// The fused first chunk's control words to the host (as ctl_publish) AND, from them, the plan of the
+// scheduled pass over the rest of the batch into `out`.  The first chunk is the heap-filling one; the
+// host would otherwise read these words back, plan on the host and only then launch the pass (~18 us
+// of idle GPU, rocprof timeline r03).  The plan is sched_plan_ranges + sched_plan_map with lane r
+// computing range r: its start is 16 r + the prefix max of (bn_j - 16 j) (= the host's running
+// max(bn, b[r - 1] + 16)), its bound a prefix min, the map's sums prefix sums (one thread doing the
+// host loops took 352 us).  No pass (out->nr = 0, and the pass's overflow word set so that its sort
+// and emit skip) unless the chunk merged on the device with the heap full and the plan fits the
+// buffers prepared for it (cap entries, 2^lb buckets).
+__global__ __launch_bounds__(64) void ctl_plan(int64_t* __restrict__ ctl, int64_t* dst, uint32_t* flag, uint32_t gen,
+                                               int64_t cand_cap, int64_t k, double S0, int64_t n, double beta,
+                                               int64_t cap, int32_t lb, SchedDev* __restrict__ out,
+                                               int64_t* __restrict__ sctl, int zero) {
+    const int r = threadIdx.x;  // 64 lanes = kMaxRanges
+    if (zero && r < kCtlWords) sctl[r] = 0;  // a fresh merge area (sched_filter zeroes its counts)
+    int64_t v[6];
+    for (int i = 0; i < 6; ++i) v[i] = ctl[i];
+    if (r < 6) dst[r] = v[r];
+    __syncthreads();
+    if (r < 2) ctl[r] = 0;
+    int nr = 0;
+    int64_t br = 0, tr = 0;
+    bool ok = v[0] <= cand_cap && v[1] == 0 && v[2] >= k && v[3] != INT64_MIN;
+    double fl = 0, ur = 0;
+    if (ok) {
+        S0 = fmax(S0, 1.0);
+        const int64_t t0 = v[3] - 1;
+        const double D0 = fmax((double)k, (double)k / sched_ufrac(t0));
+        const double dfr = fmin(1.0, fmax(0.5, D0 / S0));
+        const double g = fmax(1.08, pow((S0 + (double)n) / S0, 1.0 / (kMaxRanges - 2)));
+        const int64_t bn = r == 0 ? 0 : (((int64_t)(S0 * pow(g, (double)r) - S0) + 15) & ~(int64_t)15);
+        const uint64_t ends = __ballot(r >= 1 && bn >= n - 16);
+        nr = ends ? __ffsll((unsigned long long)ends) - 1 : kMaxRanges;
+        br = wave_scan<long long>(bn - 16 * r, [](long long a, long long b) { return a > b ? a : b; }) + 16 * r;
+        if (r >= nr) br = n;
+        const int64_t tb = r == 0 ? t0 : sched_bound_at(beta * (double)k / (D0 + dfr * (double)br));
+        tr = wave_scan<long long>(r < nr ? tb : INT64_MAX, [](long long a, long long b) { return a < b ? a : b; });
+        const int64_t bnext = __shfl_down((long long)br, 1);  // read only where r + 1 < nr
+        ur = sched_ufrac(tr);
+        const double len = r < nr ? (double)((r + 1 == nr ? n : bnext) - br) : 0.0;
+        double cp = len * fmin(1.0, ur);
+        for (int d = 32; d; d >>= 1) cp += __shfl_xor(cp, d);
+        ok = nr >= 2 && 1.5 * cp + 4 * 4096 <= (double)cap;
+        fl = len + (r == 0 ? (double)k / sched_ufrac(t0) : 0.0);  // the set's members count as range 0
+    }
+    if (__ballot(ok) != ~0ull) ok = false;
+    if (!ok) {
+        if (r == 0) out->nr = 0;
+        if (r == 1) sctl[1] = 1;  // the pass's sort and emit skip too (sched_publish re-arms it)
+        publish_flag(flag, gen);
+        return;
+    }
+    // the bucket map (sched_plan_map)
+    double fu = fl * ur, F_top = fu, L_all = fl;
+    for (int d = 32; d; d >>= 1) {
+        F_top += __shfl_xor(F_top, d);
+        L_all += __shfl_xor(L_all, d);
+    }
+    const int64_t t_lo = __shfl(tr, nr - 1);
+    const double F_lo = L_all * sched_ufrac(t_lo);
+    const double inv = 1.0 / fmax(F_top - F_lo, 1e-30);
+    const double A = wave_scan<double>(fl, [](double a, double b) { return a + b; });
+    const double FU = wave_scan<double>(fu, [](double a, double b) { return a + b; });
+    if (r + 1 < nr) {
+        out->hi_a[r] = (float)(A * inv);
+        out->hi_c[r] = (float)((F_top - FU - F_lo) * inv);
+    }
+    if (r <= nr) out->b[r] = br;
+    if (r == 63 && nr == kMaxRanges) out->b[kMaxRanges] = n;
+    if (r < nr) out->t[r] = tr;
+    if (r == 0) {
+        out->nr = nr;
+        const uint32_t B = 1u << lb;
+        out->lb = (uint32_t)lb;
+        out->B = B;
+        const double lo_frac = fmin(0.9, fmax(0.02, F_lo / F_top));
+        const uint32_t blo = (uint32_t)(lo_frac * B);
+        out->B_lo = blo < 1 ? 1u : (blo > B - 1 ? B - 1 : blo);
+        const uint64_t span_lo = (uint64_t)t_lo - (uint64_t)INT64_MIN;
+        out->lo_mult = span_lo == UINT64_MAX ? 1ull : UINT64_MAX / (span_lo + 1);
+        out->off = v[0];  // behind the chunk's own candidates in the log
+    }
+    publish_flag(flag, gen);
 }
 
 // the plan into device memory: one workgroup copies its by-value argument (the first, so it starts
@@ -942,6 +1128,12 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(int64_t* gh, KeyT* g
     return base;
 }
 
+// buckets per wave of sched_sort (dev builds vary it: make exp EXP=-DRSV_SORT_BPW=4)
+#ifndef RSV_SORT_BPW
+#define RSV_SORT_BPW 1
+#endif
+constexpr uint32_t kSortBpw = RSV_SORT_BPW;
+
 template <typename KeyT>
 __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap, int64_t* __restrict__ ctl,
                                                      int32_t log_bmax, int64_t* __restrict__ bh, KeyT* __restrict__ bk,
@@ -950,16 +1142,16 @@ __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap
     __shared__ int64_t sb[kMaxRanges + 1], stt[kMaxRanges];
     __shared__ int sdiff[kMaxRanges + 1];
     const int64_t c = ctl[0];
-    if (c > cand_cap || ctl[1]) return;  // uniform over the grid
     const int nr = sd->nr;
+    if (c > cand_cap || ctl[1] || nr < 2) return;  // uniform over the grid
     for (int i = threadIdx.x; i <= nr; i += blockDim.x) {
         sb[i] = sd->b[i];
         sdiff[i] = 0;
         if (i < nr) stt[i] = sd->t[i];
     }
     __syncthreads();
-    const uint32_t b = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    if (b < sd->B) {
+    const uint32_t b0 = (blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * kSortBpw;
+    for (uint32_t b = b0; b < b0 + kSortBpw && b < sd->B; ++b) {
         uint32_t* bcnt = bucket_count(ctl) + (size_t)b * kCountStride;
         uint32_t* bdist = bucket_distinct(ctl, log_bmax) + b;
         const uint32_t n = *bcnt;
@@ -978,17 +1170,20 @@ __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap
         }
     }
     __syncthreads();
+#ifdef RSV_EXP_NO_VACC  // dev A/B only: the verdict fails, every pass falls back (kernel times are the point)
+    return;
+#endif
     int* acc = vacc + (size_t)(blockIdx.x % kVerifyCopies) * (kMaxRanges + 1);
     for (int i = threadIdx.x; i <= nr; i += blockDim.x)
         if (sdiff[i]) atomicAdd(&acc[i], sdiff[i]);
 }
 
-// ctl[0..5] and the verification verdict (first range r >= 1 short of k elements, or -1) to
-// coherent host memory, then the flag
+// ctl[0..5], the verification verdict (first range r >= 1 short of k elements, or -1) and the
+// plan's range count (< 2: no pass ran) to coherent host memory, then the flag
 // (then re-arms the candidate counter, the overflow word and the accumulators for the next pass)
-__global__ __launch_bounds__(kBlock) void sched_publish(int64_t* __restrict__ ctl, int* __restrict__ vacc,
-                                                        const SchedDev* __restrict__ sd, int64_t k, int64_t* dst,
-                                                        uint32_t* flag, uint32_t gen) {
+__device__ __forceinline__ void sched_verdict(int64_t* __restrict__ ctl, int* __restrict__ vacc,
+                                              const SchedDev* __restrict__ sd, int64_t k, int64_t* dst, uint32_t* flag,
+                                              uint32_t gen) {
     __shared__ int col[kMaxRanges + 1];
     const int nr = sd->nr;
     for (int i = threadIdx.x; i <= nr; i += blockDim.x) {
@@ -1012,10 +1207,47 @@ __global__ __launch_bounds__(kBlock) void sched_publish(int64_t* __restrict__ ct
         for (int i = 0; i < 6; ++i) dst[i] = ctl[i];
         dst[6] = fail;
         dst[7] = minc;
+        dst[8] = nr;
         ctl[0] = 0;
         ctl[1] = 0;
     }
     publish_flag(flag, gen);
+}
+
+// the set's first min(ctl[2], k) keys into coherent host memory by every workgroup; each releases at
+// system scope and takes a ticket, the last stores the flag
+__device__ __forceinline__ void publish_set_body(const uint32_t* __restrict__ src, uint32_t* dst,
+                                                 const int64_t* __restrict__ ctl, int64_t k, int32_t key_words,
+                                                 uint32_t* flag, uint32_t gen, uint32_t* ticket) {
+    const int64_t words = std::min<int64_t>(ctl[2], k) * key_words;
+    const int64_t vecs = words >> 2;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = t0; i < vecs; i += stride) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    for (int64_t i = (vecs << 2) + t0; i < words; i += stride) dst[i] = src[i];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        const uint32_t prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence_system();
+            __hip_atomic_store(flag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// The scheduled pass's verdict (workgroup 0) and, when a target is given, the merged set's
+// speculative publication (every workgroup) in one dispatch: the set copy (~13 us for 512 KB) no
+// longer waits for a second kernel behind the verdict
+__global__ __launch_bounds__(1024) void sched_publish(int64_t* __restrict__ ctl, int* __restrict__ vacc,
+                                                     const SchedDev* __restrict__ sd, int64_t k, int64_t* dst,
+                                                     uint32_t* flag, uint32_t gen, const uint32_t* __restrict__ set_src,
+                                                     uint32_t* set_dst, int32_t key_words, uint32_t* set_flag,
+                                                     uint32_t set_gen, uint32_t* ticket) {
+    if (blockIdx.x == 0) sched_verdict(ctl, vacc, sd, k, dst, flag, gen);
+    if (set_dst) publish_set_body(set_src, set_dst, ctl, k, key_words, set_flag, set_gen, ticket);
 }
 
 // ctl[0..5] -> coherent host memory + flag (one wave; the host spins instead of a stream sync);
@@ -1039,23 +1271,7 @@ __global__ __launch_bounds__(1024) void publish_set_kernel(const uint32_t* __res
                                                            const int64_t* __restrict__ ctl, int64_t k,
                                                            int32_t key_words, uint32_t* flag, uint32_t gen,
                                                            uint32_t* ticket) {
-    const int64_t words = std::min<int64_t>(ctl[2], k) * key_words;
-    const int64_t vecs = words >> 2;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (int64_t i = t0; i < vecs; i += stride) ((uint4*)dst)[i] = ((const uint4*)src)[i];
-    for (int64_t i = (vecs << 2) + t0; i < words; i += stride) dst[i] = src[i];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence_system();
-        const uint32_t prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == gridDim.x - 1) {
-            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __threadfence_system();
-            __hip_atomic_store(flag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
+    publish_set_body(src, dst, ctl, k, key_words, flag, gen, ticket);
 }
 
 // one logged segment gathered into arrival order (perm from the radix sort of its arrival indices)
@@ -1405,6 +1621,7 @@ struct DistinctState {
     int64_t* shc = nullptr;         // coherent host: published words + flag at [12]
     int64_t* shc_dev = nullptr;
     uint32_t sgen = 0;
+    bool sdirty = false;            // sctl / vacc allocated, not yet zeroed (the fused pass zeroes them)
     bool sched = true;              // RSV_ORDERED_SCHED=0: the chunk loop only
     double sched_beta = 1.6;        // RSV_SCHED_BETA (test hook: a small beta forces the fallback)
     uint32_t* perm = nullptr;       // [ord_cap] one segment's candidates in arrival order
@@ -2121,7 +2338,7 @@ static hipError_t replay_log(DistinctState* d, hipStream_t st) {
 
 // the scheduled pass's buffers for merges of up to `entries` (set + candidates); allocated on first use
 template <typename KeyT>
-static hipError_t sched_ensure(DistinctState* d, int32_t lb, hipStream_t st) {
+static hipError_t sched_ensure(DistinctState* d, int32_t lb, hipStream_t st, bool defer_zero = false) {
     hipError_t e = hipSuccess;
     if (!d->sdev) {
         if ((e = pool_device_alloc((void**)&d->sdev, sizeof(SchedDev)))) return e;
@@ -2129,7 +2346,7 @@ static hipError_t sched_ensure(DistinctState* d, int32_t lb, hipStream_t st) {
         if ((e = hipHostGetDevicePointer((void**)&d->shc_dev, d->shc, 0))) return e;
         ((uint32_t*)(d->shc + 12))[0] = 0;
         if ((e = pool_device_alloc((void**)&d->vacc, (size_t)kVerifyCopies * (kMaxRanges + 1) * 4))) return e;
-        if ((e = hipMemsetAsync(d->vacc, 0, (size_t)kVerifyCopies * (kMaxRanges + 1) * 4, st))) return e;  // re-armed by sched_publish
+        d->sdirty = true;  // re-armed by sched_publish after every pass
         if ((e = pool_device_alloc((void**)&d->bak_h, (size_t)d->k * 8))) return e;
         if ((e = pool_device_alloc(&d->bak_k, (size_t)d->k * d->kw))) return e;
     }
@@ -2146,39 +2363,52 @@ static hipError_t sched_ensure(DistinctState* d, int32_t lb, hipStream_t st) {
         // rounded to 256 B: one aligned fill dispatch (an unaligned tail costs a second one)
         const size_t ctl_bytes = (kCtlWords * 8 + (kCountStride + 1) * 4 * B + 4 * ((B >> 4) + 1) + 255) & ~(size_t)255;
         if ((e = pool_device_alloc((void**)&d->sctl, ctl_bytes))) return e;
-        if ((e = hipMemsetAsync(d->sctl, 0, ctl_bytes, st))) return e;  // counts, counter: re-armed after each pass
+        d->sdirty = true;  // counts, counter: re-armed after each pass
         if ((e = pool_device_alloc((void**)&d->sbh, B * kBucketCap * 8))) return e;
         if ((e = pool_device_alloc(&d->sbk, B * kBucketCap * sizeof(KeyT)))) return e;
         if ((e = pool_device_alloc((void**)&d->sbi, B * kBucketCap * 4))) return e;
         d->log_bmax_s = lb;
     }
+    // zeroed here unless the caller's next pass is the fused one (ctl_plan + sched_filter zero
+    // them: two fills and their host calls fewer ahead of a fresh sampler's first kernel)
+    if (d->sdirty && !defer_zero) {
+        const size_t B = (size_t)1 << d->log_bmax_s;
+        if ((e = hipMemsetAsync(d->vacc, 0, (size_t)kVerifyCopies * (kMaxRanges + 1) * 4, st))) return e;
+        if ((e = hipMemsetAsync(d->sctl, 0, kCtlWords * 8 + kCountStride * 4 * B, st))) return e;
+        d->sdirty = false;
+    }
     return hipSuccess;
 }
 
-// The scheduled pass's buffers (and their zeroing) for a batch of n keys, queued ahead of the batch's
-// first chunk so that the pass itself starts without a host round trip for them.  Sized from an
-// estimate of the pass's candidates (sched_sample's c_pred with D0 = k and distinct elements arriving
-// at >= 3/4 of the positions); a pass that needs more reallocates in sched_ensure.
-template <typename KeyT>
-static hipError_t sched_prepare(DistinctState* d, int64_t n, hipStream_t st) {
-    const double k = (double)d->k;
-    const double c_est = d->sched_beta * k / 0.75 * std::log1p(0.75 * (double)n / k);
-    const int64_t cap = std::min<int64_t>((int64_t)(1.5 * c_est) + 4 * 4096, ((int64_t)1 << 31) - 1);
-    int32_t lb = 1;
-    while (((int64_t)1 << (lb + 6)) < d->k + cap) ++lb;
-    if (((int64_t)kBucketCap * 8 + 20) << lb > ((int64_t)1 << 30)) return hipSuccess;
-    return sched_ensure<KeyT>(d, lb, st);
+// Buffer sizes of a scheduled pass expecting c_pred candidates: its log entries (cap) and merge
+// buckets (2^lb, ~<= 64 entries per bucket: most sort in a single 64-lane pass); false: > 1 GiB of
+// buckets (the chunk loop instead)
+static bool sched_sizes(int64_t k, double c_pred, int64_t* cap, int32_t* lb) {
+    *cap = std::min<int64_t>((int64_t)(1.5 * c_pred) + 4 * 4096, ((int64_t)1 << 31) - 1);
+    int32_t l = 1;
+    while (((int64_t)1 << (l + 6)) < k + *cap) ++l;
+    *lb = l;
+    return (((int64_t)kBucketCap * 8 + 20) << l) <= ((int64_t)1 << 30);
 }
 
-// The scheduled pass over keys[0, n) of a batch, heap full (see SchedDev).  Bounds: with D
-// distinct elements seen, the k-th smallest hash sits near fraction k / D of the range; D at
-// position P is predicted as D0 + dfr (P - S0) (D0 from the current bound, dfr the history's
-// distinct fraction, clamped to [0.5, 1]), and range r's bound keeps fraction beta k / D(start)
-// (beta = 1.6: a stream whose new-distinct rate falls to ~60% of its history's still verifies).
-// Ranges grow geometrically (<= kMaxRanges).  *done = false: nothing changed, run the chunk loop.
+// a pass over n keys at the heap's first fill: its expected candidates (sched_plan_ranges' c_pred
+// with D0 = k and distinct elements arriving at >= 3/4 of the positions)
+static double sched_estimate(const DistinctState* d, int64_t n) {
+    const double k = (double)d->k;
+    return d->sched_beta * k / 0.75 * std::log1p(0.75 * (double)n / k);
+}
+
+// The scheduled pass's buffers (and their zeroing) for a batch of n keys, queued ahead of the batch's
+// first chunk so that the pass itself starts without a host round trip for them; a pass that needs
+// more reallocates in sched_ensure.
 template <typename KeyT>
-static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n, hipStream_t st,
-                        bool* done) {
+static hipError_t sched_prepare(DistinctState* d, int64_t n, hipStream_t st, bool defer_zero) {
+    int64_t cap;
+    int32_t lb;
+    if (!sched_sizes(d->k, sched_estimate(d, n), &cap, &lb)) return hipSuccess;
+    return sched_ensure<KeyT>(d, lb, st, defer_zero);
+}
+
 #define STRY(x)                                                                                        \
     do {                                                                                               \
         hipError_t _e = (x);                                                                           \
@@ -2187,97 +2417,25 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
             return _e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;                     \
         }                                                                                              \
     } while (0)
-    *done = false;
+
+// The pass's kernels over keys[0, n), the plan already in d->sdev (or being written there by a
+// kernel ahead of them): candidates into the log from lbase (+ the plan's `off`), the set's
+// backup, the bucket merge, the verdict to d->shc; then the speculative publication of the set.
+template <typename KeyT>
+static int sched_launch(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n, int64_t lbase,
+                        int64_t cap, uint32_t B, int32_t lb, hipStream_t st, uint32_t* gen, bool* spec,
+                        bool zero = false) {
     const int64_t k = d->k;
-    if (d->m != k || d->max_h == INT64_MIN || n >= ((int64_t)1 << 31) || d->set_cap < k) return RSV_OK;
-    const double beta = d->sched_beta;
-    const double two64 = 18446744073709551616.0;
-    auto ufrac = [&](int64_t t) { return ((double)((uint64_t)t - (uint64_t)INT64_MIN) + 1.0) / two64; };
-    auto bound_at = [&](double frac) -> int64_t {  // largest t with ufrac(t) <= frac
-        if (frac >= 1.0) return INT64_MAX;
-        const double x = std::floor(frac * two64) - 1.0;
-        return x < 0 ? INT64_MIN : (int64_t)((uint64_t)x ^ 0x8000000000000000ull);
-    };
-    SchedDev plan;
-    SchedDev* sp = &plan;
-    const double S0 = std::max(1.0, (double)d->seen);
-    const int64_t t0 = d->max_h - 1;
-    const double D0 = std::max((double)k, (double)k / ufrac(t0));
-    const double dfr = std::min(1.0, std::max(0.5, D0 / S0));
-    const double g = std::max(1.08, std::pow((S0 + (double)n) / S0, 1.0 / (kMaxRanges - 2)));
-    int nr = 0;
-    sp->b[0] = 0;
-    sp->t[0] = t0;
-    for (double P = S0 * g;; P *= g) {
-        ++nr;
-        int64_t bn = ((int64_t)(P - S0) + 15) & ~(int64_t)15;
-        if (bn >= n - 16 || nr == kMaxRanges) {
-            sp->b[nr] = n;
-            break;
-        }
-        bn = std::max(bn, sp->b[nr - 1] + 16);
-        sp->b[nr] = bn;
-        const double D = D0 + dfr * (double)bn;
-        sp->t[nr] = std::min(sp->t[nr - 1], bound_at(beta * (double)k / D));
-    }
-    sp->nr = nr;
-    if (nr < 2) return RSV_OK;  // one range: the plain chunk loop does the same work
-    // expected candidates (duplicates included), the buffer, and the bucket map's regions.  The
-    // merge's entries are uniform in h below their range's bound: F(h) = sum_r len_r min(u, u_r)
-    // (u = fraction of the hash range below h); the set's k members count as range 0 elements
-    // (uniform below t[0]: k / u_0 of them per unit of u)
-    double c_pred = 0;
-    for (int r = 0; r < nr; ++r) c_pred += (double)(sp->b[r + 1] - sp->b[r]) * std::min(1.0, ufrac(sp->t[r]));
-    auto flen = [&](int r) {
-        return (double)(sp->b[r + 1] - sp->b[r]) + (r == 0 ? (double)k / ufrac(sp->t[0]) : 0.0);
-    };
-    double F_top = 0, L_all = 0;
-    for (int r = 0; r < nr; ++r) {
-        F_top += flen(r) * ufrac(sp->t[r]);
-        L_all += flen(r);
-    }
-    const int64_t cap = std::min<int64_t>((int64_t)(1.5 * c_pred) + 4 * 4096, ((int64_t)1 << 31) - 1);
-    int32_t lb = 1;  // ~<= 64 entries per bucket: most sort in a single 64-lane pass
-    while (((int64_t)1 << (lb + 6)) < k + cap) ++lb;
-    if (((int64_t)kBucketCap * 8 + 20) << lb > ((int64_t)1 << 30)) return RSV_OK;  // > 1 GiB of buckets: chunk loop
-    sp->lb = (uint32_t)lb;
-    sp->B = 1u << lb;
-    const int64_t t_lo = sp->t[nr - 1];
-    const double F_lo = L_all * ufrac(t_lo);
-    const double lo_frac = std::min(0.9, std::max(0.02, F_lo / F_top));
-    sp->B_lo = std::min<uint32_t>(sp->B - 1, std::max<uint32_t>(1, (uint32_t)(lo_frac * sp->B)));
-    const uint64_t span_lo = (uint64_t)t_lo - (uint64_t)INT64_MIN;
-    sp->lo_mult = span_lo == UINT64_MAX ? 1ull : UINT64_MAX / (span_lo + 1);
-    const double Fspan = std::max(F_top - F_lo, 1e-30);
-    for (int p = 0; p + 1 < nr; ++p) {
-        double A = 0, Bc = 0;
-        for (int r = 0; r < nr; ++r) {
-            if (r <= p) A += flen(r);
-            else Bc += flen(r) * ufrac(sp->t[r]);
-        }
-        sp->hi_a[p] = (float)(A / Fspan);
-        sp->hi_c[p] = (float)((Bc - F_lo) / Fspan);
-    }
-    // the log holds this batch's candidates as one segment
-    if (d->log_n + cap > d->log_limit) {
-        if (cap > d->log_limit) return RSV_OK;
-        if (!d->segs.empty()) STRY(replay_log<KeyT>(d, st));
-        if (d->log_n + cap > d->log_limit) return RSV_OK;
-    }
-    STRY(ensure_log(d, d->log_n + cap, st));
-    STRY(sched_ensure<KeyT>(d, lb, st));
     const size_t kw = sizeof(KeyT);
-    hipLaunchKernelGGL(sched_plan_store, dim3(1), dim3(256), 0, st, plan, d->sdev);
-    const unsigned B = sp->B;
     KeyT* bk = (KeyT*)d->sbk;
     if (d->timer) d->timer->mark(st);
     {
         const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 32 + 1), 1), 256 * 32);
-        KeyT* lk = (KeyT*)d->log_k + d->log_n;
+        KeyT* lk = (KeyT*)d->log_k + lbase;
 #define RSV_SCHED_FILTER(H)                                                                                        \
     hipLaunchKernelGGL((sched_filter<KeyT, H>), dim3(grid), dim3(kBlock), 0, st, keys, hashes, n, d->r0, d->r1,      \
-                       (const SchedDev*)d->sdev, d->log_h + d->log_n, lk, d->log_i + d->log_n, d->sctl, cap,        \
-                       d->log_bmax_s)
+                       (const SchedDev*)d->sdev, d->log_h + lbase, lk, d->log_i + lbase, d->sctl, cap, d->log_bmax_s,     \
+                       zero ? d->vacc : nullptr)
         switch (d->hash_kind) {
         case kHashJavaLong: RSV_SCHED_FILTER(kHashJavaLong); break;
         case kHashJavaInt: RSV_SCHED_FILTER(kHashJavaInt); break;
@@ -2291,7 +2449,7 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
         // ~1.1 M entries waited on ~4 atomics per thread in sequence (61 us)
         const unsigned fgrid = (unsigned)std::min<int64_t>((k + cap + kBlock - 1) / kBlock, 16384);
         hipLaunchKernelGGL(sched_file<KeyT>, dim3(fgrid), dim3(kBlock), 0, st, (const SchedDev*)d->sdev,
-                           (const int64_t*)(d->log_h + d->log_n), (const KeyT*)lk, (const uint32_t*)(d->log_i + d->log_n),
+                           (const int64_t*)(d->log_h + lbase), (const KeyT*)lk, (const uint32_t*)(d->log_i + lbase),
                            d->sctl, cap, (const int64_t*)d->set_h, (const KeyT*)d->set_k, k, d->sbh, bk, d->sbi,
                            d->bak_h, (KeyT*)d->bak_k);
         STRY(hipGetLastError());
@@ -2299,55 +2457,62 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
     if (d->timer) d->timer->mark(st);
     // the difference array's -1s aggregated per wave (one LDS atomic per bucket, not per element):
     // sched_sort 64.9 -> 60.4 us (DESIGN.md 5 decision 6)
-    hipLaunchKernelGGL(sched_sort<KeyT>, dim3((B + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, k, cap,
+    const uint32_t bpb = kBlock / 64 * kSortBpw;  // buckets per workgroup
+    hipLaunchKernelGGL(sched_sort<KeyT>, dim3((B + bpb - 1) / bpb), dim3(kBlock), 0, st, k, cap,
                        d->sctl, d->log_bmax_s, d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
     hipLaunchKernelGGL(bucket_emit<KeyT>, dim3((B + kEmitBuckets - 1) / kEmitBuckets), dim3(kBlock), 0, st, k, cap,
-                       d->sctl, d->log_bmax_s, (const int64_t*)d->sbh, (const KeyT*)bk, k, d->set_h, (KeyT*)d->set_k,
-                       (int32_t)sp->lb);
-    const uint32_t gen = ++d->sgen;
-    uint32_t* flag = (uint32_t*)(d->shc + 12);
-    hipLaunchKernelGGL(sched_publish, dim3(1), dim3(kBlock), 0, st, d->sctl, d->vacc,
-                       (const SchedDev*)d->sdev, k, d->shc_dev, (uint32_t*)(d->shc_dev + 12), gen);
+                       d->sctl, d->log_bmax_s, (const int64_t*)d->sbh, (const KeyT*)bk, k, d->set_h, (KeyT*)d->set_k, lb);
+    *gen = ++d->sgen;
+    // the merged set published speculatively with the verdict (size from sctl[2] on the device):
+    // result() takes it if the pass verified and left no tie for the replica to settle
+    *spec = d->spec_dst && n >= d->spec_min;
+    const int64_t per = 32 * 1024;  // bytes per workgroup, as launch_publish_multi
+    const unsigned pgrid =
+        *spec ? (unsigned)std::min<int64_t>(32, std::max<int64_t>(1, (k * (int64_t)kw + per - 1) / per)) : 1u;
+    const uint32_t g = *spec ? ++*d->spec_gen_ctr : 0u;
+    hipLaunchKernelGGL(sched_publish, dim3(pgrid), dim3(1024), 0, st, d->sctl, d->vacc, (const SchedDev*)d->sdev, k,
+                       d->shc_dev, (uint32_t*)(d->shc_dev + 12), *gen, (const uint32_t*)d->set_k,
+                       *spec ? (uint32_t*)d->spec_dst : nullptr, (int32_t)(kw / 4), d->spec_flag, g,
+                       (uint32_t*)(d->ctl + 4));
     STRY(hipGetLastError());
-    // the merged set published speculatively behind the verdict (size from sctl[2] on the device): it
-    // runs while the host turns the verdict around, and result() takes it if the pass verified and
-    // left no tie for the replica to settle
-    bool spec = false;
-    if (d->spec_dst && n >= d->spec_min) {
-        const uint32_t g = ++*d->spec_gen_ctr;
-        const int64_t per = 32 * 1024;  // bytes per workgroup, as launch_publish_multi
-        const unsigned pgrid = (unsigned)std::min<int64_t>(32, std::max<int64_t>(1, (k * (int64_t)kw + per - 1) / per));
-        hipLaunchKernelGGL(publish_set_kernel, dim3(pgrid), dim3(1024), 0, st, (const uint32_t*)d->set_k,
-                           (uint32_t*)d->spec_dst, (const int64_t*)d->sctl, k, (int32_t)(kw / 4), d->spec_flag, g,
-                           (uint32_t*)(d->ctl + 4));
-        STRY(hipGetLastError());
-        d->spec_gen = g;
-        spec = true;
-    }
-    {
-        const auto t0w = std::chrono::steady_clock::now();
-        bool seen = false;
-        for (uint32_t spin = 1;; ++spin) {
-            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == gen) {
-                seen = true;
-                break;
-            }
-            __builtin_ia32_pause();
-            if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0w > std::chrono::milliseconds(50)) break;
+    if (*spec) d->spec_gen = g;
+    return RSV_OK;
+}
+
+// the host side of a pass's verdict: spin on the flag (a stream synchronize after 50 ms)
+static int sched_wait(DistinctState* d, uint32_t gen, hipStream_t st, int64_t* hv) {
+    uint32_t* flag = (uint32_t*)(d->shc + 12);
+    const auto t0w = std::chrono::steady_clock::now();
+    bool seen = false;
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == gen) {
+            seen = true;
+            break;
         }
-        if (!seen) {
-            STRY(hipStreamSynchronize(st));
-            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != gen) STRY(hipErrorUnknown);
-        }
+        __builtin_ia32_pause();
+        if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0w > std::chrono::milliseconds(50)) break;
     }
-    int64_t hv[8];
-    for (int i = 0; i < 8; ++i) hv[i] = __atomic_load_n(d->shc + i, __ATOMIC_RELAXED);
+    if (!seen) {
+        STRY(hipStreamSynchronize(st));
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != gen) STRY(hipErrorUnknown);
+    }
+    for (int i = 0; i < 9; ++i) hv[i] = __atomic_load_n(d->shc + i, __ATOMIC_RELAXED);
+    return RSV_OK;
+}
+
+// The verdict of a pass over n elements from bound t0 whose log starts at log_n: the host fields,
+// or (false *done) the batch left to the chunk loop with the set restored
+template <typename KeyT>
+static int sched_finish(DistinctState* d, const int64_t* hv, int64_t n, int64_t t0, int64_t cap, uint32_t B,
+                        bool spec, hipStream_t st, bool* done) {
+    *done = false;
+    const int64_t k = d->k;
     const int64_t c = hv[0];
     static const bool debug = std::getenv("RSV_SCHED_DEBUG") != nullptr;
     if (debug)
-        std::fprintf(stderr, "[rsv sched] n=%lld ranges=%d cand=%lld pred=%.0f cap=%lld bucket_overflow=%lld "
+        std::fprintf(stderr, "[rsv sched] n=%lld ranges=%lld cand=%lld cap=%lld bucket_overflow=%lld "
                              "failed_range=%lld min_count=%lld k=%lld\n",
-                     (long long)n, nr, (long long)c, c_pred, (long long)cap, (long long)hv[1], (long long)hv[6],
+                     (long long)n, (long long)hv[8], (long long)c, (long long)cap, (long long)hv[1], (long long)hv[6],
                      (long long)hv[7], (long long)k);
     if (c > cap || hv[1]) {  // buffer or bucket overflow: nothing was merged; the counts were not consumed
         STRY(hipMemsetAsync(d->sctl + kCtlWords, 0, (size_t)kCountStride * 4 * B, st));
@@ -2356,7 +2521,7 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
     }
     if (hv[6] >= 0) {  // a predicted bound was too tight: put the set back, the chunk loop redoes the batch
         STRY(hipMemcpyAsync(d->set_h, d->bak_h, (size_t)k * 8, hipMemcpyDeviceToDevice, st));
-        STRY(hipMemcpyAsync(d->set_k, d->bak_k, (size_t)k * kw, hipMemcpyDeviceToDevice, st));
+        STRY(hipMemcpyAsync(d->set_k, d->bak_k, (size_t)k * sizeof(KeyT), hipMemcpyDeviceToDevice, st));
         ++d->sched_fallbacks;
         return RSV_OK;
     }
@@ -2375,8 +2540,79 @@ static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashe
     d->spec_ok = spec && d->m == k && !d->over;  // verified, and no replay will change the set
     *done = true;
     return RSV_OK;
-#undef STRY
 }
+
+// The scheduled pass over keys[0, n) of a batch, heap full (see SchedDev).  Bounds: with D
+// distinct elements seen, the k-th smallest hash sits near fraction k / D of the range; D at
+// position P is predicted as D0 + dfr (P - S0) (D0 from the current bound, dfr the history's
+// distinct fraction, clamped to [0.5, 1]), and range r's bound keeps fraction beta k / D(start)
+// (beta = 1.6: a stream whose new-distinct rate falls to ~60% of its history's still verifies).
+// Ranges grow geometrically (<= kMaxRanges).  *done = false: nothing changed, run the chunk loop.
+template <typename KeyT>
+static int sched_sample(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n, hipStream_t st,
+                        bool* done) {
+    *done = false;
+    const int64_t k = d->k;
+    if (d->m != k || d->max_h == INT64_MIN || n >= ((int64_t)1 << 31) || d->set_cap < k) return RSV_OK;
+    SchedDev plan;
+    const int64_t t0 = d->max_h - 1;
+    const double c_pred = sched_plan_ranges(&plan, (double)d->seen, t0, n, k, d->sched_beta);
+    if (c_pred < 0) return RSV_OK;  // one range: the plain chunk loop does the same work
+    int64_t cap;
+    int32_t lb;
+    if (!sched_sizes(k, c_pred, &cap, &lb)) return RSV_OK;
+    sched_plan_map(&plan, k, lb);
+    plan.off = 0;
+    // the log holds this batch's candidates as one segment
+    if (d->log_n + cap > d->log_limit) {
+        if (cap > d->log_limit) return RSV_OK;
+        if (!d->segs.empty()) STRY(replay_log<KeyT>(d, st));
+        if (d->log_n + cap > d->log_limit) return RSV_OK;
+    }
+    STRY(ensure_log(d, d->log_n + cap, st));
+    STRY(sched_ensure<KeyT>(d, lb, st));
+    hipLaunchKernelGGL(sched_plan_store, dim3(1), dim3(256), 0, st, plan, d->sdev);
+    uint32_t gen;
+    bool spec;
+    if (int rc = sched_launch<KeyT>(d, keys, hashes, n, d->log_n, cap, plan.B, lb, st, &gen, &spec)) return rc;
+    int64_t hv[9];
+    if (int rc = sched_wait(d, gen, st, hv)) return rc;
+    return sched_finish<KeyT>(d, hv, n, t0, cap, plan.B, spec, st, done);
+}
+
+// The heap-filling chunk with the scheduled pass over the rest of the batch behind it, on the
+// device without a host turnaround between them (ctl_plan plans the pass from the chunk's merge).
+// Launches keys[0, m) as a chunk (candidates at log_n, <= ccap of them) and keys[m, n) as a pass
+// (its log right behind the chunk's candidates); waits once, for the pass's verdict; leaves the
+// chunk's control words in hp.  *pass: the plan was valid (the pass ran; its verdict in hv).
+template <typename KeyT>
+static int fused_fill_and_pass(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t m, int64_t n,
+                               int64_t ccap, int64_t cap, int32_t lb, hipStream_t st, int64_t* hp, int64_t* hv,
+                               bool* pass, bool* spec) {
+    int64_t* lh = d->log_h + d->log_n;
+    KeyT* lk = (KeyT*)d->log_k + d->log_n;
+    if (d->timer) d->timer->mark(st);
+    STRY(launch_filter_idx<KeyT>(d, keys, hashes, m, INT64_MAX, lh, lk, d->log_i + d->log_n, ccap, st));
+    if (d->timer) d->timer->mark(st);
+    STRY(launch_bucket_merge<KeyT>(d, INT64_MAX, st, lh, lk, ccap));
+    const uint32_t cgen = ++d->hc_gen;
+    const bool zero = d->sdirty;
+    hipLaunchKernelGGL(ctl_plan, dim3(1), dim3(64), 0, st, d->ctl, d->hc_dev, (uint32_t*)(d->hc_dev + 8), cgen, ccap,
+                       (int64_t)d->k, std::max(1.0, (double)(d->seen + m)), n - m, d->sched_beta, cap, lb, d->sdev,
+                       d->sctl, (int)zero);
+    STRY(hipGetLastError());
+    uint32_t gen;
+    if (int rc = sched_launch<KeyT>(d, keys + m, hashes ? hashes + m : nullptr, n - m, d->log_n, cap, 1u << lb, lb, st,
+                                    &gen, spec, zero))
+        return rc;
+    d->sdirty = false;
+    if (int rc = sched_wait(d, gen, st, hv)) return rc;
+    if (__atomic_load_n((uint32_t*)(d->hc + 8), __ATOMIC_ACQUIRE) != cgen) STRY(hipErrorUnknown);  // stream order
+    for (int i = 0; i < 6; ++i) hp[i] = __atomic_load_n(d->hc + i, __ATOMIC_RELAXED);
+    *pass = hv[8] >= 2;
+    return RSV_OK;
+}
+#undef STRY
 
 // RSV_DISTINCT_ORDERED: the reference's exact RandomValues (strict `elemHash < maxHash` and the
 // scala PriorityQueue's choice among equal hashes, Sampler.scala:394-409), without replaying the
@@ -2411,7 +2647,12 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
     int64_t pos = 0;
     int64_t m_next = 0;  // chunk length after an overflow retry
     bool sched_tried = !d->sched || d->log_bmax < 0;
-    if (!sched_tried && n >= 9 * ccap && n < ((int64_t)1 << 31)) OTRY(sched_prepare<KeyT>(d, n, st));
+    // the heap-filling chunk and the pass behind it in one enqueue (fused_fill_and_pass): its sizes
+    int64_t fcap = 0;
+    int32_t flb = 0;
+    const bool fuse_ok = !sched_tried && n >= 9 * ccap && n < ((int64_t)1 << 31) && d->m < k &&
+                         sched_sizes(k, sched_estimate(d, n), &fcap, &flb);
+    if (!sched_tried && n >= 9 * ccap && n < ((int64_t)1 << 31)) OTRY(sched_prepare<KeyT>(d, n, st, fuse_ok));
     while (pos < n) {
         const bool full = d->m == k;
         if (full && d->max_h == INT64_MIN) break;  // nothing is < Long.MinValue
@@ -2453,14 +2694,30 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
         int64_t* lh = d->log_h + d->log_n;
         KeyT* lk = (KeyT*)d->log_k + d->log_n;
         const bool bucketed = d->log_bmax >= 0 && d->set_cap >= k;
-        // candidate counter and overflow word: zeroed at creation and re-armed by every read_ctl
-        if (d->timer) d->timer->mark(st);
-        OTRY(launch_filter_idx<KeyT>(d, keys + pos, hashes ? hashes + pos : nullptr, m, tinc, lh, lk,
-                                     d->log_i + d->log_n, ccap, st));
-        if (d->timer) d->timer->mark(st);
-        if (bucketed) OTRY(launch_bucket_merge<KeyT>(d, tinc, st, lh, lk, ccap));
         int64_t* hp = d->h_pinned + 4;
-        OTRY(read_ctl(d, hp, st));
+        // the chunk that may fill the heap, with the pass over the rest planned on the device behind
+        // it when the plan's buffers are in place (sched_sample plans on the host: ~18 us of idle GPU
+        // between the chunk's merge and the pass, rocprof timeline r03)
+        bool pass = false, spec = false;
+        int64_t hv[9];
+        if (fuse_ok && !sched_tried && !full && bucketed && !m_next && d->m + m >= k && n - pos - m >= 8 * ccap &&
+            d->log_n + ccap + fcap <= d->log_limit) {
+            sched_tried = true;
+            OTRY(ensure_log(d, d->log_n + ccap + fcap, st));
+            OTRY(sched_ensure<KeyT>(d, flb, st, true));
+            if (int rc = fused_fill_and_pass<KeyT>(d, keys + pos, hashes ? hashes + pos : nullptr, m, n - pos, ccap,
+                                                   fcap, flb, st, hp, hv, &pass, &spec))
+                return rc;
+            if (!pass) sched_tried = false;  // no plan: the chunk loop may still schedule the rest
+        } else {
+            // candidate counter and overflow word: zeroed at creation and re-armed by every read_ctl
+            if (d->timer) d->timer->mark(st);
+            OTRY(launch_filter_idx<KeyT>(d, keys + pos, hashes ? hashes + pos : nullptr, m, tinc, lh, lk,
+                                         d->log_i + d->log_n, ccap, st));
+            if (d->timer) d->timer->mark(st);
+            if (bucketed) OTRY(launch_bucket_merge<KeyT>(d, tinc, st, lh, lk, ccap));
+            OTRY(read_ctl(d, hp, st));
+        }
         const int64_t c = hp[0];
         if (c > ccap) {  // repeats of members (or a degenerate hash) overflowed the buffer: shorter chunk
             m_next = std::max<int64_t>(1, (int64_t)((double)m * ccap / (double)c / 2));
@@ -2491,6 +2748,14 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
         d->log_n += c;
         pos += m;
         d->seen += m;
+        if (pass) {  // the pass's verdict, after the chunk's (its log right behind the chunk's)
+            bool done = false;
+            if (int rc = sched_finish<KeyT>(d, hv, n - pos, d->max_h - 1, fcap, 1u << flb, spec, st, &done)) return rc;
+            if (done) {
+                pos = n;
+                break;
+            }
+        }
     }
     d->seen += n - pos;  // the rest was rejected wholesale (maxHash == Long.MinValue)
     d->exact = d->m < k || !d->over;

@@ -6,6 +6,7 @@
   C2L the reference's Algorithm L (engine java_l) on C2: 1e9 keys, k = 1024 (K1' replay)
   C2I C2 through the boundary as the JVM binding's sampleAll(IndexedSeq): a 1e9-element host
       sequence sampled by index (rsv_sample_indexed), map + keys only for the <= 1024 winners
+  C3K K2 past the LDS winner table (k = 8192, global tables) beside k = 4096 on 4096 x 2^17 keys
   C4M C4's combine on one GPU: 8 shard sets of k = 65536 merged by distributed.merge_local
       (8 x rsv_export_packed + the device rsv_merge_packed), both hashes
 
@@ -89,6 +90,36 @@ def c3(dev):
                                      "8-B loads, ~57 distinct 128-B lines per row): the memory work K2 "
                                      "cannot avoid; frac = floor / K2 launch"},
             "winner_gather_bytes": S * k * 8}
+
+
+def c3_large_k(dev):
+    """K2 past the LDS winner table: k = 8192 (per-wave tables in global memory, the GT form) beside
+    k = 4096 (LDS tables) on the same 4096 streams x 2^17 keys; VALU model of the Philox draws each
+    needs, and the winner gather's floor (k random 8-B loads per stream)."""
+    from reservoir_amd import batch
+
+    S, L = 4096, 1 << 17
+    n = S * L
+    keys = torch.empty(n, dtype=torch.int64, device=dev)
+    splitmix_fill(keys, 3)
+    offs = torch.arange(0, n + 1, L, dtype=torch.int64, device=dev)
+    out = []
+    for k in (4096, 8192):
+        t = timed(lambda: batch.sample_segmented(keys, offs, k, seed=1), reps=7)
+        l0, l1 = R.k2_calls(S, L, k)
+        g = torch.Generator(device=dev)
+        g.manual_seed(k)
+        idx = torch.randint(0, L, (S, k), device=dev, generator=g)
+        rows = keys.view(S, L)
+        t_g = timed(lambda: torch.gather(rows, 1, idx), reps=5)
+        del idx
+        out.append({"config": f"K2 {S} streams x {L} keys, k={k} ({'global' if k > 4416 else 'LDS'} winner tables)",
+                    "elements": n, "seconds": t, "Gelem_s": n / t / 1e9,
+                    "roofline": R.valu_roofline(l0, l1, t, "k2_segmented",
+                                                note="launch time = median of 7 (HIP events); VALU: the Philox "
+                                                     "draws alone"),
+                    "gather_floor": {"seconds": t_g, "frac": t_g / t}})
+    return out
 
 
 def c4(dev, hash_kind="identity", order="auto", twins=False, seed=7):
@@ -265,6 +296,10 @@ def main():
         print(json.dumps(c2l(dev)), flush=True)
     if "c2i" in todo:
         print(json.dumps(c2_indexed(dev)), flush=True)
+    if "c3k" in todo:
+        for r in c3_large_k(dev):
+            print(json.dumps(r), flush=True)
+        torch.cuda.empty_cache()
     if "c4m" in todo:
         for r in c4_merge(dev):
             print(json.dumps(r), flush=True)
