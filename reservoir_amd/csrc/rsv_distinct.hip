@@ -472,8 +472,32 @@ __device__ __forceinline__ T shfl_any(T v, int src) {
 // Bitonic network: strides >= 64 swap between a lane's own slots, smaller ones exchange with lane
 // ^ stride; then the first of each run of equal entries is kept and written back compacted;
 // bucket_distinct[b] = their number.
-template <typename KeyT, int R>
-__device__ __forceinline__ uint32_t wave_sort_bucket(int64_t* gh, KeyT* gk, uint32_t n, uint32_t* out_cnt) {
+// entries (h, key) read in place (bucket_sort, rows_sort) or through a coarse bin's permutation
+// in LDS (set_bin_sort)
+template <typename KeyT>
+struct PairSrc {
+    const int64_t* h;
+    const KeyT* k;
+    __device__ __forceinline__ void load(uint32_t i, int64_t& hh, KeyT& kk) const {
+        hh = h[i];
+        kk = k[i];
+    }
+};
+template <typename KeyT>
+struct LdsPairSrc {
+    const int64_t* h;
+    const KeyT* k;
+    const uint16_t* perm;
+    __device__ __forceinline__ void load(uint32_t i, int64_t& hh, KeyT& kk) const {
+        const uint32_t p = perm[i];
+        hh = h[p];
+        kk = k[p];
+    }
+};
+
+template <typename KeyT, int R, typename Src>
+__device__ __forceinline__ uint32_t wave_sort_bucket(const Src src, int64_t* gh, KeyT* gk, uint32_t n,
+                                                     uint32_t* out_cnt) {
     const uint32_t lane = threadIdx.x & 63;
     constexpr uint32_t N = 64u * R;
     int64_t h[R];
@@ -482,8 +506,7 @@ __device__ __forceinline__ uint32_t wave_sort_bucket(int64_t* gh, KeyT* gk, uint
     for (int r = 0; r < R; ++r) {
         const uint32_t i = r * 64u + lane;
         if (i < n) {
-            h[r] = gh[i];
-            k[r] = gk[i];
+            src.load(i, h[r], k[r]);
         } else {
             h[r] = INT64_MAX;
             k[r] = std::numeric_limits<KeyT>::max();
@@ -557,6 +580,11 @@ __device__ __forceinline__ uint32_t wave_sort_bucket(int64_t* gh, KeyT* gk, uint
     }
     if (lane == 0) *out_cnt = base;
     return base;
+}
+
+template <typename KeyT, int R>
+__device__ __forceinline__ uint32_t wave_sort_bucket(int64_t* gh, KeyT* gk, uint32_t n, uint32_t* out_cnt) {
+    return wave_sort_bucket<KeyT, R>(PairSrc<KeyT>{gh, gk}, gh, gk, n, out_cnt);
 }
 
 template <typename KeyT>
@@ -999,8 +1027,36 @@ __device__ __forceinline__ bool ent_less3(int64_t ha, KeyT ka, uint32_t ia, int6
 // one wave per bucket: sort by (h, key, tag), keep the first of each (h, key) run (its earliest
 // arrival), write them back compacted; each kept element adds +1 / -1 at ranges r_a / r_h + 1 of
 // the block's difference array (sdiff, LDS)
-template <typename KeyT, int R>
-__device__ __forceinline__ uint32_t wave_sort_bucket_tagged(int64_t* gh, KeyT* gk, uint32_t* gi, uint32_t n,
+// a bucket's entries in place in global memory (sched_sort)
+template <typename KeyT>
+struct BucketSrc {
+    const int64_t* h;
+    const KeyT* k;
+    const uint32_t* g;
+    __device__ __forceinline__ void load(uint32_t i, int64_t& hh, KeyT& kk, uint32_t& gg) const {
+        hh = h[i];
+        kk = k[i];
+        gg = g[i];
+    }
+};
+
+// a fine bucket of a coarse bin staged in LDS, through the bin's permutation (sched_bin_sort)
+template <typename KeyT>
+struct LdsBinSrc {
+    const int64_t* h;
+    const KeyT* k;
+    const uint32_t* g;
+    const uint16_t* perm;
+    __device__ __forceinline__ void load(uint32_t i, int64_t& hh, KeyT& kk, uint32_t& gg) const {
+        const uint32_t p = perm[i];
+        hh = h[p];
+        kk = k[p];
+        gg = g[p];
+    }
+};
+
+template <typename KeyT, int R, typename Src>
+__device__ __forceinline__ uint32_t wave_sort_bucket_tagged(const Src src, int64_t* gh, KeyT* gk, uint32_t n,
                                                             const int64_t* sb, const int64_t* stt, int nr,
                                                             int* sdiff) {
     const uint32_t lane = threadIdx.x & 63;
@@ -1012,9 +1068,7 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(int64_t* gh, KeyT* g
     for (int r = 0; r < R; ++r) {
         const uint32_t i = r * 64u + lane;
         if (i < n) {
-            h[r] = gh[i];
-            k[r] = gk[i];
-            g[r] = gi[i];
+            src.load(i, h[r], k[r], g[r]);
         } else {
             h[r] = INT64_MAX;
             k[r] = std::numeric_limits<KeyT>::max();
@@ -1160,9 +1214,12 @@ __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap
         uint32_t* gi = bi + (size_t)b * kBucketCap;
         uint32_t nd = 0;
         if (n > 0)
-            nd = n <= 64    ? wave_sort_bucket_tagged<KeyT, 1>(gh, gk, gi, n, sb, stt, nr, sdiff)
-                 : n <= 128 ? wave_sort_bucket_tagged<KeyT, 2>(gh, gk, gi, n, sb, stt, nr, sdiff)
-                            : wave_sort_bucket_tagged<KeyT, 4>(gh, gk, gi, n, sb, stt, nr, sdiff);
+        {
+            const BucketSrc<KeyT> src{gh, gk, gi};
+            nd = n <= 64    ? wave_sort_bucket_tagged<KeyT, 1>(src, gh, gk, n, sb, stt, nr, sdiff)
+                 : n <= 128 ? wave_sort_bucket_tagged<KeyT, 2>(src, gh, gk, n, sb, stt, nr, sdiff)
+                            : wave_sort_bucket_tagged<KeyT, 4>(src, gh, gk, n, sb, stt, nr, sdiff);
+        }
         if ((threadIdx.x & 63) == 0) {
             *bdist = nd;
             if (nd) atomicAdd(bucket_group(ctl, log_bmax) + (b >> 4), nd);
@@ -1176,6 +1233,351 @@ __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap
     int* acc = vacc + (size_t)(blockIdx.x % kVerifyCopies) * (kMaxRanges + 1);
     for (int i = threadIdx.x; i <= nr; i += blockDim.x)
         if (sdiff[i]) atomicAdd(&acc[i], sdiff[i]);
+}
+
+// ---- the scheduled merge by coarse bins (sched_bin_file -> sched_bin_sort) -------------------
+// The merge's 2^lb fine buckets grouped 2^kBinLog to a coarse bin.  sched_bin_file files every
+// entry into its bin: a workgroup's 4096 entries are counted per bin in LDS, ONE global atomic per
+// (workgroup, bin) reserves their places (~4 entries per atomic at 1024 bins, where sched_file paid
+// one returning atomic per entry on 128-B count lines), and they are stored in runs.  sched_bin_sort
+// then stages one bin in LDS (one workgroup per bin), splits it into its fine buckets by a counting
+// sort there, and sorts / dedups / verifies each fine bucket with the same wave network as
+// sched_sort, reading LDS instead of global memory; the bin's group sums are plain stores and its
+// verification columns one set of atomics per bin.  Bin capacity kBinCap (LDS): ~2.3x the plan's
+// expected fill; more (like a fine bucket over kBucketCap) is the overflow the host falls back on.
+constexpr int kBinLog = 5;
+constexpr uint32_t kBinCap = 3072;
+constexpr int kBinTile = 4;          // entries per thread of sched_bin_file (1024 threads: >= 256 workgroups at C4)
+constexpr int kBinSortThreads = 512;
+
+__host__ __device__ inline uint32_t bin_log(uint32_t lb, uint32_t fl = kBinLog) { return lb > fl ? lb - fl : 0u; }
+
+// the filter path's merges fill a bucket with 64-128 entries on average (bucket_log), the
+// scheduled merge with <= 64: their bins hold 16 fine buckets, not 32
+constexpr int kSetBinLog = 4;
+
+template <typename KeyT>
+__global__ __launch_bounds__(1024) void sched_bin_file(const SchedDev* __restrict__ sd, const int64_t* __restrict__ cand_h,
+                                                       const KeyT* __restrict__ cand_k, const uint32_t* __restrict__ cand_i,
+                                                       int64_t* __restrict__ ctl, int64_t cap,
+                                                       const int64_t* __restrict__ set_h, const KeyT* __restrict__ set_k,
+                                                       int64_t m, int64_t* __restrict__ bh, KeyT* __restrict__ bk,
+                                                       uint32_t* __restrict__ bi, int64_t* __restrict__ bak_h,
+                                                       KeyT* __restrict__ bak_k) {
+    extern __shared__ uint32_t hist[];  // [2^lbin]
+    __shared__ int64_t stt[kMaxRanges];
+    const int nr = sd->nr;
+    if (nr < 2) return;
+    const uint32_t lb = sd->lb, lbin = bin_log(lb), C = 1u << lbin;
+    const int64_t total = m + std::min<int64_t>((int64_t)__hip_atomic_load((const unsigned long long*)ctl,
+                                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                                cap);
+    const int64_t base = (int64_t)blockIdx.x * (1024 * kBinTile);
+    if (base >= total) return;  // whole workgroup
+    const int64_t off = sd->off;
+    cand_h += off;
+    cand_k += off;
+    cand_i += off;
+    for (int i = threadIdx.x; i < nr; i += blockDim.x) stt[i] = sd->t[i];
+    for (uint32_t i = threadIdx.x; i < C; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    const uint32_t B_lo = sd->B_lo;
+    const uint64_t q = sd->lo_mult;
+    const SchedMap map{sd, stt, sd->B, B_lo, (uint32_t)nr, stt[nr - 1], q > UINT64_MAX / B_lo ? UINT64_MAX : q * B_lo};
+    int64_t eh[kBinTile];
+    KeyT ek[kBinTile];
+    uint32_t eg[kBinTile], ebin[kBinTile], eloc[kBinTile];
+#pragma unroll
+    for (int j = 0; j < kBinTile; ++j) {
+        const int64_t t = base + (int64_t)j * 1024 + threadIdx.x;
+        ebin[j] = 0xFFFFFFFFu;
+        if (t < total) {
+            if (t < m) {
+                eh[j] = set_h[t];
+                ek[j] = set_k[t];
+                eg[j] = 0u;
+                bak_h[t] = eh[j];
+                bak_k[t] = ek[j];
+            } else {
+                eh[j] = cand_h[t - m];
+                ek[j] = cand_k[t - m];
+                eg[j] = cand_i[t - m] + 1u;
+            }
+            ebin[j] = map(eh[j]) >> (lb - lbin);
+            eloc[j] = atomicAdd(&hist[ebin[j]], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t* bcnt = bucket_count(ctl);
+    for (uint32_t i = threadIdx.x; i < C; i += blockDim.x) {
+        const uint32_t n = hist[i];
+        if (n) hist[i] = atomicAdd(&bcnt[(size_t)i * kCountStride], n);
+    }
+    __syncthreads();
+    const uint32_t cap_bin = std::min<uint32_t>(kBinCap, (uint32_t)kBucketCap << (lb - lbin));
+    bool over = false;
+#pragma unroll
+    for (int j = 0; j < kBinTile; ++j) {
+        if (ebin[j] == 0xFFFFFFFFu) continue;
+        const uint32_t pos = hist[ebin[j]] + eloc[j];
+        if (pos < cap_bin) {
+            const size_t slot = ((size_t)ebin[j] << (lb - lbin)) * kBucketCap + pos;
+            bh[slot] = eh[j];
+            bk[slot] = ek[j];
+            bi[slot] = eg[j];
+        } else {
+            over = true;
+        }
+    }
+    if (over) ctl[1] = 1;
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(kBinSortThreads) void sched_bin_sort(int64_t cand_cap, int64_t* __restrict__ ctl,
+                                                                  int32_t log_bmax, int64_t* __restrict__ bh,
+                                                                  KeyT* __restrict__ bk, uint32_t* __restrict__ bi,
+                                                                  const SchedDev* __restrict__ sd,
+                                                                  int* __restrict__ vacc) {
+    constexpr uint32_t kF = 1u << kBinLog;
+    __shared__ int64_t lh[kBinCap];
+    __shared__ KeyT lk[kBinCap];
+    __shared__ uint32_t lg[kBinCap];
+    __shared__ uint16_t perm[kBinCap];
+    __shared__ int64_t sb[kMaxRanges + 1], stt[kMaxRanges];
+    __shared__ int sdiff[kMaxRanges + 1];
+    __shared__ uint32_t fcnt[kF], foff[kF], fnd[kF];
+    const int64_t c = ctl[0];
+    const int nr = sd->nr;
+    if (c > cand_cap || ctl[1] || nr < 2) return;  // uniform over the grid (set before this kernel)
+    const uint32_t lb = sd->lb, lbin = bin_log(lb), F = 1u << (lb - lbin);
+    const uint32_t bin = blockIdx.x, fb0 = bin * F;
+    for (int i = threadIdx.x; i <= nr; i += blockDim.x) {
+        sb[i] = sd->b[i];
+        sdiff[i] = 0;
+        if (i < nr) stt[i] = sd->t[i];
+    }
+    if (threadIdx.x < kF) fcnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t B_lo = sd->B_lo;
+    const uint64_t q = sd->lo_mult;
+    const SchedMap map{sd, stt, sd->B, B_lo, (uint32_t)nr, stt[nr - 1], q > UINT64_MAX / B_lo ? UINT64_MAX : q * B_lo};
+    uint32_t* bcnt = bucket_count(ctl) + (size_t)bin * kCountStride;
+    const uint32_t nb = std::min<uint32_t>(*bcnt, kBinCap);  // more: sched_bin_file flagged the overflow
+    const size_t slab = (size_t)fb0 * kBucketCap;
+    constexpr int kPer = kBinCap / kBinSortThreads;
+    uint32_t fj[kPer], fr[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t i = j * kBinSortThreads + threadIdx.x;
+        if (i < nb) {
+            const int64_t h = bh[slab + i];
+            lh[i] = h;
+            lk[i] = bk[slab + i];
+            lg[i] = bi[slab + i];
+            fj[j] = map(h) - fb0;
+            fr[j] = atomicAdd(&fcnt[fj[j]], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the fine counts (F <= 64)
+        const uint32_t lane = threadIdx.x;
+        const uint32_t v = lane < F ? fcnt[lane] : 0u;
+        uint32_t x = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(x, d);
+            if ((int)lane >= d) x += o;
+        }
+        if (lane < F) foff[lane] = x - v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t i = j * kBinSortThreads + threadIdx.x;
+        if (i < nb) perm[foff[fj[j]] + fr[j]] = (uint16_t)i;
+    }
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* bdist = bucket_distinct(ctl, log_bmax);
+    for (uint32_t f = wave; f < F; f += kBinSortThreads / 64) {
+        const uint32_t n = fcnt[f], b = fb0 + f;
+        uint32_t nd = 0;
+        if (n > kBucketCap) {
+            if (lane == 0) ctl[1] = 1;  // the verdict reports the overflow; emit skips
+        } else if (n > 0) {
+            const LdsBinSrc<KeyT> src{lh, lk, lg, perm + foff[f]};
+            int64_t* gh = bh + (size_t)b * kBucketCap;
+            KeyT* gk = bk + (size_t)b * kBucketCap;
+            nd = n <= 64    ? wave_sort_bucket_tagged<KeyT, 1>(src, gh, gk, n, sb, stt, nr, sdiff)
+                 : n <= 128 ? wave_sort_bucket_tagged<KeyT, 2>(src, gh, gk, n, sb, stt, nr, sdiff)
+                            : wave_sort_bucket_tagged<KeyT, 4>(src, gh, gk, n, sb, stt, nr, sdiff);
+        }
+        if (lane == 0) {
+            bdist[b] = nd;
+            fnd[f] = nd;
+        }
+    }
+    __syncthreads();
+    uint32_t* gsum = bucket_group(ctl, log_bmax);
+    for (uint32_t g = threadIdx.x; g < (F + 15) / 16; g += blockDim.x) {
+        uint32_t v = 0;
+        for (uint32_t f = g * 16; f < std::min(F, g * 16 + 16); ++f) v += fnd[f];
+        gsum[(fb0 >> 4) + g] = v;
+    }
+    int* acc = vacc + (size_t)(bin % kVerifyCopies) * (kMaxRanges + 1);
+    for (int i = threadIdx.x; i <= nr; i += blockDim.x)
+        if (sdiff[i]) atomicAdd(&acc[i], sdiff[i]);
+    if (threadIdx.x == 0) *bcnt = 0;
+}
+
+// The filter path's bucketed merge (set mode, ordered chunks) by coarse bins, as the scheduled
+// merge above: set_bin_file replaces bucket_scatter's returning atomic per entry, set_bin_sort stages
+// a bin in LDS and runs bucket_sort's wave network on its fine buckets.  The bucket count is read
+// on the device (bucket_log of the merge's size), so both grids are sized for the largest.
+template <typename KeyT>
+__global__ __launch_bounds__(1024) void set_bin_file(const int64_t* __restrict__ set_h, const KeyT* __restrict__ set_k,
+                                                     int64_t m, const int64_t* __restrict__ cand_h,
+                                                     const KeyT* __restrict__ cand_k, int64_t cand_cap,
+                                                     int64_t* __restrict__ ctl, uint64_t q, int32_t log_bmax,
+                                                     int64_t* __restrict__ bh, KeyT* __restrict__ bk) {
+    extern __shared__ uint32_t hist[];  // [2^bin_log(lb)]
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) ctl[5] = 0;  // bucket_emit sets it
+        zero_bucket_groups(ctl, log_bmax);
+    }
+    const int64_t c = ctl[0];
+    if (c > cand_cap) return;  // the filter overflowed its buffer: the host tightens and reruns
+    const int64_t total = m + c;
+    const int64_t base = (int64_t)blockIdx.x * (1024 * kBinTile);
+    if (base >= total) return;
+    const uint32_t lb = bucket_log(total, log_bmax), lbin = bin_log(lb, kSetBinLog), C = 1u << lbin;
+    const BucketMap map(q, lb);
+    for (uint32_t i = threadIdx.x; i < C; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    int64_t eh[kBinTile];
+    KeyT ek[kBinTile];
+    uint32_t ebin[kBinTile], eloc[kBinTile];
+#pragma unroll
+    for (int j = 0; j < kBinTile; ++j) {
+        const int64_t t = base + (int64_t)j * 1024 + threadIdx.x;
+        ebin[j] = 0xFFFFFFFFu;
+        if (t < total) {
+            if (t < m) {
+                eh[j] = set_h[t];
+                ek[j] = set_k[t];
+            } else {
+                eh[j] = cand_h[t - m];
+                ek[j] = cand_k[t - m];
+            }
+            ebin[j] = map(eh[j]) >> (lb - lbin);
+            eloc[j] = atomicAdd(&hist[ebin[j]], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t* bcnt = bucket_count(ctl);
+    for (uint32_t i = threadIdx.x; i < C; i += blockDim.x) {
+        const uint32_t n = hist[i];
+        if (n) hist[i] = atomicAdd(&bcnt[(size_t)i * kCountStride], n);
+    }
+    __syncthreads();
+    const uint32_t cap_bin = std::min<uint32_t>(kBinCap, (uint32_t)kBucketCap << (lb - lbin));
+    bool over = false;
+#pragma unroll
+    for (int j = 0; j < kBinTile; ++j) {
+        if (ebin[j] == 0xFFFFFFFFu) continue;
+        const uint32_t pos = hist[ebin[j]] + eloc[j];
+        if (pos < cap_bin) {
+            const size_t slot = ((size_t)ebin[j] << (lb - lbin)) * kBucketCap + pos;
+            bh[slot] = eh[j];
+            bk[slot] = ek[j];
+        } else {
+            over = true;
+        }
+    }
+    if (over) ctl[1] = 1;
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(kBinSortThreads) void set_bin_sort(int64_t m, int64_t cand_cap, int64_t* __restrict__ ctl,
+                                                                int32_t log_bmax, uint64_t q, int64_t* __restrict__ bh,
+                                                                KeyT* __restrict__ bk) {
+    constexpr uint32_t kF = 1u << kBinLog;
+    __shared__ int64_t lh[kBinCap];
+    __shared__ KeyT lk[kBinCap];
+    __shared__ uint16_t perm[kBinCap];
+    __shared__ uint32_t fcnt[kF], foff[kF], fnd[kF];
+    const int64_t c = ctl[0];
+    if (c > cand_cap || ctl[1]) return;
+    const uint32_t lb = bucket_log(m + c, log_bmax), lbin = bin_log(lb, kSetBinLog), F = 1u << (lb - lbin);
+    const uint32_t bin = blockIdx.x;
+    if (bin >= (1u << lbin)) return;
+    const uint32_t fb0 = bin * F;
+    const BucketMap map(q, lb);
+    if (threadIdx.x < kF) fcnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t* bcnt = bucket_count(ctl) + (size_t)bin * kCountStride;
+    const uint32_t nb = std::min<uint32_t>(*bcnt, kBinCap);
+    const size_t slab = (size_t)fb0 * kBucketCap;
+    constexpr int kPer = kBinCap / kBinSortThreads;
+    uint32_t fj[kPer], fr[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t i = j * kBinSortThreads + threadIdx.x;
+        if (i < nb) {
+            const int64_t h = bh[slab + i];
+            lh[i] = h;
+            lk[i] = bk[slab + i];
+            fj[j] = map(h) - fb0;
+            fr[j] = atomicAdd(&fcnt[fj[j]], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x;
+        const uint32_t v = lane < F ? fcnt[lane] : 0u;
+        uint32_t x = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(x, d);
+            if ((int)lane >= d) x += o;
+        }
+        if (lane < F) foff[lane] = x - v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t i = j * kBinSortThreads + threadIdx.x;
+        if (i < nb) perm[foff[fj[j]] + fr[j]] = (uint16_t)i;
+    }
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* bdist = bucket_distinct(ctl, log_bmax);
+    for (uint32_t f = wave; f < F; f += kBinSortThreads / 64) {
+        const uint32_t n = fcnt[f], b = fb0 + f;
+        uint32_t nd = 0;
+        if (n > kBucketCap) {
+            if (lane == 0) {
+                ctl[1] = 1;
+                bdist[b] = 0;
+            }
+        } else if (n > 0) {
+            const LdsPairSrc<KeyT> src{lh, lk, perm + foff[f]};
+            int64_t* gh = bh + (size_t)b * kBucketCap;
+            KeyT* gk = bk + (size_t)b * kBucketCap;
+            nd = n <= 64    ? wave_sort_bucket<KeyT, 1>(src, gh, gk, n, bdist + b)
+                 : n <= 128 ? wave_sort_bucket<KeyT, 2>(src, gh, gk, n, bdist + b)
+                            : wave_sort_bucket<KeyT, 4>(src, gh, gk, n, bdist + b);
+        } else if (lane == 0) {
+            bdist[b] = 0;
+        }
+        if (lane == 0) fnd[f] = nd;
+    }
+    __syncthreads();
+    uint32_t* gsum = bucket_group(ctl, log_bmax);
+    for (uint32_t g = threadIdx.x; g < (F + 15) / 16; g += blockDim.x) {
+        uint32_t v = 0;
+        for (uint32_t f = g * 16; f < std::min(F, g * 16 + 16); ++f) v += fnd[f];
+        gsum[(fb0 >> 4) + g] = v;
+    }
+    if (threadIdx.x == 0) *bcnt = 0;
 }
 
 // ctl[0..5], the verification verdict (first range r >= 1 short of k elements, or -1) and the
@@ -1969,10 +2371,21 @@ static hipError_t launch_bucket_merge(DistinctState* d, int64_t tinc, hipStream_
     const unsigned wgrid = (waves + kBlock / 64 - 1) / (kBlock / 64);
     const unsigned sgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(d->m + cand_cap), 1), 1024);
     KeyT* bk = (KeyT*)d->bk;
+#ifdef RSV_SCHED_FINE  // dev A/B: per-entry scatter, one wave per bucket from global memory
     hipLaunchKernelGGL(bucket_scatter<KeyT>, dim3(sgrid), dim3(kBlock), 0, st, d->set_h, (const KeyT*)d->set_k, d->m,
                        cand_h, cand_k, cand_cap, d->ctl, q, d->log_bmax, d->bh, bk);
     hipLaunchKernelGGL(bucket_sort<KeyT>, dim3(wgrid), dim3(kBlock), 0, st, d->m, cand_cap, d->ctl, d->log_bmax,
                        d->bh, bk);
+#else
+    (void)sgrid;
+    (void)wgrid;
+    const uint32_t cmax = 1u << bin_log((uint32_t)d->log_bmax, kSetBinLog);  // bins at the largest bucket count
+    const unsigned fgrid = (unsigned)std::max<int64_t>(1, (d->m + cand_cap + 1024 * kBinTile - 1) / (1024 * kBinTile));
+    hipLaunchKernelGGL(set_bin_file<KeyT>, dim3(fgrid), dim3(1024), cmax * 4, st, d->set_h, (const KeyT*)d->set_k,
+                       d->m, cand_h, cand_k, cand_cap, d->ctl, q, d->log_bmax, d->bh, bk);
+    hipLaunchKernelGGL(set_bin_sort<KeyT>, dim3(cmax), dim3(kBinSortThreads), 0, st, d->m, cand_cap, d->ctl,
+                       d->log_bmax, q, d->bh, bk);
+#endif
     const unsigned egrid = (waves + kEmitBuckets - 1) / kEmitBuckets;
     hipLaunchKernelGGL(bucket_emit<KeyT>, dim3(egrid), dim3(kBlock), 0, st, d->m, cand_cap, d->ctl, d->log_bmax,
                        (const int64_t*)d->bh, (const KeyT*)bk, (int64_t)d->k, d->set_h, (KeyT*)d->set_k);
@@ -2447,19 +2860,33 @@ static int sched_launch(DistinctState* d, const KeyT* keys, const int64_t* hashe
         // one entry per thread (the count is on the device: sized for the buffer's capacity, idle
         // threads exit): every bucket atomic in flight at once -- a 1024-workgroup grid-stride over
         // ~1.1 M entries waited on ~4 atomics per thread in sequence (61 us)
+#ifdef RSV_SCHED_FINE  // dev A/B: the per-entry filing and one wave per fine bucket from global memory
         const unsigned fgrid = (unsigned)std::min<int64_t>((k + cap + kBlock - 1) / kBlock, 16384);
         hipLaunchKernelGGL(sched_file<KeyT>, dim3(fgrid), dim3(kBlock), 0, st, (const SchedDev*)d->sdev,
                            (const int64_t*)(d->log_h + lbase), (const KeyT*)lk, (const uint32_t*)(d->log_i + lbase),
                            d->sctl, cap, (const int64_t*)d->set_h, (const KeyT*)d->set_k, k, d->sbh, bk, d->sbi,
                            d->bak_h, (KeyT*)d->bak_k);
+#else
+        const uint32_t C = 1u << bin_log((uint32_t)lb);
+        const unsigned fgrid = (unsigned)((k + cap + 1024 * kBinTile - 1) / (1024 * kBinTile));
+        hipLaunchKernelGGL(sched_bin_file<KeyT>, dim3(fgrid), dim3(1024), C * 4, st, (const SchedDev*)d->sdev,
+                           (const int64_t*)(d->log_h + lbase), (const KeyT*)lk, (const uint32_t*)(d->log_i + lbase),
+                           d->sctl, cap, (const int64_t*)d->set_h, (const KeyT*)d->set_k, k, d->sbh, bk, d->sbi,
+                           d->bak_h, (KeyT*)d->bak_k);
+#endif
         STRY(hipGetLastError());
     }
     if (d->timer) d->timer->mark(st);
+#ifdef RSV_SCHED_FINE
     // the difference array's -1s aggregated per wave (one LDS atomic per bucket, not per element):
     // sched_sort 64.9 -> 60.4 us (DESIGN.md 5 decision 6)
     const uint32_t bpb = kBlock / 64 * kSortBpw;  // buckets per workgroup
     hipLaunchKernelGGL(sched_sort<KeyT>, dim3((B + bpb - 1) / bpb), dim3(kBlock), 0, st, k, cap,
                        d->sctl, d->log_bmax_s, d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
+#else
+    hipLaunchKernelGGL(sched_bin_sort<KeyT>, dim3(1u << bin_log((uint32_t)lb)), dim3(kBinSortThreads), 0, st, cap, d->sctl, d->log_bmax_s,
+                       d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
+#endif
     hipLaunchKernelGGL(bucket_emit<KeyT>, dim3((B + kEmitBuckets - 1) / kEmitBuckets), dim3(kBlock), 0, st, k, cap,
                        d->sctl, d->log_bmax_s, (const int64_t*)d->sbh, (const KeyT*)bk, k, d->set_h, (KeyT*)d->set_k, lb);
     *gen = ++d->sgen;
