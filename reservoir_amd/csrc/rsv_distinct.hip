@@ -472,8 +472,64 @@ __device__ __forceinline__ T shfl_any(T v, int src) {
 // Bitonic network: strides >= 64 swap between a lane's own slots, smaller ones exchange with lane
 // ^ stride; then the first of each run of equal entries is kept and written back compacted;
 // bucket_distinct[b] = their number.
-// entries (h, key) read in place (bucket_sort, rows_sort) or through a coarse bin's permutation
-// in LDS (set_bin_sort)
+// The one-register bucket (n <= 64) sorted on ONE 64-bit word per lane: (h - min h) << 6 | lane,
+// when the bucket's hashes span < 2^58 (a merge bucket covers a narrow slice of the hash range:
+// always, in practice; else the caller runs the full network).  The 21 compare-exchange stages then
+// move 2 words instead of 5 (h, key, tag) and compare once; the entries are re-read by their slot
+// after it, and runs of equal h (duplicates, colliding hashes) are put in (key, tag) order by an
+// odd-even transposition restricted to the run.  In: this lane's entry (lane < n; others MAX).
+template <typename KeyT, bool TAGGED, typename Load>
+__device__ __forceinline__ bool wave_packed_sort(const Load& load, uint32_t n, int64_t& h, KeyT& k, uint32_t& g) {
+    const uint32_t lane = threadIdx.x & 63;
+    const bool valid = lane < n;
+    const uint64_t u = (uint64_t)h ^ 0x8000000000000000ull;
+    uint64_t lo = valid ? u : ~0ull;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = shfl_xor_any(lo, d);
+        lo = o < lo ? o : lo;
+    }
+    if (__ballot(valid && ((u - lo) >> 58) != 0)) return false;
+    uint64_t key = valid ? ((u - lo) << 6) | lane : ~0ull;
+#pragma unroll
+    for (uint32_t size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            const uint64_t o = shfl_xor_any(key, (int)stride);
+            const bool lower = (lane & stride) == 0;
+            const bool up = (lane & size) == 0;
+            const bool take = (lower == up) ? (o < key) : (key < o);
+            key = take ? o : key;
+        }
+    }
+    if (valid) load((uint32_t)key & 63u, h, k, g);
+    for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            int partner = p == 0 ? (int)(lane ^ 1u) : ((lane & 1u) ? (int)lane + 1 : (int)lane - 1);
+            if (partner < 0 || partner > 63) partner = (int)lane;
+            const int64_t oh = shfl_any(h, partner);
+            const KeyT ok = shfl_any(k, partner);
+            const uint32_t og = TAGGED ? (uint32_t)__shfl((int)g, partner) : 0u;
+            bool sw = false;
+            if (valid && (uint32_t)partner < n && partner != (int)lane && oh == h) {
+                const bool other_less = ok < k || (TAGGED && ok == k && og < g);
+                const bool mine_less = k < ok || (TAGGED && k == ok && g < og);
+                sw = (int)lane < partner ? other_less : mine_less;
+            }
+            if (sw) {
+                k = ok;
+                g = og;
+            }
+            any |= sw;
+        }
+        if (!__ballot(any)) break;
+    }
+    return true;
+}
+
+// entries (h, key) read in place (bucket_sort, rows_sort)
 template <typename KeyT>
 struct PairSrc {
     const int64_t* h;
@@ -481,17 +537,6 @@ struct PairSrc {
     __device__ __forceinline__ void load(uint32_t i, int64_t& hh, KeyT& kk) const {
         hh = h[i];
         kk = k[i];
-    }
-};
-template <typename KeyT>
-struct LdsPairSrc {
-    const int64_t* h;
-    const KeyT* k;
-    const uint16_t* perm;
-    __device__ __forceinline__ void load(uint32_t i, int64_t& hh, KeyT& kk) const {
-        const uint32_t p = perm[i];
-        hh = h[p];
-        kk = k[p];
     }
 };
 
@@ -512,6 +557,13 @@ __device__ __forceinline__ uint32_t wave_sort_bucket(const Src src, int64_t* gh,
             k[r] = std::numeric_limits<KeyT>::max();
         }
     }
+    bool packed = false;
+    if constexpr (R == 1) {
+        uint32_t g0 = 0;
+        packed = wave_packed_sort<KeyT, false>(
+            [&](uint32_t i, int64_t& hh, KeyT& kk, uint32_t&) { src.load(i, hh, kk); }, n, h[0], k[0], g0);
+    }
+    if (!packed) {
 #pragma unroll
     for (uint32_t size = 2; size <= N; size <<= 1) {
 #pragma unroll
@@ -554,6 +606,7 @@ __device__ __forceinline__ uint32_t wave_sort_bucket(const Src src, int64_t* gh,
             }
         }
     }
+    }  // !packed
     // distinct: entry i differs from entry i - 1
     uint32_t base = 0;
     int64_t prev_h_last = 0;
@@ -1075,6 +1128,11 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(const Src src, int64
             g[r] = 0xFFFFFFFFu;
         }
     }
+    bool packed = false;
+    if constexpr (R == 1)
+        packed = wave_packed_sort<KeyT, true>(
+            [&](uint32_t i, int64_t& hh, KeyT& kk, uint32_t& gg) { src.load(i, hh, kk, gg); }, n, h[0], k[0], g[0]);
+    if (!packed) {
 #pragma unroll
     for (uint32_t size = 2; size <= N; size <<= 1) {
 #pragma unroll
@@ -1120,6 +1178,7 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(const Src src, int64
             }
         }
     }
+    }  // !packed
     uint32_t base = 0;
     int64_t prev_h_last = 0;
     KeyT prev_k_last = 0;
@@ -1182,12 +1241,8 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(const Src src, int64
     return base;
 }
 
-// buckets per wave of sched_sort (dev builds vary it: make exp EXP=-DRSV_SORT_BPW=4)
-#ifndef RSV_SORT_BPW
-#define RSV_SORT_BPW 1
-#endif
-constexpr uint32_t kSortBpw = RSV_SORT_BPW;
-
+// (dev builds only, -DRSV_SCHED_FINE: sched_file + sched_sort, the round-3 form of the scheduled
+// merge -- one returning atomic per entry, one wave per fine bucket from global memory)
 template <typename KeyT>
 __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap, int64_t* __restrict__ ctl,
                                                      int32_t log_bmax, int64_t* __restrict__ bh, KeyT* __restrict__ bk,
@@ -1204,8 +1259,8 @@ __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap
         if (i < nr) stt[i] = sd->t[i];
     }
     __syncthreads();
-    const uint32_t b0 = (blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * kSortBpw;
-    for (uint32_t b = b0; b < b0 + kSortBpw && b < sd->B; ++b) {
+    const uint32_t b = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (b < sd->B) {
         uint32_t* bcnt = bucket_count(ctl) + (size_t)b * kCountStride;
         uint32_t* bdist = bucket_distinct(ctl, log_bmax) + b;
         const uint32_t n = *bcnt;
@@ -1227,9 +1282,6 @@ __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap
         }
     }
     __syncthreads();
-#ifdef RSV_EXP_NO_VACC  // dev A/B only: the verdict fails, every pass falls back (kernel times are the point)
-    return;
-#endif
     int* acc = vacc + (size_t)(blockIdx.x % kVerifyCopies) * (kMaxRanges + 1);
     for (int i = threadIdx.x; i <= nr; i += blockDim.x)
         if (sdiff[i]) atomicAdd(&acc[i], sdiff[i]);
@@ -1252,9 +1304,7 @@ constexpr int kBinSortThreads = 512;
 
 __host__ __device__ inline uint32_t bin_log(uint32_t lb, uint32_t fl = kBinLog) { return lb > fl ? lb - fl : 0u; }
 
-// the filter path's merges fill a bucket with 64-128 entries on average (bucket_log), the
-// scheduled merge with <= 64: their bins hold 16 fine buckets, not 32
-constexpr int kSetBinLog = 4;
+
 
 template <typename KeyT>
 __global__ __launch_bounds__(1024) void sched_bin_file(const SchedDev* __restrict__ sd, const int64_t* __restrict__ cand_h,
@@ -1426,157 +1476,6 @@ __global__ __launch_bounds__(kBinSortThreads) void sched_bin_sort(int64_t cand_c
     int* acc = vacc + (size_t)(bin % kVerifyCopies) * (kMaxRanges + 1);
     for (int i = threadIdx.x; i <= nr; i += blockDim.x)
         if (sdiff[i]) atomicAdd(&acc[i], sdiff[i]);
-    if (threadIdx.x == 0) *bcnt = 0;
-}
-
-// The filter path's bucketed merge (set mode, ordered chunks) by coarse bins, as the scheduled
-// merge above: set_bin_file replaces bucket_scatter's returning atomic per entry, set_bin_sort stages
-// a bin in LDS and runs bucket_sort's wave network on its fine buckets.  The bucket count is read
-// on the device (bucket_log of the merge's size), so both grids are sized for the largest.
-template <typename KeyT>
-__global__ __launch_bounds__(1024) void set_bin_file(const int64_t* __restrict__ set_h, const KeyT* __restrict__ set_k,
-                                                     int64_t m, const int64_t* __restrict__ cand_h,
-                                                     const KeyT* __restrict__ cand_k, int64_t cand_cap,
-                                                     int64_t* __restrict__ ctl, uint64_t q, int32_t log_bmax,
-                                                     int64_t* __restrict__ bh, KeyT* __restrict__ bk) {
-    extern __shared__ uint32_t hist[];  // [2^bin_log(lb)]
-    if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) ctl[5] = 0;  // bucket_emit sets it
-        zero_bucket_groups(ctl, log_bmax);
-    }
-    const int64_t c = ctl[0];
-    if (c > cand_cap) return;  // the filter overflowed its buffer: the host tightens and reruns
-    const int64_t total = m + c;
-    const int64_t base = (int64_t)blockIdx.x * (1024 * kBinTile);
-    if (base >= total) return;
-    const uint32_t lb = bucket_log(total, log_bmax), lbin = bin_log(lb, kSetBinLog), C = 1u << lbin;
-    const BucketMap map(q, lb);
-    for (uint32_t i = threadIdx.x; i < C; i += blockDim.x) hist[i] = 0;
-    __syncthreads();
-    int64_t eh[kBinTile];
-    KeyT ek[kBinTile];
-    uint32_t ebin[kBinTile], eloc[kBinTile];
-#pragma unroll
-    for (int j = 0; j < kBinTile; ++j) {
-        const int64_t t = base + (int64_t)j * 1024 + threadIdx.x;
-        ebin[j] = 0xFFFFFFFFu;
-        if (t < total) {
-            if (t < m) {
-                eh[j] = set_h[t];
-                ek[j] = set_k[t];
-            } else {
-                eh[j] = cand_h[t - m];
-                ek[j] = cand_k[t - m];
-            }
-            ebin[j] = map(eh[j]) >> (lb - lbin);
-            eloc[j] = atomicAdd(&hist[ebin[j]], 1u);
-        }
-    }
-    __syncthreads();
-    uint32_t* bcnt = bucket_count(ctl);
-    for (uint32_t i = threadIdx.x; i < C; i += blockDim.x) {
-        const uint32_t n = hist[i];
-        if (n) hist[i] = atomicAdd(&bcnt[(size_t)i * kCountStride], n);
-    }
-    __syncthreads();
-    const uint32_t cap_bin = std::min<uint32_t>(kBinCap, (uint32_t)kBucketCap << (lb - lbin));
-    bool over = false;
-#pragma unroll
-    for (int j = 0; j < kBinTile; ++j) {
-        if (ebin[j] == 0xFFFFFFFFu) continue;
-        const uint32_t pos = hist[ebin[j]] + eloc[j];
-        if (pos < cap_bin) {
-            const size_t slot = ((size_t)ebin[j] << (lb - lbin)) * kBucketCap + pos;
-            bh[slot] = eh[j];
-            bk[slot] = ek[j];
-        } else {
-            over = true;
-        }
-    }
-    if (over) ctl[1] = 1;
-}
-
-template <typename KeyT>
-__global__ __launch_bounds__(kBinSortThreads) void set_bin_sort(int64_t m, int64_t cand_cap, int64_t* __restrict__ ctl,
-                                                                int32_t log_bmax, uint64_t q, int64_t* __restrict__ bh,
-                                                                KeyT* __restrict__ bk) {
-    constexpr uint32_t kF = 1u << kBinLog;
-    __shared__ int64_t lh[kBinCap];
-    __shared__ KeyT lk[kBinCap];
-    __shared__ uint16_t perm[kBinCap];
-    __shared__ uint32_t fcnt[kF], foff[kF], fnd[kF];
-    const int64_t c = ctl[0];
-    if (c > cand_cap || ctl[1]) return;
-    const uint32_t lb = bucket_log(m + c, log_bmax), lbin = bin_log(lb, kSetBinLog), F = 1u << (lb - lbin);
-    const uint32_t bin = blockIdx.x;
-    if (bin >= (1u << lbin)) return;
-    const uint32_t fb0 = bin * F;
-    const BucketMap map(q, lb);
-    if (threadIdx.x < kF) fcnt[threadIdx.x] = 0;
-    __syncthreads();
-    uint32_t* bcnt = bucket_count(ctl) + (size_t)bin * kCountStride;
-    const uint32_t nb = std::min<uint32_t>(*bcnt, kBinCap);
-    const size_t slab = (size_t)fb0 * kBucketCap;
-    constexpr int kPer = kBinCap / kBinSortThreads;
-    uint32_t fj[kPer], fr[kPer];
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const uint32_t i = j * kBinSortThreads + threadIdx.x;
-        if (i < nb) {
-            const int64_t h = bh[slab + i];
-            lh[i] = h;
-            lk[i] = bk[slab + i];
-            fj[j] = map(h) - fb0;
-            fr[j] = atomicAdd(&fcnt[fj[j]], 1u);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        const uint32_t lane = threadIdx.x;
-        const uint32_t v = lane < F ? fcnt[lane] : 0u;
-        uint32_t x = v;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(x, d);
-            if ((int)lane >= d) x += o;
-        }
-        if (lane < F) foff[lane] = x - v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const uint32_t i = j * kBinSortThreads + threadIdx.x;
-        if (i < nb) perm[foff[fj[j]] + fr[j]] = (uint16_t)i;
-    }
-    __syncthreads();
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint32_t* bdist = bucket_distinct(ctl, log_bmax);
-    for (uint32_t f = wave; f < F; f += kBinSortThreads / 64) {
-        const uint32_t n = fcnt[f], b = fb0 + f;
-        uint32_t nd = 0;
-        if (n > kBucketCap) {
-            if (lane == 0) {
-                ctl[1] = 1;
-                bdist[b] = 0;
-            }
-        } else if (n > 0) {
-            const LdsPairSrc<KeyT> src{lh, lk, perm + foff[f]};
-            int64_t* gh = bh + (size_t)b * kBucketCap;
-            KeyT* gk = bk + (size_t)b * kBucketCap;
-            nd = n <= 64    ? wave_sort_bucket<KeyT, 1>(src, gh, gk, n, bdist + b)
-                 : n <= 128 ? wave_sort_bucket<KeyT, 2>(src, gh, gk, n, bdist + b)
-                            : wave_sort_bucket<KeyT, 4>(src, gh, gk, n, bdist + b);
-        } else if (lane == 0) {
-            bdist[b] = 0;
-        }
-        if (lane == 0) fnd[f] = nd;
-    }
-    __syncthreads();
-    uint32_t* gsum = bucket_group(ctl, log_bmax);
-    for (uint32_t g = threadIdx.x; g < (F + 15) / 16; g += blockDim.x) {
-        uint32_t v = 0;
-        for (uint32_t f = g * 16; f < std::min(F, g * 16 + 16); ++f) v += fnd[f];
-        gsum[(fb0 >> 4) + g] = v;
-    }
     if (threadIdx.x == 0) *bcnt = 0;
 }
 
@@ -2371,21 +2270,10 @@ static hipError_t launch_bucket_merge(DistinctState* d, int64_t tinc, hipStream_
     const unsigned wgrid = (waves + kBlock / 64 - 1) / (kBlock / 64);
     const unsigned sgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(d->m + cand_cap), 1), 1024);
     KeyT* bk = (KeyT*)d->bk;
-#ifdef RSV_SCHED_FINE  // dev A/B: per-entry scatter, one wave per bucket from global memory
     hipLaunchKernelGGL(bucket_scatter<KeyT>, dim3(sgrid), dim3(kBlock), 0, st, d->set_h, (const KeyT*)d->set_k, d->m,
                        cand_h, cand_k, cand_cap, d->ctl, q, d->log_bmax, d->bh, bk);
     hipLaunchKernelGGL(bucket_sort<KeyT>, dim3(wgrid), dim3(kBlock), 0, st, d->m, cand_cap, d->ctl, d->log_bmax,
                        d->bh, bk);
-#else
-    (void)sgrid;
-    (void)wgrid;
-    const uint32_t cmax = 1u << bin_log((uint32_t)d->log_bmax, kSetBinLog);  // bins at the largest bucket count
-    const unsigned fgrid = (unsigned)std::max<int64_t>(1, (d->m + cand_cap + 1024 * kBinTile - 1) / (1024 * kBinTile));
-    hipLaunchKernelGGL(set_bin_file<KeyT>, dim3(fgrid), dim3(1024), cmax * 4, st, d->set_h, (const KeyT*)d->set_k,
-                       d->m, cand_h, cand_k, cand_cap, d->ctl, q, d->log_bmax, d->bh, bk);
-    hipLaunchKernelGGL(set_bin_sort<KeyT>, dim3(cmax), dim3(kBinSortThreads), 0, st, d->m, cand_cap, d->ctl,
-                       d->log_bmax, q, d->bh, bk);
-#endif
     const unsigned egrid = (waves + kEmitBuckets - 1) / kEmitBuckets;
     hipLaunchKernelGGL(bucket_emit<KeyT>, dim3(egrid), dim3(kBlock), 0, st, d->m, cand_cap, d->ctl, d->log_bmax,
                        (const int64_t*)d->bh, (const KeyT*)bk, (int64_t)d->k, d->set_h, (KeyT*)d->set_k);
@@ -2880,8 +2768,7 @@ static int sched_launch(DistinctState* d, const KeyT* keys, const int64_t* hashe
 #ifdef RSV_SCHED_FINE
     // the difference array's -1s aggregated per wave (one LDS atomic per bucket, not per element):
     // sched_sort 64.9 -> 60.4 us (DESIGN.md 5 decision 6)
-    const uint32_t bpb = kBlock / 64 * kSortBpw;  // buckets per workgroup
-    hipLaunchKernelGGL(sched_sort<KeyT>, dim3((B + bpb - 1) / bpb), dim3(kBlock), 0, st, k, cap,
+    hipLaunchKernelGGL(sched_sort<KeyT>, dim3((B + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, k, cap,
                        d->sctl, d->log_bmax_s, d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
 #else
     hipLaunchKernelGGL(sched_bin_sort<KeyT>, dim3(1u << bin_log((uint32_t)lb)), dim3(kBinSortThreads), 0, st, cap, d->sctl, d->log_bmax_s,
