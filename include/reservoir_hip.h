@@ -153,6 +153,14 @@ rsv_status rsv_fill_slots(rsv_sampler* s, const void* keys_host);
 rsv_status rsv_result(rsv_sampler* s, void* out, int64_t cap, int64_t* out_n);
 /* Same, into device memory (no host round trip of the keys). */
 rsv_status rsv_result_device(rsv_sampler* s, void* out_dev, int64_t cap, int64_t* out_n);
+/* Same as rsv_result, without the host copy: a single-use sampler whose result is published into
+ * its pinned result buffer (ELEMENTS and DISTINCT, k x key_width <= 1 MB) hands that buffer over.
+ * *buf holds the *out_n keys (as rsv_result writes them) and belongs to the caller until
+ * rsv_host_release(*buf); the sampler closes as after rsv_result.  The copy it saves is a read of
+ * memory the GPU just wrote (k = 65536: ~22 us from DRAM).  Anything else (reusable samplers, larger
+ * results) returns RSV_E_UNSUPPORTED with the sampler untouched: call rsv_result instead. */
+rsv_status rsv_result_take(rsv_sampler* s, void** buf, int64_t* out_n);
+void       rsv_host_release(void* buf);
 
 int32_t    rsv_is_open(const rsv_sampler* s); /* Sampler.isOpen (S:67, S:193, S:380) */
 int64_t    rsv_count(const rsv_sampler* s);   /* elements sampled so far (S:203) */

@@ -24,7 +24,8 @@ DISTINCT_AUTO, DISTINCT_SET, DISTINCT_ORDERED = 0, 1, 2
 # every symbol include/reservoir_hip.h declares
 EXPORTED_SYMBOLS = (
     "rsv_abi_version", "rsv_last_error", "rsv_status_string", "rsv_config_init", "rsv_create",
-    "rsv_destroy", "rsv_sample", "rsv_sample_batch", "rsv_result", "rsv_result_device",
+    "rsv_destroy", "rsv_sample", "rsv_sample_batch", "rsv_result", "rsv_result_device", "rsv_result_take",
+    "rsv_host_release",
     "rsv_is_open", "rsv_count", "rsv_set_stream", "rsv_get_stream", "rsv_synchronize", "rsv_seek",
     "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
     "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
@@ -108,6 +109,9 @@ def load():
     L.rsv_sample_batch.argtypes = [vp, vp, i64, i32, vp]
     L.rsv_result.argtypes = [vp, vp, i64, C.POINTER(i64)]
     L.rsv_result_device.argtypes = [vp, vp, i64, C.POINTER(i64)]
+    L.rsv_result_take.argtypes = [vp, C.POINTER(vp), C.POINTER(i64)]
+    L.rsv_host_release.argtypes = [vp]
+    L.rsv_host_release.restype = None
     L.rsv_is_open.argtypes = [vp]
     L.rsv_is_open.restype = i32
     L.rsv_count.argtypes = [vp]
@@ -137,7 +141,7 @@ def load():
     L.rsv_fill_slots.argtypes = [vp, vp]
     L.rsv_retain_log.argtypes = [vp, i32]
     for name in ("rsv_config_init", "rsv_create", "rsv_sample", "rsv_sample_batch", "rsv_result",
-                 "rsv_result_device", "rsv_set_stream", "rsv_synchronize", "rsv_seek",
+                 "rsv_result_device", "rsv_result_take", "rsv_set_stream", "rsv_synchronize", "rsv_seek",
                  "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
                  "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
                  "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read", "rsv_stage_acquire",

@@ -802,7 +802,8 @@ static rsv_status wait_flag(rsv_sampler* s, uint32_t gen) {
     return fail(RSV_E_DEVICE, "result publish flag not set after stream synchronize");
 }
 
-static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* out_n, bool device_out) {
+static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* out_n, bool device_out,
+                              bool take = false) {
     if (rsv_status st = check_open(s)) return st;
     if (!out_n) return fail(RSV_E_NULL_POINTER, "out_n is NULL");
     DeviceGuard g(s->device);
@@ -813,7 +814,7 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
         if (int rc = distinct_finalize(s->distinct, s->stream)) return (rsv_status)rc;
         m = distinct_size(s->distinct);
         if (m > cap) return fail(RSV_E_ILLEGAL_ARGUMENT, "result buffer too small");
-        if (m && !out) return fail(RSV_E_NULL_POINTER, "out is NULL");
+        if (m && !out && !take) return fail(RSV_E_NULL_POINTER, "out is NULL");
         if (m) {
             if (device_out) {
                 if (int rc = distinct_export(s->distinct, out, nullptr, s->stream)) return (rsv_status)rc;
@@ -832,7 +833,7 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
                     if (rsv_status st = wait_flag(s, gen)) return st;
                     // the publication was the handle's last work: no stream synchronize
                     if (s->result_gen == gen) s->ops_done = s->ops;
-                    memcpy(out, s->result_h, (size_t)m * s->kw);
+                    if (!take) memcpy(out, s->result_h, (size_t)m * s->kw);
                     *out_n = m;
                     if (!s->cfg.reusable) s->open = false;
                     return RSV_OK;
@@ -848,8 +849,9 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
     } else {
         m = std::min<int64_t>(s->count, (int64_t)s->k);  // resultImpl, Sampler.scala:318-331
         if (m > cap) return fail(RSV_E_ILLEGAL_ARGUMENT, "result buffer too small");
-        if (m && !out) return fail(RSV_E_NULL_POINTER, "out is NULL");
+        if (m && !out && !take) return fail(RSV_E_NULL_POINTER, "out is NULL");
         src = s->slot_key;
+        if (m && !out && take) out = s->result_h;  // checked: a published result (see rsv_result_take)
         if (m && device_out) {
             touch(s);
             RSV_HIP_TRY(hipMemcpyAsync(out, src, m * s->kw, hipMemcpyDeviceToDevice, s->stream));
@@ -867,7 +869,7 @@ static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* o
                 }
                 if (rsv_status st = wait_flag(s, gen)) return st;
                 if (s->pub_valid && s->pub_ops == s->ops && s->result_gen == gen) s->ops_done = s->ops;
-                memcpy(out, s->result_h, (size_t)m * s->kw);
+                if (!take) memcpy(out, s->result_h, (size_t)m * s->kw);
                 *out_n = m;
                 if (!s->cfg.reusable) s->open = false;
                 return RSV_OK;
@@ -890,6 +892,33 @@ rsv_status rsv_result(rsv_sampler* s, void* out, int64_t cap, int64_t* out_n) {
 
 rsv_status rsv_result_device(rsv_sampler* s, void* out_dev, int64_t cap, int64_t* out_n) {
     return result_impl(s, out_dev, cap, out_n, true);
+}
+
+rsv_status rsv_result_take(rsv_sampler* s, void** buf, int64_t* out_n) {
+    if (rsv_status st = check_open(s)) return st;
+    if (!buf || !out_n) return fail(RSV_E_NULL_POINTER, "buf / out_n is NULL");
+    if (s->cfg.reusable || (int64_t)s->k * s->kw > kPublishMaxBytes)
+        return fail(RSV_E_UNSUPPORTED, "rsv_result_take: single-use samplers with a published result only");
+    {
+        DeviceGuard g(s->device);
+        if (rsv_status st = ensure_result_buffer(s)) return st;
+    }
+    // the published path of rsv_result, with the buffer handed over instead of copied
+    void* h = s->result_h;
+    const int64_t cap = s->k;
+    rsv_status st = result_impl(s, nullptr, cap, out_n, false, /*take=*/true);
+    if (st != RSV_OK) return st;
+    *buf = h;
+    s->result_h = nullptr;  // the caller's now: a closed single-use handle publishes nothing more
+    s->result_dev = nullptr;
+    s->result_flag = nullptr;
+    s->result_flag_dev = nullptr;
+    s->result_publish = false;
+    return RSV_OK;
+}
+
+void rsv_host_release(void* buf) {
+    if (buf) pool_host_free(buf);
 }
 
 int32_t rsv_is_open(const rsv_sampler* s) { return s && s->open ? 1 : 0; }

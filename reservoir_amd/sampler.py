@@ -121,6 +121,26 @@ def _current_raw_stream(torch, t) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+
+class _HostBuffer:
+    """A pinned result buffer handed over by rsv_result_take: exposed to numpy as raw bytes, released
+    (rsv_host_release) when the last array viewing it is gone."""
+
+    def __init__(self, lib, ptr: int, nbytes: int):
+        self._lib = lib
+        self._ptr = ptr
+        # (numpy wants a non-NULL address even for an empty view)
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "version": 3,
+                                    "data": (ptr or 1, False)}
+
+    def __del__(self):
+        ptr, self._ptr = self._ptr, 0
+        if ptr:
+            try:
+                self._lib.rsv_host_release(C.c_void_p(ptr))
+            except Exception:  # interpreter shutdown: the process frees it
+                pass
+
 class GpuSampler:
     """A ``Sampler[A, B]`` whose state lives on an MI355X (one opaque C-ABI handle)."""
 
@@ -145,6 +165,7 @@ class GpuSampler:
             self._dtype = np.dtype(f"V{self._width}")
         self._kind = kind
         self._k = max_sample_size
+        self._reusable = bool(reusable)
         cfg = N.RsvConfig()
         N.check(self._L.rsv_config_init(C.byref(cfg)))
         cfg.kind = kind
@@ -315,8 +336,17 @@ class GpuSampler:
 
     def result(self) -> np.ndarray:
         """Sampler.result (Sampler.scala:59-60). Slot order for element samplers."""
-        if not self._L.rsv_is_open(self._h):
+        if self._h is None or not self._L.rsv_is_open(self._h):
             raise IllegalStateException("use of sampler after calling `result()`")
+        if not self._reusable and self._width <= 8:
+            # the published keys handed over instead of copied (rsv_result_take); the array owns the
+            # pinned buffer and releases it when the last view of it goes
+            buf, n = C.c_void_p(), C.c_int64(0)
+            st = self._L.rsv_result_take(self._h, C.byref(buf), C.byref(n))
+            if st == N.OK:
+                return np.asarray(_HostBuffer(self._L, buf.value or 0, n.value * self._width)).view(self._dtype)
+            if st != N.E_UNSUPPORTED:
+                N.check(st)
         out = np.empty(self._k, dtype=self._dtype)
         n = C.c_int64(0)
         N.check(self._L.rsv_result(self._h, out.ctypes.data_as(C.c_void_p), self._k, C.byref(n)))
