@@ -186,6 +186,17 @@ struct RangeBound {
     }
 };
 
+// streaming shape of the filter passes: 16-B loads in flight per lane, workgroups per CU
+// (dev builds vary them: make exp EXP="-DRSV_K3_U=16 -DRSV_K3_WGCU=64")
+#ifndef RSV_K3_U
+#define RSV_K3_U 8
+#endif
+#ifndef RSV_K3_WGCU
+#define RSV_K3_WGCU 32
+#endif
+constexpr int kK3U = RSV_K3_U;
+constexpr int64_t kK3Grid = 256 * RSV_K3_WGCU;
+
 template <typename KeyT, int HASH, int U, bool GUARD, typename Out, typename Bound>
 __device__ __forceinline__ void k3_tile(const typename Vec<KeyT>::T* x, int64_t v0, int64_t T, int64_t n_vec,
                                         const KeyT* keys, const int64_t* hashes, int64_t r0, int64_t r1,
@@ -223,7 +234,7 @@ __device__ __forceinline__ void k3_filter_body(const KeyT* __restrict__ keys, co
                                                unsigned long long* __restrict__ counter, int64_t cap,
                                                uint32_t* __restrict__ cand_i, Sink* sink = nullptr) {
     using V = Vec<KeyT>;
-    constexpr int U = 8;  // 8 x 16-B loads in flight per lane (tools/micro_k3: 6.0 -> 6.4 TB/s vs 4)
+    constexpr int U = kK3U;  // 8 x 16-B loads in flight per lane (tools/micro_k3: 6.0 -> 6.4 TB/s vs 4)
     constexpr uint32_t Q = CandOut<KeyT, IDX>::B + 64;
     __shared__ int64_t sh_h[kBlock / 64][Q];
     __shared__ KeyT sh_k[kBlock / 64][Q];
@@ -2159,7 +2170,7 @@ template <typename KeyT>
 static hipError_t launch_filter(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
                                 int64_t tinc, hipStream_t st) {
     // 32 workgroups per CU over the pass (tools/micro_k3: 2048 -> 8192 workgroups, 5.9 -> 6.4 TB/s)
-    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 32 + 1), 1), 256 * 32);
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 32 + 1), 1), kK3Grid);
     KeyT* ck = (KeyT*)d->cand_k;
     switch (d->hash_kind) {
     case kHashJavaLong:
@@ -2731,7 +2742,7 @@ static int sched_launch(DistinctState* d, const KeyT* keys, const int64_t* hashe
     KeyT* bk = (KeyT*)d->sbk;
     if (d->timer) d->timer->mark(st);
     {
-        const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 32 + 1), 1), 256 * 32);
+        const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 32 + 1), 1), kK3Grid);
         KeyT* lk = (KeyT*)d->log_k + lbase;
 #define RSV_SCHED_FILTER(H)                                                                                        \
     hipLaunchKernelGGL((sched_filter<KeyT, H>), dim3(grid), dim3(kBlock), 0, st, keys, hashes, n, d->r0, d->r1,      \

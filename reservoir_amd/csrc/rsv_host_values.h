@@ -147,6 +147,7 @@ struct HostValues {
             pq_add(elem, h);
             set_add(elem);
             max_hash = hh[1];
+            prefetch(he[1]);  // the next replacement removes the new root from the set
         }
     }
     // sample() over a run in arrival order: elem(t), hash(t) for t in [0, c).  Once the heap is

@@ -61,20 +61,34 @@ int run(const v2i64* d, int64_t n_vec, unsigned long long* cnt, int grid, const 
     return 0;
 }
 
-int main() {
+__global__ void fill_random(int64_t* p, int64_t n) {  // splitmix64 of the index (the C4 keys' shape)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = (int64_t)(z ^ (z >> 31));
+    }
+}
+
+int main(int argc, char** argv) {
     const int64_t n = 500000000;  // C4 per-GPU share: 5e8 int64 keys = 4 GB
     v2i64* d;
     CK(hipMalloc(&d, n * 8));
-    CK(hipMemset(d, 0x5A, n * 8));
+    // argv[1] == "random": splitmix64 keys (the product's data); default: a constant byte (r02)
+    if (argc > 1 && argv[1][0] == 'r') {
+        hipLaunchKernelGGL(fill_random, dim3(8192), dim3(256), 0, 0, (int64_t*)d, n);
+        CK(hipDeviceSynchronize());
+    } else {
+        CK(hipMemset(d, 0x5A, n * 8));
+    }
     unsigned long long* cnt;
     CK(hipMalloc(&cnt, 8));
     const int64_t nv = n / 2;
-    for (int grid : {1024, 2048, 4096, 8192}) {
+    for (int grid : {4096, 8192, 16384}) {
         if (run<4, 1>(d, nv, cnt, grid, "nt")) return 1;
-        if (run<4, 0>(d, nv, cnt, grid, "plain")) return 1;
         if (run<8, 1>(d, nv, cnt, grid, "nt")) return 1;
         if (run<8, 0>(d, nv, cnt, grid, "plain")) return 1;
-        if (run<2, 1>(d, nv, cnt, grid, "nt")) return 1;
+        if (run<16, 1>(d, nv, cnt, grid, "nt")) return 1;
     }
     return 0;
 }

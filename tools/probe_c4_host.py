@@ -53,6 +53,28 @@ def main():
         cc = a[a[:, 2] == 1] * 1e6
         print(f"{hk}/{order}: sample_all median {np.median(a[:, 0]) * 1e6:.1f} us, result() median {np.median(py[:, 1]):.1f} us, "
               f"rsv_result alone {np.median(cc[:, 1]):.1f} us")
+    # the Python mirror's share: sample_all vs the bare ctypes call with its arguments prepared
+    for hk in ("identity", "default"):
+        rows = []
+        for rep in range(14):
+            mk = Sampler.distinct(k, seed=7)
+            d = mk() if hk == "default" else mk(hash=hk)
+            d.set_stream(torch.cuda.current_stream().cuda_stream)
+            ptr = C.c_void_p(vals.data_ptr())
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            if rep % 2:
+                d.sample_all(vals)
+            else:
+                N.check(L.rsv_sample_batch(d.handle, ptr, n, N.MEM_DEVICE, None))
+            t1 = time.perf_counter()
+            d.result()
+            d.close()
+            if rep >= 2:
+                rows.append((t1 - t0, rep % 2))
+        a = np.array(rows)
+        print(f"{hk}: sample_all {np.median(a[a[:, 1] == 1, 0]) * 1e6:.1f} us, bare rsv_sample_batch "
+              f"{np.median(a[a[:, 1] == 0, 0]) * 1e6:.1f} us")
     # the copy alone: 512 KB from a fresh numpy buffer vs a reused one
     src = torch.empty(k, dtype=torch.int64, pin_memory=True)
     ts, tr = [], []
