@@ -1210,23 +1210,21 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(const Src src, int64
             gh[o] = h[r];
             gk[o] = k[r];
             // ranges this element verifies: r_a = first r >= 1 with b[r] >= tag (arrived before b[r]),
-            // r_h = last r with t[r] >= h
-            int lo = 0, hi = nr;  // b[lo] < tag <= b[hi] (b[nr] = n >= every tag)
-            if (g[r] == 0) hi = 1;
-            else
-                while (hi - lo > 1) {
-                    const int mid = (lo + hi) >> 1;
-                    if (sb[mid] >= (int64_t)g[r]) hi = mid;
-                    else lo = mid;
-                }
-            ra = std::max(1, hi);
-            int a = 0, z = nr;  // t[a] >= h > t[z] (t[nr] treated as -inf)
-            while (z - a > 1) {
-                const int mid = (a + z) >> 1;
-                if (stt[mid] >= h[r]) a = mid;
-                else z = mid;
+            // r_h = last r with t[r] >= h.  Both as fixed six-step searches (nr <= 64) run side by
+            // side, so their dependent LDS reads overlap: pa = last index with b[pa] < tag (b[0] = 0,
+            // b[nr] = n >= every tag; a set member, tag 0, stays at 0), pt = last with t[pt] >= h
+            const int64_t tag = (int64_t)g[r];
+            int pa = 0, pt = 0;
+#pragma unroll
+            for (int step = 32; step; step >>= 1) {
+                const int qa = pa + step, qt = pt + step;
+                const bool ma = qa <= nr && sb[qa < kMaxRanges ? qa : kMaxRanges] < tag;
+                const bool mt = qt < nr && stt[qt < kMaxRanges ? qt : kMaxRanges - 1] >= h[r];
+                pa = ma ? qa : pa;
+                pt = mt ? qt : pt;
             }
-            rh = stt[0] >= h[r] ? a : -1;
+            ra = pa + 1;
+            rh = stt[0] >= h[r] ? pt : -1;
         }
         // +1 at r_a, -1 at r_h + 1 of the difference array.  The bucket map is monotone in h, so a
         // bucket's elements share r_h almost always: one atomic for the wave's -1s then, instead of
