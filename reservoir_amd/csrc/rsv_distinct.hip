@@ -467,6 +467,42 @@ __device__ __forceinline__ T shfl_xor_any(T v, int mask) {
     }
 }
 
+// lane ^ s exchange without the LDS crossbar (ds_bpermute: an LDS round trip on the sort networks'
+// dependent chains): quad_perm DPP for s = 1, 2, two row shifts for 4, row_ror for 8, the gfx950
+// permlane16/32 swaps for 16, 32.  s folds to a constant once the networks are unrolled.
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v, int s) {
+    switch (s) {
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    case 4: {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xF, 0xF, false);  // row_shl:4 (i + 4)
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, false);  // row_shr:4 (i - 4)
+        return (threadIdx.x & 4) ? dn : up;
+    }
+    case 8: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    case 16: {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (threadIdx.x & 16) ? r[0] : r[1];
+    }
+    case 32: {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (threadIdx.x & 32) ? r[0] : r[1];
+    }
+    default: return (uint32_t)__shfl_xor((int)v, s);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T xor_any(T v, int s) {
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t x = (uint64_t)v;
+        const uint32_t lo = xor_lane32((uint32_t)x, s), hi = xor_lane32((uint32_t)(x >> 32), s);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)xor_lane32((uint32_t)v, s);
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ T shfl_any(T v, int src) {
     if constexpr (sizeof(T) == 8) {
@@ -497,7 +533,7 @@ __device__ __forceinline__ bool wave_packed_sort(const Load& load, uint32_t n, i
     uint64_t lo = valid ? u : ~0ull;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t o = shfl_xor_any(lo, d);
+        const uint64_t o = xor_any(lo, d);
         lo = o < lo ? o : lo;
     }
     if (__ballot(valid && ((u - lo) >> 58) != 0)) return false;
@@ -506,7 +542,7 @@ __device__ __forceinline__ bool wave_packed_sort(const Load& load, uint32_t n, i
     for (uint32_t size = 2; size <= 64; size <<= 1) {
 #pragma unroll
         for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-            const uint64_t o = shfl_xor_any(key, (int)stride);
+            const uint64_t o = xor_any(key, (int)stride);
             const bool lower = (lane & stride) == 0;
             const bool up = (lane & size) == 0;
             const bool take = (lower == up) ? (o < key) : (key < o);
@@ -601,8 +637,8 @@ __device__ __forceinline__ uint32_t wave_sort_bucket(const Src src, int64_t* gh,
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const uint32_t i = r * 64u + lane;
-                    const int64_t oh = shfl_xor_any(h[r], (int)stride);
-                    const KeyT ok = shfl_xor_any(k[r], (int)stride);
+                    const int64_t oh = xor_any(h[r], (int)stride);
+                    const KeyT ok = xor_any(k[r], (int)stride);
                     const bool lower = (lane & stride) == 0;
                     const bool up = (i & size) == 0;
                     // the lower lane keeps the smaller entry in an ascending run, the larger otherwise
@@ -1173,9 +1209,9 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(const Src src, int64
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const uint32_t i = r * 64u + lane;
-                    const int64_t oh = shfl_xor_any(h[r], (int)stride);
-                    const KeyT ok = shfl_xor_any(k[r], (int)stride);
-                    const uint32_t og = (uint32_t)__shfl_xor((int)g[r], (int)stride);
+                    const int64_t oh = xor_any(h[r], (int)stride);
+                    const KeyT ok = xor_any(k[r], (int)stride);
+                    const uint32_t og = xor_lane32(g[r], (int)stride);
                     const bool lower = (lane & stride) == 0;
                     const bool up = (i & size) == 0;
                     const bool other_less = ent_less3<KeyT>(oh, ok, og, h[r], k[r], g[r]);
