@@ -1346,14 +1346,6 @@ constexpr int kBinLog = 5;
 constexpr uint32_t kBinCap = 3072;
 constexpr int kBinTile = 4;          // entries per thread of sched_bin_file (1024 threads: >= 256 workgroups at C4)
 constexpr int kBinSortThreads = 512;
-// each bin's places are reserved on kBinCopies counters (workgroup w uses copy w % kBinCopies, its
-// own sub-slab of the bin's memory): every workgroup reserves on every bin at about the same
-// moment, and ~460 returning atomics queued on one address serialise (dev A/B: -DRSV_BIN_COPIES=1)
-#ifndef RSV_BIN_COPIES
-#define RSV_BIN_COPIES 8
-#endif
-constexpr uint32_t kBinCopies = RSV_BIN_COPIES;
-__host__ __device__ inline uint32_t bin_copies(uint32_t lb) { return lb >= 8 ? kBinCopies : 1u; }
 
 __host__ __device__ inline uint32_t bin_log(uint32_t lb, uint32_t fl = kBinLog) { return lb > fl ? lb - fl : 0u; }
 
@@ -1412,20 +1404,19 @@ __global__ __launch_bounds__(1024) void sched_bin_file(const SchedDev* __restric
     }
     __syncthreads();
     uint32_t* bcnt = bucket_count(ctl);
-    const uint32_t copies = bin_copies(lb), copy = blockIdx.x % copies;
     for (uint32_t i = threadIdx.x; i < C; i += blockDim.x) {
         const uint32_t n = hist[i];
-        if (n) hist[i] = atomicAdd(&bcnt[((size_t)i * copies + copy) * kCountStride], n);
+        if (n) hist[i] = atomicAdd(&bcnt[(size_t)i * kCountStride], n);
     }
     __syncthreads();
-    const uint32_t sub = ((uint32_t)kBucketCap << (lb - lbin)) / copies;  // entries per sub-slab
+    const uint32_t cap_bin = std::min<uint32_t>(kBinCap, (uint32_t)kBucketCap << (lb - lbin));
     bool over = false;
 #pragma unroll
     for (int j = 0; j < kBinTile; ++j) {
         if (ebin[j] == 0xFFFFFFFFu) continue;
         const uint32_t pos = hist[ebin[j]] + eloc[j];
-        if (pos < sub) {
-            const size_t slot = ((size_t)ebin[j] << (lb - lbin)) * kBucketCap + (size_t)copy * sub + pos;
+        if (pos < cap_bin) {
+            const size_t slot = ((size_t)ebin[j] << (lb - lbin)) * kBucketCap + pos;
             bh[slot] = eh[j];
             bk[slot] = ek[j];
             bi[slot] = eg[j];
@@ -1465,24 +1456,8 @@ __global__ __launch_bounds__(kBinSortThreads) void sched_bin_sort(int64_t cand_c
     const uint32_t B_lo = sd->B_lo;
     const uint64_t q = sd->lo_mult;
     const SchedMap map{sd, stt, sd->B, B_lo, (uint32_t)nr, stt[nr - 1], q > UINT64_MAX / B_lo ? UINT64_MAX : q * B_lo};
-    const uint32_t copies = bin_copies(lb), sub = ((uint32_t)kBucketCap << (lb - lbin)) / copies;
-    uint32_t* bcnt = bucket_count(ctl) + (size_t)bin * copies * kCountStride;
-    __shared__ uint32_t s_pre[kBinCopies + 1];
-    if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-        for (uint32_t c = 0; c < copies; ++c) {
-            s_pre[c] = tot;
-            tot += std::min(bcnt[(size_t)c * kCountStride], sub);  // more: sched_bin_file flagged it
-        }
-        s_pre[copies] = tot;
-    }
-    __syncthreads();
-    if (s_pre[copies] > kBinCap) {  // the bin does not fit LDS: the verdict reports an overflow
-        if (threadIdx.x < copies) bcnt[(size_t)threadIdx.x * kCountStride] = 0;
-        if (threadIdx.x == 0) ctl[1] = 1;
-        return;
-    }
-    const uint32_t nb = s_pre[copies];
+    uint32_t* bcnt = bucket_count(ctl) + (size_t)bin * kCountStride;
+    const uint32_t nb = std::min<uint32_t>(*bcnt, kBinCap);  // more: sched_bin_file flagged the overflow
     const size_t slab = (size_t)fb0 * kBucketCap;
     constexpr int kPer = kBinCap / kBinSortThreads;
     uint32_t fj[kPer], fr[kPer];
@@ -1490,13 +1465,10 @@ __global__ __launch_bounds__(kBinSortThreads) void sched_bin_sort(int64_t cand_c
     for (int j = 0; j < kPer; ++j) {
         const uint32_t i = j * kBinSortThreads + threadIdx.x;
         if (i < nb) {
-            uint32_t c = 0;
-            while (s_pre[c + 1] <= i) ++c;
-            const size_t src = slab + (size_t)c * sub + (i - s_pre[c]);
-            const int64_t h = bh[src];
+            const int64_t h = bh[slab + i];
             lh[i] = h;
-            lk[i] = bk[src];
-            lg[i] = bi[src];
+            lk[i] = bk[slab + i];
+            lg[i] = bi[slab + i];
             fj[j] = map(h) - fb0;
             fr[j] = atomicAdd(&fcnt[fj[j]], 1u);
         }
@@ -1549,7 +1521,7 @@ __global__ __launch_bounds__(kBinSortThreads) void sched_bin_sort(int64_t cand_c
     int* acc = vacc + (size_t)(bin % kVerifyCopies) * (kMaxRanges + 1);
     for (int i = threadIdx.x; i <= nr; i += blockDim.x)
         if (sdiff[i]) atomicAdd(&acc[i], sdiff[i]);
-    if (threadIdx.x < copies) bcnt[(size_t)threadIdx.x * kCountStride] = 0;
+    if (threadIdx.x == 0) *bcnt = 0;
 }
 
 // ctl[0..5], the verification verdict (first range r >= 1 short of k elements, or -1) and the
