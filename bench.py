@@ -394,6 +394,12 @@ def main() -> None:
     keys = torch.empty(n, dtype=torch.int64, device=dev)
     splitmix_fill(keys, 0x5EED0000 + offset)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    # N > 1 over RCCL: each step's combine (export, all-gather, merge) runs on a communication
+    # stream, handed over from the sampling stream by an event (rsv_set_stream), so the next step's
+    # K1 is not queued behind this step's collective.  (Not under gloo: its all-gather of CUDA
+    # tensors waits on the host for the stream it runs on, which then serialises the steps -- the
+    # 2-rank rehearsal ran 0.54 -> 1.05 ms per step with it.)
+    comm = torch.cuda.Stream(device=dev) if world > 1 and backend == "nccl" else None
 
     L = _native.load()
 
@@ -404,7 +410,11 @@ def main() -> None:
         s.set_stream(stream)
         s.seek(offset)
         s.sample_all(keys)
-        if world > 1:
+        if comm is not None:
+            s.set_stream(comm.cuda_stream)
+            with torch.cuda.stream(comm):
+                D.combine(s, device=dev, total_count=n * world)
+        elif world > 1:
             D.combine(s, device=dev, total_count=n * world)
         return s
 

@@ -64,8 +64,19 @@ def _worker(rank, world, port, q):
             out[f"elements_{kt}"] = (s.result().astype(np.int64).tolist(), s.count)
             s2 = Sampler(k, seed=0xC0FFEE, stream_id=0x5A5A, key_type=kt)()
             D.sample_shard(s2, kd, lo)
-            D.combine(s2, device=dev, total_count=n)  # bench.py's form
+            D.combine(s2, device=dev, total_count=n)
             out[f"elements_{kt}_total"] = (s2.result().astype(np.int64).tolist(), s2.count)
+            # bench.py's form: sampled on torch's stream, combined on a communication stream that
+            # the sampler hands over to (rsv_set_stream: an event wait, no host wait)
+            comm = torch.cuda.Stream(device=dev)
+            s3 = Sampler(k, seed=0xC0FFEE, stream_id=0x5A5A, key_type=kt)()
+            s3.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            s3.seek(lo)
+            s3.sample_all(kd)
+            s3.set_stream(comm.cuda_stream)
+            with torch.cuda.stream(comm):
+                D.combine(s3, device=dev, total_count=n)
+            out[f"elements_{kt}_comm"] = (s3.result().astype(np.int64).tolist(), s3.count)
         vals = np.random.default_rng(3).integers(-2**63, 2**63 - 1, size=400_000, dtype=np.int64)
         vals = np.concatenate([vals, vals[: 150_000]])
         dlo, dhi = D.shard_range(vals.size, rank, world)
@@ -115,9 +126,9 @@ def test_gloo_ranks_real_engine(cuda, oracle, world):
     ref = oracle.Distinct(5000, 9, oracle.HASH_IDENTITY)
     ref.sample_all(vals)
     for rank, out in outs:
-        for key in ("elements_long", "elements_long_total"):
+        for key in ("elements_long", "elements_long_total", "elements_long_comm"):
             assert out[key] == (want.tolist(), n), (rank, key)
-        for key in ("elements_int", "elements_int_total"):
+        for key in ("elements_int", "elements_int_total", "elements_int_comm"):
             assert out[key] == (want32.tolist(), n), (rank, key)
         assert out["distinct"] == (sorted(ref.result()[0].tolist()), vals.size), rank
     replays = 0
