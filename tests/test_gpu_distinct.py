@@ -493,6 +493,28 @@ def test_ordered_scheduled_pass(cuda, oracle, monkeypatch, k, n, seed, batches):
     torch.cuda.empty_cache()
 
 
+def test_ordered_fused_plan_without_full_heap(cuda, oracle):
+    """A fresh sampler's first chunk that does NOT fill the heap (its keys repeat a small set): the
+    device plan behind it is void (ctl_plan), the chunk loop goes on, and the host plans the
+    scheduled pass once the heap is full -- same set as the reference."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    rng = np.random.default_rng(77)
+    k = 2048
+    head = rng.integers(-2**63, 2**63 - 1, size=1500, dtype=np.int64)[rng.integers(0, 1500, 200_000)]
+    tail = rng.integers(-2**63, 2**63 - 1, size=3_000_000, dtype=np.int64)
+    vals = np.concatenate([head, tail, tail[:500_000]])
+    ref = oracle.Distinct(k, 31, oracle.HASH_JAVA_LONG)
+    ref.sample_all(vals)
+    d = Sampler.distinct(k, seed=31)()
+    d.sample_all(torch.from_numpy(vals).to(cuda))
+    info = d.distinct_info()
+    assert info["sched_passes"] >= 1, info
+    assert d.result().tolist() == ref.result()[0].tolist()
+
+
 def test_ordered_scheduled_pass_ties(cuda, oracle):
     """Colliding Long.hashCode values (tied boundary buckets) through the scheduled pass: the pass's
     candidates form one logged segment, and the host replay over it reproduces the reference."""
