@@ -306,6 +306,24 @@ __global__ __launch_bounds__(kBlock) void k3_filter(const KeyT* __restrict__ key
     k3_filter_body<KeyT, HASH, IDX>(keys, hashes, n, r0, r1, ConstBound{tinc}, cand_h, cand_k, counter, cap, cand_i);
 }
 
+// A filter with no bound (the heap still filling): every element is a candidate, so element i is
+// written to place i -- no staging, no reservation atomics -- and the counter set to n
+// (heap-filling chunk of C4's ordered share, 132k keys: the staged k3_filter took 12.4 us)
+template <typename KeyT, int HASH, bool IDX>
+__global__ __launch_bounds__(kBlock) void hash_all(const KeyT* __restrict__ keys, const int64_t* __restrict__ hashes,
+                                                   int64_t n, int64_t r0, int64_t r1, int64_t* __restrict__ out_h,
+                                                   KeyT* __restrict__ out_k, uint32_t* __restrict__ out_i,
+                                                   unsigned long long* __restrict__ counter) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const KeyT key = keys[i];
+        out_h[i] = elem_hash<KeyT, HASH>(keys, hashes, i, key, r0, r1);
+        out_k[i] = key;
+        if constexpr (IDX) out_i[i] = (uint32_t)i;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *counter = (unsigned long long)n;  // re-armed to 0 by read_ctl
+}
+
 template <typename KeyT, int HASH>
 __global__ __launch_bounds__(kBlock) void sample_hash_kernel(const KeyT* __restrict__ keys,
                                                              const int64_t* __restrict__ hashes,
@@ -2203,9 +2221,23 @@ int distinct_publish(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, u
 template <typename KeyT>
 static hipError_t launch_filter(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
                                 int64_t tinc, hipStream_t st) {
+    KeyT* ck = (KeyT*)d->cand_k;
+    if (tinc == INT64_MAX && n <= d->cand_cap) {  // no bound: every element a candidate, in place
+        const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n), 1), 4096);
+#define RSV_HASH_ALL(H)                                                                                       \
+    hipLaunchKernelGGL((hash_all<KeyT, H, false>), dim3(g), dim3(kBlock), 0, st, keys, hashes, n, d->r0, d->r1, \
+                       d->cand_h, ck, (uint32_t*)nullptr, d->counter)
+        switch (d->hash_kind) {
+        case kHashJavaLong: RSV_HASH_ALL(kHashJavaLong); break;
+        case kHashJavaInt: RSV_HASH_ALL(kHashJavaInt); break;
+        case kHashPrecomputed: RSV_HASH_ALL(kHashPrecomputed); break;
+        default: RSV_HASH_ALL(kHashIdentity);
+        }
+#undef RSV_HASH_ALL
+        return hipGetLastError();
+    }
     // 32 workgroups per CU over the pass (tools/micro_k3: 2048 -> 8192 workgroups, 5.9 -> 6.4 TB/s)
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n / 32 + 1), 1), kK3Grid);
-    KeyT* ck = (KeyT*)d->cand_k;
     switch (d->hash_kind) {
     case kHashJavaLong:
         hipLaunchKernelGGL((k3_filter<KeyT, kHashJavaLong>), dim3(grid), dim3(kBlock), 0, st, keys, hashes,
@@ -2516,6 +2548,20 @@ template <typename KeyT>
 static hipError_t launch_filter_idx(DistinctState* d, const KeyT* keys, const int64_t* hashes, int64_t n,
                                     int64_t tinc, int64_t* out_h, KeyT* out_k, uint32_t* out_i, int64_t cap,
                                     hipStream_t st) {
+    if (tinc == INT64_MAX && n <= cap) {  // no bound (the heap filling): every element in place
+        const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(grid_1d(n), 1), 4096);
+#define RSV_HASH_ALL(H)                                                                                        \
+    hipLaunchKernelGGL((hash_all<KeyT, H, true>), dim3(g), dim3(kBlock), 0, st, keys, hashes, n, d->r0, d->r1, out_h, \
+                       out_k, out_i, d->counter)
+        switch (d->hash_kind) {
+        case kHashJavaLong: RSV_HASH_ALL(kHashJavaLong); break;
+        case kHashJavaInt: RSV_HASH_ALL(kHashJavaInt); break;
+        case kHashPrecomputed: RSV_HASH_ALL(kHashPrecomputed); break;
+        default: RSV_HASH_ALL(kHashIdentity);
+        }
+#undef RSV_HASH_ALL
+        return hipGetLastError();
+    }
     // ~8 keys per thread (one 1024-key tile per two waves) up to 8192 workgroups: a short chunk
     // where every key is a candidate (the heap filling) would otherwise run on a few waves
     // (132k keys: 17 workgroups, 18 us)
