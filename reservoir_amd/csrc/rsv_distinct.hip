@@ -846,12 +846,13 @@ struct SchedMap {
     __device__ __forceinline__ uint32_t operator()(int64_t h) const {
         const uint64_t u = (uint64_t)h ^ 0x8000000000000000ull;
         if (h <= t_lo) return std::min<uint32_t>(B_lo - 1, (uint32_t)__umul64hi(u, lo_mult));
-        // piece p = the last range with t[p] >= h (t non-increasing; the set's top sits at t[0] + 1)
-        int lo = 0, hi = (int)nr - 1;  // t[lo] >= h > t[hi]
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (st[mid] >= h) lo = mid;
-            else hi = mid;
+        // piece p = the last range with t[p] >= h (t non-increasing; the set's top sits at t[0] + 1),
+        // by a fixed six-step search (nr <= 64; h > t[nr - 1] here, so p < nr - 1)
+        int lo = 0;
+#pragma unroll
+        for (int step = 32; step; step >>= 1) {
+            const int q = lo + step;
+            lo = (q < (int)nr - 1 && st[q < kMaxRanges ? q : kMaxRanges - 1] >= h) ? q : lo;
         }
         const float pos = sd->hi_a[lo] * (float)((double)u * 5.421010862427522e-20) + sd->hi_c[lo];
         const uint32_t bh = (uint32_t)std::max(0.0f, pos * (float)(B - B_lo));
