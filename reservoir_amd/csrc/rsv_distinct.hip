@@ -1363,7 +1363,11 @@ __global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap
 // expected fill; more (like a fine bucket over kBucketCap) is the overflow the host falls back on.
 constexpr int kBinLog = 5;
 constexpr uint32_t kBinCap = 3072;
-constexpr int kBinTile = 4;          // entries per thread of sched_bin_file (1024 threads: >= 256 workgroups at C4)
+constexpr int kBinTile = 4;          // entries per thread of sched_bin_file
+#ifndef RSV_BIN_FILE_THREADS
+#define RSV_BIN_FILE_THREADS 1024
+#endif
+constexpr int kBinFileThreads = RSV_BIN_FILE_THREADS;  // (dev builds vary it)
 constexpr int kBinSortThreads = 512;
 
 __host__ __device__ inline uint32_t bin_log(uint32_t lb, uint32_t fl = kBinLog) { return lb > fl ? lb - fl : 0u; }
@@ -1371,7 +1375,7 @@ __host__ __device__ inline uint32_t bin_log(uint32_t lb, uint32_t fl = kBinLog) 
 
 
 template <typename KeyT>
-__global__ __launch_bounds__(1024) void sched_bin_file(const SchedDev* __restrict__ sd, const int64_t* __restrict__ cand_h,
+__global__ __launch_bounds__(kBinFileThreads) void sched_bin_file(const SchedDev* __restrict__ sd, const int64_t* __restrict__ cand_h,
                                                        const KeyT* __restrict__ cand_k, const uint32_t* __restrict__ cand_i,
                                                        int64_t* __restrict__ ctl, int64_t cap,
                                                        const int64_t* __restrict__ set_h, const KeyT* __restrict__ set_k,
@@ -1386,7 +1390,7 @@ __global__ __launch_bounds__(1024) void sched_bin_file(const SchedDev* __restric
     const int64_t total = m + std::min<int64_t>((int64_t)__hip_atomic_load((const unsigned long long*)ctl,
                                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                                                 cap);
-    const int64_t base = (int64_t)blockIdx.x * (1024 * kBinTile);
+    const int64_t base = (int64_t)blockIdx.x * (kBinFileThreads * kBinTile);
     if (base >= total) return;  // whole workgroup
     const int64_t off = sd->off;
     cand_h += off;
@@ -1403,7 +1407,7 @@ __global__ __launch_bounds__(1024) void sched_bin_file(const SchedDev* __restric
     uint32_t eg[kBinTile], ebin[kBinTile], eloc[kBinTile];
 #pragma unroll
     for (int j = 0; j < kBinTile; ++j) {
-        const int64_t t = base + (int64_t)j * 1024 + threadIdx.x;
+        const int64_t t = base + (int64_t)j * kBinFileThreads + threadIdx.x;
         ebin[j] = 0xFFFFFFFFu;
         if (t < total) {
             if (t < m) {
@@ -2848,8 +2852,8 @@ static int sched_launch(DistinctState* d, const KeyT* keys, const int64_t* hashe
                            d->bak_h, (KeyT*)d->bak_k);
 #else
         const uint32_t C = 1u << bin_log((uint32_t)lb);
-        const unsigned fgrid = (unsigned)((k + cap + 1024 * kBinTile - 1) / (1024 * kBinTile));
-        hipLaunchKernelGGL(sched_bin_file<KeyT>, dim3(fgrid), dim3(1024), C * 4, st, (const SchedDev*)d->sdev,
+        const unsigned fgrid = (unsigned)((k + cap + kBinFileThreads * kBinTile - 1) / (kBinFileThreads * kBinTile));
+        hipLaunchKernelGGL(sched_bin_file<KeyT>, dim3(fgrid), dim3(kBinFileThreads), C * 4, st, (const SchedDev*)d->sdev,
                            (const int64_t*)(d->log_h + lbase), (const KeyT*)lk, (const uint32_t*)(d->log_i + lbase),
                            d->sctl, cap, (const int64_t*)d->set_h, (const KeyT*)d->set_k, k, d->sbh, bk, d->sbi,
                            d->bak_h, (KeyT*)d->bak_k);
