@@ -1643,6 +1643,20 @@ __global__ __launch_bounds__(1024) void publish_set_kernel(const uint32_t* __res
     publish_set_body(src, dst, ctl, k, key_words, flag, gen, ticket);
 }
 
+// First-occurrence flags of one segment for the host replay (rsv_host_values.h: only the first
+// occurrence of a key can be admitted): the replica's members at the segment's start followed by the
+// segment's keys in arrival order, stably sorted by key with their positions as values; entry t
+// keeps its flag when it heads its key's run (no member and no earlier entry carries the key).
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void mark_first(const KeyT* __restrict__ sk, const uint32_t* __restrict__ sv,
+                                                     int64_t total, uint32_t nm, uint8_t* __restrict__ flag) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += stride) {
+        const uint32_t v = sv[p];
+        if (v >= nm) flag[v - nm] = (p == 0 || sk[p] != sk[p - 1]) ? 1 : 0;
+    }
+}
+
 // one logged segment gathered into arrival order (perm from the radix sort of its arrival indices)
 template <typename KeyT>
 __global__ __launch_bounds__(kBlock) void permute_log(const uint32_t* __restrict__ perm, const int64_t* __restrict__ h,
@@ -2000,6 +2014,17 @@ struct DistinctState {
     int64_t ord_cap = 0;            // capacity of the two buffers above and of the pinned copies
     int64_t* ph = nullptr;          // pinned: hashes, keys (as KeyT) of one segment in arrival order
     void* pk = nullptr;
+    // first-occurrence flags (segment_to_host with `first`): members + segment keys, sorted copies,
+    // their positions, the flags on the device and pinned, the members' pinned staging
+    void* fk_in = nullptr;
+    void* fk_out = nullptr;
+    uint32_t* fv = nullptr;
+    uint8_t* fflag = nullptr;
+    uint8_t* pflag = nullptr;
+    void* pmem = nullptr;
+    int64_t fcap = 0;               // capacity (entries) of fk_in / fk_out / fv; fflag / pflag hold ord_cap
+    int64_t pmem_cap = 0;
+    int64_t first_min = 4096;       // segments at least this long replay through the flags (no host set)
     // Exact multi-rank merge of ordered samplers (rsv_export_log / rsv_merge_log): the candidates
     // the replica consumed (arrival order, host) + the segments still in the log, and the segments
     // logged before the last merge -- together every candidate logged since creation (`arch_ok`).
@@ -2130,6 +2155,8 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
         d->log_limit = std::max<int64_t>(d->cand_limit, std::atoll(v));
     if (const char* v = std::getenv("RSV_ORDERED_SCHED")) d->sched = v[0] != '0';
     if (const char* v = std::getenv("RSV_SCHED_BETA")) d->sched_beta = std::atof(v);
+    if (const char* v = std::getenv("RSV_FIRST_MIN"))  // test hook: which replay form serves small segments
+        d->first_min = std::max<int64_t>(1, std::atoll(v));
     if (const char* v = std::getenv("RSV_SPEC_MIN_BATCH"))  // test hook: speculative publication
         d->spec_min = std::max<int64_t>(1, std::atoll(v));
     hipError_t e = hipSuccess;
@@ -2185,12 +2212,14 @@ void distinct_destroy(DistinctState* d) {
     void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->ctl, d->bh, d->bk, d->mh0, d->mh1, d->mk0,
                   d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp, d->log_h, d->log_k, d->log_i,
                   d->perm, d->sorted_i, d->ord_h, d->ord_k, d->sdev, d->sctl, d->sbh, d->sbk, d->sbi, d->vacc,
-                  d->bak_h, d->bak_k, d->mstart};
+                  d->bak_h, d->bak_k, d->mstart, d->fk_in, d->fk_out, d->fv, d->fflag};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
     pool_host_free(d->h_pinned);
     pool_host_free(d->hc);
     pool_host_free(d->ph);
     pool_host_free(d->pk);
+    pool_host_free(d->pflag);
+    pool_host_free(d->pmem);
     pool_host_free(d->shc);
     delete d;
 }
@@ -2599,6 +2628,10 @@ static hipError_t ensure_ordered(DistinctState* d, int64_t cap, hipStream_t st) 
     d->pk = nullptr;
     if ((e = pool_host_alloc((void**)&d->ph, (size_t)cap * 8, hipHostMallocDefault))) return e;
     if ((e = pool_host_alloc(&d->pk, (size_t)cap * d->kw, hipHostMallocDefault))) return e;
+    if ((e = grow((void**)&d->fflag, 0, (size_t)cap, false, st))) return e;
+    pool_host_free(d->pflag);
+    d->pflag = nullptr;
+    if ((e = pool_host_alloc((void**)&d->pflag, (size_t)cap, hipHostMallocDefault))) return e;
     size_t tb = 0;
     if ((e = rocprim::radix_sort_pairs(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                        rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (size_t)cap)))
@@ -2660,8 +2693,36 @@ static hipError_t upload_replica(DistinctState* d, hipStream_t st) {
 // the chunk-relative index restores the order, and the permutation is applied on the device, so
 // the host reads the segment sequentially (two random reads per element from a ~20 MB log cost
 // more than the replica's heap).
+// the first-occurrence sort's buffers for `total` entries (members + one segment)
 template <typename KeyT>
-static hipError_t segment_to_host(DistinctState* d, const DistinctState::Seg& g, hipStream_t st) {
+static hipError_t ensure_first(DistinctState* d, int64_t nm, int64_t total, hipStream_t st) {
+    hipError_t e;
+    if (nm > d->pmem_cap) {
+        const int64_t c = std::min<int64_t>(d->k, std::max<int64_t>(nm, 2 * d->pmem_cap));
+        pool_host_free(d->pmem);
+        d->pmem = nullptr;
+        d->pmem_cap = 0;
+        if ((e = pool_host_alloc(&d->pmem, (size_t)c * sizeof(KeyT), hipHostMallocDefault))) return e;
+        d->pmem_cap = c;
+    }
+    if (total <= d->fcap) return hipSuccess;
+    if ((e = grow(&d->fk_in, 0, (size_t)total * sizeof(KeyT), false, st))) return e;
+    if ((e = grow(&d->fk_out, 0, (size_t)total * sizeof(KeyT), false, st))) return e;
+    if ((e = grow((void**)&d->fv, 0, (size_t)total * 4, false, st))) return e;
+    size_t tb = 0;
+    if ((e = rocprim::radix_sort_pairs(nullptr, tb, (KeyT*)nullptr, (KeyT*)nullptr,
+                                       rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (size_t)total)))
+        return e;
+    if (tb > d->temp_bytes) {
+        if ((e = grow(&d->temp, 0, tb, false, st))) return e;
+        d->temp_bytes = tb;
+    }
+    d->fcap = total;
+    return hipSuccess;
+}
+
+template <typename KeyT>
+static hipError_t segment_to_host(DistinctState* d, const DistinctState::Seg& g, hipStream_t st, bool first) {
     hipError_t e;
     if ((e = ensure_ordered(d, g.c, st))) return e;
     unsigned bits = 1;
@@ -2674,6 +2735,25 @@ static hipError_t segment_to_host(DistinctState* d, const DistinctState::Seg& g,
                        dim3(kBlock), 0, st, d->perm, d->log_h + g.off, (const KeyT*)d->log_k + g.off, g.c, d->ord_h,
                        (KeyT*)d->ord_k);
     if ((e = hipGetLastError())) return e;
+    if (first) {
+        const int64_t nm = d->rep.size(), total = nm + g.c;
+        if ((e = ensure_first<KeyT>(d, nm, total, st))) return e;
+        KeyT* pm = (KeyT*)d->pmem;
+        for (int64_t i = 0; i < nm; ++i) pm[i] = (KeyT)d->rep.he[(size_t)i + 1];
+        if (nm && (e = hipMemcpyAsync(d->fk_in, pm, (size_t)nm * sizeof(KeyT), hipMemcpyHostToDevice, st))) return e;
+        if ((e = hipMemcpyAsync((KeyT*)d->fk_in + nm, d->ord_k, (size_t)g.c * sizeof(KeyT), hipMemcpyDeviceToDevice, st)))
+            return e;
+        size_t fb = d->temp_bytes;
+        if ((e = rocprim::radix_sort_pairs(d->temp, fb, (KeyT*)d->fk_in, (KeyT*)d->fk_out,
+                                           rocprim::counting_iterator<uint32_t>(0), d->fv, (size_t)total, 0,
+                                           8 * (unsigned)sizeof(KeyT), st)))
+            return e;
+        hipLaunchKernelGGL(mark_first<KeyT>, dim3((unsigned)std::min<int64_t>((total + kBlock - 1) / kBlock, 8192)),
+                           dim3(kBlock), 0, st, (const KeyT*)d->fk_out, (const uint32_t*)d->fv, total, (uint32_t)nm,
+                           d->fflag);
+        if ((e = hipGetLastError())) return e;
+        if ((e = hipMemcpyAsync(d->pflag, d->fflag, (size_t)g.c, hipMemcpyDeviceToHost, st))) return e;
+    }
     if ((e = hipMemcpyAsync(d->ph, d->ord_h, (size_t)g.c * 8, hipMemcpyDeviceToHost, st))) return e;
     if ((e = hipMemcpyAsync(d->pk, d->ord_k, (size_t)g.c * sizeof(KeyT), hipMemcpyDeviceToHost, st))) return e;
     return hipStreamSynchronize(st);
@@ -2714,7 +2794,8 @@ static hipError_t replay_log(DistinctState* d, hipStream_t st) {
     if (d->rep_stale && (e = rebuild_replica<KeyT>(d, st))) return e;
     for (const DistinctState::Seg& g : d->segs) {
         if (g.c == 0) continue;
-        if ((e = segment_to_host<KeyT>(d, g, st))) return e;
+        const bool first = g.c >= d->first_min;
+        if ((e = segment_to_host<KeyT>(d, g, st, first))) return e;
         const KeyT* pk = (const KeyT*)d->pk;
         const int64_t* ph = d->ph;
         if (d->retain && d->arch_ok) {
@@ -2726,7 +2807,11 @@ static hipError_t replay_log(DistinctState* d, hipStream_t st) {
                 else d->arch_k4.insert(d->arch_k4.end(), pk, pk + g.c);
             }
         }
-        d->rep.sample_run(g.c, [&](int64_t t) { return (int64_t)pk[t]; }, [&](int64_t t) { return ph[t]; });
+        if (first)
+            d->rep.sample_run_unique(g.c, d->pflag, [&](int64_t t) { return (int64_t)pk[t]; },
+                                     [&](int64_t t) { return ph[t]; });
+        else
+            d->rep.sample_run(g.c, [&](int64_t t) { return (int64_t)pk[t]; }, [&](int64_t t) { return ph[t]; });
     }
     d->segs.clear();
     if (d->pre_segs.empty()) d->log_n = 0;  // else the log still holds the pre-merge segments
@@ -3462,7 +3547,7 @@ static int log_export_impl(DistinctState* d, int64_t bound, int64_t* out_h, KeyT
     for (const std::vector<DistinctState::Seg>* v : {&d->pre_segs, &d->segs})
         for (const DistinctState::Seg& g : *v) {
             if (g.c == 0) continue;
-            if (hipError_t e = segment_to_host<KeyT>(d, g, st)) {
+            if (hipError_t e = segment_to_host<KeyT>(d, g, st, false)) {
                 set_error(std::string("rsv_export_log: ") + hipGetErrorString(e));
                 return e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;
             }

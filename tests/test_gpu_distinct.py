@@ -255,6 +255,33 @@ def test_ordered_eager_log_replay(cuda, oracle, monkeypatch):
         assert d.result().tolist() == want
 
 
+@pytest.mark.parametrize("first_min", ["1", "1000000000"])
+def test_ordered_first_occurrence_replay(cuda, oracle, monkeypatch, first_min):
+    """The host replay of a logged segment either probes the member set per candidate or runs the
+    heap alone over the device's first-occurrence flags (a key that repeats an earlier candidate of
+    the segment or a member at its start can never be admitted).  RSV_FIRST_MIN (test hook, read at
+    creation) picks the form for every segment; eager replays (RSV_ORDERED_LOG_LIMIT) and a reusable
+    sampler give many segments whose candidates repeat members and each other: the same set."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    monkeypatch.setenv("RSV_FIRST_MIN", first_min)
+    rng = np.random.default_rng(21)
+    base = _colliding(rng, 300_000, 2000)
+    vals = np.concatenate([base, base[rng.integers(0, base.size, size=200_000)]])
+    rng.shuffle(vals)
+    for limit in (None, "1"):
+        if limit:
+            monkeypatch.setenv("RSV_ORDERED_LOG_LIMIT", limit)
+        ref = oracle.Distinct(500, 9, oracle.HASH_JAVA_LONG)
+        r = Sampler.distinct(500, seed=9, reusable=True)()
+        for part in np.array_split(vals, 4):
+            r.sample_all(torch.from_numpy(part).to(cuda))
+            ref.sample_all(part)
+            assert r.result().tolist() == ref.result()[0].tolist(), (first_min, limit)
+
+
 def test_precomputed_hash(cuda, oracle):
     from reservoir_amd import Sampler
 
