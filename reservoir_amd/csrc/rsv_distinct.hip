@@ -2663,36 +2663,33 @@ static hipError_t ensure_log(DistinctState* d, int64_t need, hipStream_t st) {
 // result / export / merge read the same place in both modes.
 template <typename KeyT>
 static hipError_t upload_replica(DistinctState* d, hipStream_t st) {
-    std::vector<HostValues::Ent> es;
-    for (int64_t i = 1; i <= d->rep.size(); ++i) es.push_back(HostValues::Ent{d->rep.he[(size_t)i], d->rep.hh[(size_t)i]});
-    std::sort(es.begin(), es.end(), [](const HostValues::Ent& a, const HostValues::Ent& b) {
-        return a.h != b.h ? a.h < b.h : a.elem < b.elem;
-    });
-    const int64_t m = (int64_t)es.size();
+    // the heap's entries go up in heap order and are put in ascending (h, key) order on the device by
+    // two stable radix sorts, key then h (a host std::sort of k = 65536 entries took ~3 ms)
+    const int64_t m = d->rep.size();
     hipError_t e = ensure_caps(d, 0, m, st);
     if (e != hipSuccess || m == 0) {
         d->m = 0;
         return e;
     }
-    std::vector<int64_t> hh((size_t)m);
     std::vector<KeyT> kk((size_t)m);
-    for (int64_t i = 0; i < m; ++i) {
-        hh[(size_t)i] = es[(size_t)i].h;
-        kk[(size_t)i] = (KeyT)es[(size_t)i].elem;
-    }
-    if ((e = hipMemcpyAsync(d->set_h, hh.data(), (size_t)m * 8, hipMemcpyHostToDevice, st))) return e;
-    if ((e = hipMemcpyAsync(d->set_k, kk.data(), (size_t)m * sizeof(KeyT), hipMemcpyHostToDevice, st))) return e;
-    if ((e = hipStreamSynchronize(st))) return e;  // the host vectors go out of scope
+    for (int64_t i = 0; i < m; ++i) kk[(size_t)i] = (KeyT)d->rep.he[(size_t)i + 1];
+    if ((e = hipMemcpyAsync(d->mh0, d->rep.hh.data() + 1, (size_t)m * 8, hipMemcpyHostToDevice, st))) return e;
+    if ((e = hipMemcpyAsync(d->mk0, kk.data(), (size_t)m * sizeof(KeyT), hipMemcpyHostToDevice, st))) return e;
+    size_t tb = d->temp_bytes;
+    if ((e = rocprim::radix_sort_pairs(d->temp, tb, (KeyT*)d->mk0, (KeyT*)d->mk1, d->mh0, d->mh1, (size_t)m, 0,
+                                       8 * (unsigned)sizeof(KeyT), st)))
+        return e;
+    tb = d->temp_bytes;
+    if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->mh1, d->set_h, (KeyT*)d->mk1, (KeyT*)d->set_k, (size_t)m, 0,
+                                       64, st)))
+        return e;
+    if ((e = hipStreamSynchronize(st))) return e;  // kk goes out of scope
     d->m = m;
     d->max_h = d->rep.max_hash;
-    d->set_top = hh[(size_t)m - 1];
+    d->set_top = d->rep.hh[1];  // the heap's root: the set's largest hash
     return hipSuccess;
 }
 
-// One logged segment in arrival order into the pinned host copies d->ph / d->pk: a radix sort by
-// the chunk-relative index restores the order, and the permutation is applied on the device, so
-// the host reads the segment sequentially (two random reads per element from a ~20 MB log cost
-// more than the replica's heap).
 // the first-occurrence sort's buffers for `total` entries (members + one segment)
 template <typename KeyT>
 static hipError_t ensure_first(DistinctState* d, int64_t nm, int64_t total, hipStream_t st) {
@@ -2721,6 +2718,10 @@ static hipError_t ensure_first(DistinctState* d, int64_t nm, int64_t total, hipS
     return hipSuccess;
 }
 
+// One logged segment in arrival order into the pinned host copies d->ph / d->pk: a radix sort by
+// the chunk-relative index restores the order, and the permutation is applied on the device, so
+// the host reads the segment sequentially (two random reads per element from a ~20 MB log cost
+// more than the replica's heap).  With `first`, also its first-occurrence flags into d->pflag.
 template <typename KeyT>
 static hipError_t segment_to_host(DistinctState* d, const DistinctState::Seg& g, hipStream_t st, bool first) {
     hipError_t e;
@@ -2795,7 +2796,10 @@ static hipError_t replay_log(DistinctState* d, hipStream_t st) {
     for (const DistinctState::Seg& g : d->segs) {
         if (g.c == 0) continue;
         const bool first = g.c >= d->first_min;
+        static const bool debug = std::getenv("RSV_REPLAY_DEBUG") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
         if ((e = segment_to_host<KeyT>(d, g, st, first))) return e;
+        const auto t1 = std::chrono::steady_clock::now();
         const KeyT* pk = (const KeyT*)d->pk;
         const int64_t* ph = d->ph;
         if (d->retain && d->arch_ok) {
@@ -2812,6 +2816,16 @@ static hipError_t replay_log(DistinctState* d, hipStream_t st) {
                                      [&](int64_t t) { return ph[t]; });
         else
             d->rep.sample_run(g.c, [&](int64_t t) { return (int64_t)pk[t]; }, [&](int64_t t) { return ph[t]; });
+        if (debug) {
+            const auto t2 = std::chrono::steady_clock::now();
+            int64_t kept = 0;
+            if (first)
+                for (int64_t t = 0; t < g.c; ++t) kept += d->pflag[t];
+            std::fprintf(stderr, "[rsv replay] candidates=%lld first=%d kept=%lld to_host_us=%.1f run_us=%.1f\n",
+                         (long long)g.c, (int)first, (long long)kept,
+                         std::chrono::duration<double, std::micro>(t1 - t0).count(),
+                         std::chrono::duration<double, std::micro>(t2 - t1).count());
+        }
     }
     d->segs.clear();
     if (d->pre_segs.empty()) d->log_n = 0;  // else the log still holds the pre-merge segments
@@ -3277,8 +3291,15 @@ int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* ha
 int distinct_finalize(DistinctState* d, hipStream_t st) {
     if (int rc = distinct_settle(d, st)) return rc;
     if (!d->ordered || d->exact) return RSV_OK;
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = d->kw == 8 ? replay_log<int64_t>(d, st) : replay_log<int32_t>(d, st);
+    const auto t1 = std::chrono::steady_clock::now();
     if (e == hipSuccess) e = d->kw == 8 ? upload_replica<int64_t>(d, st) : upload_replica<int32_t>(d, st);
+    static const bool debug = std::getenv("RSV_REPLAY_DEBUG") != nullptr;
+    if (debug)
+        std::fprintf(stderr, "[rsv replay] finalize: replay_us=%.1f upload_us=%.1f\n",
+                     std::chrono::duration<double, std::micro>(t1 - t0).count(),
+                     std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count());
     if (e != hipSuccess) {
         set_error(std::string("distinct (ordered) replay: ") + hipGetErrorString(e));
         return e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;
