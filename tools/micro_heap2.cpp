@@ -7,6 +7,8 @@
 #include <cstdio>
 #include <cstring>
 #include <vector>
+#include <sys/mman.h>
+#include <cstdlib>
 
 #include "../reservoir_amd/csrc/rsv_host_values.h"
 
@@ -279,6 +281,137 @@ struct SeenReplica : HeapOnly<1> {
     }
 };
 
+// heap-only, branch-free fixDown: the larger-child path (left on ties) to the last complete level
+// (plus one step into a partial level), the moves counted as the path entries above the sinking
+// hash (the path's hashes only fall), every path node rewritten with a selected value
+struct Branchless : HeapOnly<0> {
+    using HeapOnly<0>::HeapOnly;
+    void dequeue() {
+        int64_t* H = hh.data();
+        int64_t* E = he.data();
+        const int64_t h = H[n], e = E[n];
+        const int64_t nn = --n;
+        if (nn == 0) return;
+        H[nn + 1] = h;
+        const int L = 63 - __builtin_clzll((uint64_t)nn + 1);  // complete levels
+        int64_t pp[64], pv[64];
+        int64_t p = 1;
+        int D = L - 1;
+        for (int d = 0; d < D; ++d) {
+            int64_t c = 2 * p;
+            const int64_t a = H[c], b = H[c + 1];
+            const bool s = a < b;
+            c += s;
+            pv[d] = s ? b : a;
+            pp[d] = c;
+            p = c;
+        }
+        if (2 * p <= nn) {
+            int64_t c = 2 * p;
+            const int64_t a = H[c], b = H[c + 1];
+            const bool s = a < b;
+            c += s;
+            pv[D] = s ? b : a;
+            pp[D] = c;
+            ++D;
+        }
+        int m = 0;
+        for (int d = 0; d < D; ++d) m += pv[d] > h;
+        // moves: node_d (node_0 = 1, node_{d+1} = pp[d]) takes the entry of node_{d+1} for d < m;
+        // node_m takes the sinking entry
+        int64_t node = 1;
+        for (int d = 0; d < m; ++d) {
+            H[node] = pv[d];
+            E[node] = E[pp[d]];
+            node = pp[d];
+        }
+        H[node] = h;
+        E[node] = e;
+    }
+    void run(int64_t c, const int64_t* ek, const int64_t* eh) {
+        int64_t t = 0;
+        for (; t < c && n < k; ++t) {
+            add(ek[t], eh[t]);
+            if (eh[t] > max_hash) max_hash = eh[t];
+        }
+        for (; t < c; ++t) {
+            const int64_t h = eh[t];
+            if (h < max_hash) {
+                dequeue();
+                add(ek[t], h);
+                max_hash = hh[1];
+            }
+        }
+    }
+};
+
+// heap-only over arrays in one 2 MB-aligned block advised as a huge page (the deep levels' lines are
+// on 128 different 4 KB pages otherwise)
+template <int PF>
+struct HugeHeap {
+    int64_t* H;
+    int64_t* E;
+    int64_t k, n = 0, max_hash = INT64_MIN, cap;
+    std::vector<int64_t> hh, he;  // copies for the check
+    explicit HugeHeap(int64_t kk) : k(kk) {
+        cap = ((kk + 2) * 8 + (2 << 20) - 1) / (2 << 20) * (2 << 20);
+        void* m = std::aligned_alloc(2 << 20, 2 * cap);
+        madvise(m, 2 * cap, MADV_HUGEPAGE);
+        std::memset(m, 0, 2 * cap);
+        H = (int64_t*)m;
+        E = (int64_t*)((char*)m + cap);
+    }
+    void add(int64_t e, int64_t h) {
+        int64_t m = ++n;
+        while (m > 1 && H[m >> 1] < h) {
+            H[m] = H[m >> 1];
+            E[m] = E[m >> 1];
+            m >>= 1;
+        }
+        H[m] = h;
+        E[m] = e;
+    }
+    void dequeue() {
+        const int64_t h = H[n], e = E[n];
+        const int64_t nn = --n;
+        H[nn + 1] = h;
+        const int64_t last = cap / 8 - 1;
+        int64_t kk = 1;
+        while (nn >= 2 * kk) {
+            int64_t j = 2 * kk;
+            __builtin_prefetch(H + std::min(4 * j, last));
+            if (PF >= 2) {
+                __builtin_prefetch(H + std::min(8 * j, last));
+                __builtin_prefetch(H + std::min(8 * j + 8, last));
+            }
+            j += H[j] < H[j + 1];
+            if (h >= H[j]) break;
+            H[kk] = H[j];
+            E[kk] = E[j];
+            kk = j;
+        }
+        H[kk] = h;
+        E[kk] = e;
+    }
+    void run(int64_t c, const int64_t* ek, const int64_t* eh) {
+        int64_t t = 0;
+        for (; t < c && n < k; ++t) {
+            add(ek[t], eh[t]);
+            if (eh[t] > max_hash) max_hash = eh[t];
+        }
+        for (; t < c; ++t) {
+            const int64_t h = eh[t];
+            if (h < max_hash) {
+                dequeue();
+                add(ek[t], h);
+                max_hash = H[1];
+            }
+        }
+        hh.assign(H, H + k + 2);
+        he.assign(E, E + k + 2);
+    }
+};
+
 template <class F>
 static double timed(F f) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -335,6 +468,15 @@ int main(int argc, char** argv) {
         const double t6 = timed([&] { w3.run(c, lk.data(), lh.data()); });
         SeenReplica sr(k);
         const double t7 = timed([&] { sr.run(c, lk.data(), lh.data()); });
+        HugeHeap<1> hg1(k);
+        const double t9 = timed([&] { hg1.run(c, lk.data(), lh.data()); });
+        HugeHeap<2> hg2(k);
+        const double t10 = timed([&] { hg2.run(c, lk.data(), lh.data()); });
+        std::printf("huge page %.1f (%d) +deep prefetch %.1f (%d)\n", t9, (int)check(hg1.hh, hg1.he), t10,
+                    (int)check(hg2.hh, hg2.he));
+        Branchless bl(k);
+        const double t8 = timed([&] { bl.run(c, lk.data(), lh.data()); });
+        std::printf("branchless descent %.1f (%d)\n", t8, (int)check(bl.hh, bl.he));
         std::printf("seen-set replica %.1f (%d)\n", t7, (int)check(sr.hh, sr.he));
         std::printf("ahead2 %.1f (%d) ahead3 %.1f (%d)\n", t5, (int)check(w2.hh, w2.he), t6, (int)check(w3.hh, w3.he));
         std::printf("library %.1f ms | heap-only %.1f (%d) | +deep prefetch %.1f (%d) | +E prefetch %.1f (%d) | bottom-up %.1f (%d)\n",
