@@ -2795,7 +2795,9 @@ static hipError_t replay_log(DistinctState* d, hipStream_t st) {
     if (d->rep_stale && (e = rebuild_replica<KeyT>(d, st))) return e;
     for (const DistinctState::Seg& g : d->segs) {
         if (g.c == 0) continue;
-        const bool first = g.c >= d->first_min;
+        // (the flags' sort holds the members too: ~20 B per entry on the device, so a huge replica
+        // keeps the set-based form)
+        const bool first = g.c >= d->first_min && d->rep.size() + g.c <= ((int64_t)1 << 28);
         static const bool debug = std::getenv("RSV_REPLAY_DEBUG") != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
         if ((e = segment_to_host<KeyT>(d, g, st, first))) return e;
