@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-4 evidence run (one gpurun call): GPU suite + smoke, the default bench line, rocprofv3
+# Round-4 evidence run: the default bench line, rocprofv3
 # kernel stats + PMC passes for K1 (C2) and K2 (C3), the C4 ordered timeline, the device combine,
-# and a 2-rank gloo rehearsal of the N>1 bench.  Summaries: tools/collect_profiles.py and
+# and a 2-rank gloo rehearsal of the N>1 bench (the GPU suite + smoke: scripts/gpu_r04_check.sh).  Summaries: tools/collect_profiles.py and
 # tools/timeline.py -> profiles/r04/
 OUT=${OUT:-r04z}
 P="rocprofv3 --output-format csv"
@@ -9,8 +9,6 @@ SQ="GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYC
 B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary"
 D=gpurun_out/$OUT
 exec scripts/gpu_run.sh $OUT \
-  pytest 900 python3 -u -m pytest tests -m gpu -q -rfE -x --timeout 300 --timeout-method thread :: \
-  smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" :: \
   bench 600 python3 bench.py :: \
   k1_trace 200 $P --kernel-trace --stats -d $D/k1 -o k1 -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-secondary :: \
   k1_pmc_sq 120 $P --pmc $SQ --kernel-trace -d $D/k1_sq -o pmc -- $B :: \
@@ -21,4 +19,5 @@ exec scripts/gpu_run.sh $OUT \
   c4_trace 200 $P --kernel-trace --stats -d $D/c4 -o c4 -- python3 tools/bench_paths.py --only c4o :: \
   paths 300 python3 tools/bench_paths.py --only c4,c4r,c2i,c4m,c3k :: \
   rehearse 500 env RSV_BENCH_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node=2 \
-      --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --c4-steps 3 --no-cpu-baseline
+      --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --c4-steps 3 --no-cpu-baseline :: \
+  trim 30 find $D -name "*_kernel_trace.csv" -size +4M -delete
