@@ -282,6 +282,28 @@ def test_ordered_first_occurrence_replay(cuda, oracle, monkeypatch, first_min):
             assert r.result().tolist() == ref.result()[0].tolist(), (first_min, limit)
 
 
+def test_ordered_first_occurrence_replay_int_keys(cuda, monkeypatch):
+    """The flags form with 4-byte keys (a colliding precomputed hash, so the replay runs): the same
+    set as the set-based form, and as the same stream sampled as Long keys (the scrambled hash
+    depends on the hash value only)."""
+    from reservoir_amd import Sampler
+
+    rng = np.random.default_rng(4)
+    xs = rng.integers(-2**31, 2**31 - 1, size=6_000).astype(np.int64)
+    xs = np.concatenate([xs, xs[rng.integers(0, xs.size, size=3_000)]]).tolist()
+    got = []
+    for first_min, key_type in (("1", "int"), ("1000000000", "int"), ("1", "long")):
+        monkeypatch.setenv("RSV_FIRST_MIN", first_min)
+        monkeypatch.setenv("RSV_ORDERED_LOG_LIMIT", "1")
+        d = Sampler.distinct(40, seed=12, key_type=key_type)(hash=lambda x: x % 211)
+        d.sample_all(xs)
+        info = d.distinct_info()
+        got.append(sorted(int(v) for v in d.result().tolist()))
+        assert info["ordered"] and info["tied"]  # the boundary bucket is oversubscribed: replayed
+    assert got[0] == got[1] == got[2]
+    assert len(got[0]) == 40
+
+
 def test_precomputed_hash(cuda, oracle):
     from reservoir_amd import Sampler
 
