@@ -16,7 +16,8 @@ def main(path: str) -> None:
         sys.exit("no scheduled pass in the trace")
     i = idx[-2]
     j = i
-    while j > 0 and "k3_filter" not in rows[j]["Kernel_Name"]:
+    # the heap-filling chunk's filter: k3_filter, or hash_all when it has no bound (round 4)
+    while j > 0 and "k3_filter" not in rows[j]["Kernel_Name"] and "hash_all" not in rows[j]["Kernel_Name"]:
         j -= 1
     end = i
     while end + 1 < len(rows) and "publish" not in rows[end]["Kernel_Name"]:
