@@ -204,3 +204,71 @@ JNIEXPORT void JNICALL JNI_FN(sampleIndexed)(JNIEnv* env, jobject self, jlong s,
 
 FILL_ARRAY(fillLongs, jlongArray, jlong, GetLongArrayRegion)
 FILL_ARRAY(fillInts, jintArray, jint, GetIntArrayRegion)
+
+/* fixed-width byte keys (java.util.UUID: key_width 16) travel as key_width / 8 Longs per key, in
+ * key order: sampleWords / resultWords / fillWords are the Long-array forms above with n counting
+ * keys, not array elements */
+JNIEXPORT void JNICALL JNI_FN(sampleWords)(JNIEnv* env, jobject self, jlong s, jlongArray words, jlongArray hashes,
+                                           jint n) {
+    (void)self;
+    const jint w = session(s)->key_width / 8;
+    jint done = 0;
+    while (done < n) {
+        void* kb = NULL;
+        int64_t* hb = NULL;
+        int64_t room = 0;
+        rsv_status st = rsv_jvm_stage_span(session(s), &kb, &hb, &room);
+        if (st != RSV_OK) {
+            throw_status(env, st);
+            return;
+        }
+        const jint c = room < (int64_t)(n - done) ? (jint)room : n - done;
+        (*env)->GetLongArrayRegion(env, words, done * w, c * w, (jlong*)kb);
+        if (hb && hashes) (*env)->GetLongArrayRegion(env, hashes, done, c, (jlong*)hb);
+        if ((*env)->ExceptionCheck(env)) return;
+        if (hb && !hashes) {
+            throw_status(env, RSV_E_NULL_POINTER);
+            return;
+        }
+        rsv_jvm_stage_advance(session(s), c);
+        done += c;
+    }
+}
+
+JNIEXPORT jint JNICALL JNI_FN(resultWords)(JNIEnv* env, jobject self, jlong s, jlongArray out) {
+    (void)self;
+    const jint w = session(s)->key_width / 8;
+    const jsize len = (*env)->GetArrayLength(env, out);
+    jlong* buf = (jlong*)malloc((size_t)(len > 0 ? len : 1) * sizeof(jlong));
+    if (!buf) {
+        throw_status(env, RSV_E_OUT_OF_MEMORY);
+        return 0;
+    }
+    int64_t n = 0;
+    rsv_status st = rsv_jvm_result(session(s), buf, len / w, &n);
+    if (st == RSV_OK) (*env)->SetLongArrayRegion(env, out, 0, (jsize)(n * w), buf);
+    free(buf);
+    if (st != RSV_OK) throw_status(env, st);
+    return (jint)n;
+}
+
+JNIEXPORT void JNICALL JNI_FN(fillWords)(JNIEnv* env, jobject self, jlong s, jlongArray keys) {
+    (void)self;
+    const jint kw = session(s)->k * (session(s)->key_width / 8);
+    jlong* buf = (jlong*)malloc((size_t)kw * sizeof(jlong));
+    if (!buf) {
+        throw_status(env, RSV_E_OUT_OF_MEMORY);
+        return;
+    }
+    (*env)->GetLongArrayRegion(env, keys, 0, kw, buf);
+    rsv_status st = (*env)->ExceptionCheck(env) ? RSV_OK : rsv_jvm_fill_slots(session(s), buf);
+    free(buf);
+    if (st != RSV_OK) throw_status(env, st);
+}
+
+/* `map` threw while the keys of an index-only batch were owed: drop the batch (the JVM rethrows) */
+JNIEXPORT void JNICALL JNI_FN(abortIndexed)(JNIEnv* env, jobject self, jlong s) {
+    (void)self;
+    rsv_status st = rsv_jvm_abort_indexed(session(s));
+    if (st != RSV_OK) throw_status(env, st);
+}

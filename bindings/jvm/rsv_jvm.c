@@ -127,6 +127,12 @@ rsv_status rsv_jvm_fill_slots(rsv_jvm* s, const void* keys) {
     return rsv_fill_slots(s->h, keys);
 }
 
+rsv_status rsv_jvm_abort_indexed(rsv_jvm* s) {
+    g_local_error = 0;
+    if (!s->open) return closed();
+    return rsv_abort_indexed(s->h);
+}
+
 rsv_status rsv_jvm_result(rsv_jvm* s, void* out, int64_t cap, int64_t* out_n) {
     g_local_error = 0;
     if (!s->open) return closed();

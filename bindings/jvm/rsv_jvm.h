@@ -30,7 +30,7 @@ typedef struct rsv_jvm {
     rsv_sampler* h;       /* NULL once a single-use result() has destroyed the handle */
     int32_t open;         /* Sampler.isOpen */
     int32_t reusable;     /* MultiResult* (S:353-381, :430-433): result() keeps the handle */
-    int32_t k, key_width;
+    int32_t k, key_width; /* key_width 4 (Int), 8 (Long) or 16..256 (byte keys: UUID = 16) */
     int32_t precomputed;  /* RSV_HASH_PRECOMPUTED: a caller hash rides beside every key */
     uint8_t* stage;       /* acquired pinned staging (engine-owned): keys */
     int64_t* stage_hash;  /*   and hashes (precomputed only) */
@@ -54,6 +54,9 @@ void rsv_jvm_stage_advance(rsv_jvm* s, int64_t n);
  * keys[slot] (a k-key array, other entries ignored) and passes it to rsv_jvm_fill_slots. */
 rsv_status rsv_jvm_sample_indexed(rsv_jvm* s, int64_t n, int64_t* slot_offsets);
 rsv_status rsv_jvm_fill_slots(rsv_jvm* s, const void* keys);
+/* `map` threw on an element owed after rsv_jvm_sample_indexed: drop that batch (rsv_abort_indexed)
+ * so the sampler stays usable; the binding rethrows the exception */
+rsv_status rsv_jvm_abort_indexed(rsv_jvm* s);
 /* Sampler.result (S:59-60): writes min(count, k) keys; a single-use sampler closes (S:345-350) */
 rsv_status rsv_jvm_result(rsv_jvm* s, void* out, int64_t cap, int64_t* out_n);
 /* zero-copy form for a producer that writes keys itself (keys-only samplers): the free tail of

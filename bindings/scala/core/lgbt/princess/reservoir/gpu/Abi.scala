@@ -2,10 +2,11 @@ package lgbt.princess.reservoir.gpu
 
 import scala.reflect.ClassTag
 
-/** Constants of the C ABI (include/reservoir_hip.h) and the primitive key kinds the engine stores.
+/** Constants of the C ABI (include/reservoir_hip.h) and the key kinds the engine stores.
   *
-  * The engine keeps primitive keys only: `B = Long` (8 bytes) or `B = Int` (4 bytes), which `map`
-  * extracts on the JVM (Sampler.scala:115-116 allows `map` to run more than `maxSampleSize` times).
+  * The engine keeps fixed-width keys only: `B = Long` (8 bytes), `B = Int` (4 bytes) or
+  * `B = java.util.UUID` (16 bytes, [mostSigBits | leastSigBits]), which `map` extracts on the JVM
+  * (Sampler.scala:115-116 allows `map` to run more than `maxSampleSize` times).
   */
 private[reservoir] object Abi {
   // rsv_status -> the reference's exceptions (Sampler.scala:80-82, :94, :186)
@@ -23,7 +24,7 @@ private[reservoir] object Abi {
   final val EnginePhiloxR = 0
   final val EngineJavaL   = 1
   // rsv_hash_kind
-  final val HashDefault     = 0 // B#hashCode().toLong (Sampler.scala:75): the engine folds it on the GPU
+  final val HashDefault     = 0 // B#hashCode().toLong (Sampler.scala:75): Long / Int / UUID hashCode on the GPU
   final val HashIdentity    = 1
   final val HashJavaLong    = 2
   final val HashJavaInt     = 3
@@ -50,9 +51,16 @@ private[reservoir] object KeyKind {
   case object LongKey extends KeyKind[Long](8)
   case object IntKey  extends KeyKind[Int](4)
 
+  /** java.util.UUID as two Longs, [mostSigBits | leastSigBits]: UUID.equals is equality of both
+    * words, so the engine's byte equality is the reference's `elements.contains` (Sampler.scala:398,
+    * :403), and its default hash is UUID.hashCode computed on the GPU.  (An Array[Byte] has
+    * reference equality in a Scala Set: it never maps to a key kind and stays on the JVM classes.) */
+  case object UuidKey extends KeyKind[java.util.UUID](16)
+
   def of[B](implicit ct: ClassTag[B]): Option[KeyKind[B]] =
     if (ct == ClassTag.Long) Some(LongKey.asInstanceOf[KeyKind[B]])
     else if (ct == ClassTag.Int) Some(IntKey.asInstanceOf[KeyKind[B]])
+    else if (ct.runtimeClass == classOf[java.util.UUID]) Some(UuidKey.asInstanceOf[KeyKind[B]])
     else None
 }
 

@@ -41,6 +41,11 @@ private[reservoir] object Jni {
   @native def sampleIndexed(session: Long, n: Long, offsets: Array[Long]): Unit
   @native def fillLongs(session: Long, keys: Array[Long]): Unit
   @native def fillInts(session: Long, keys: Array[Int]): Unit
+  // byte keys (UUID): key_width / 8 Longs per key, n counts keys
+  @native def sampleWords(session: Long, words: Array[Long], hashes: Array[Long], n: Int): Unit
+  @native def resultWords(session: Long, out: Array[Long]): Int
+  @native def fillWords(session: Long, words: Array[Long]): Unit
+  @native def abortIndexed(session: Long): Unit
 }
 
 /** One native session (a malloc'd rsv_jvm, reservoir_jni.c) released exactly once: by a single-use
@@ -87,9 +92,9 @@ private[gpu] object JniCleaner {
   }
 }
 
-/** A GPU-backed `Sampler[A, B]` over JNI, B = Long or Int: keys are buffered in a JVM array and handed
-  * over 65536 at a time (one JNI call per batch, none per element); the native session copies them
-  * into the engine's pinned staging buffer.  Lifecycle as FfmSampler: `isOpen` tracked here, the
+/** A GPU-backed `Sampler[A, B]` over JNI, B = Long, Int or UUID: keys are buffered in a JVM array and
+  * handed over 65536 at a time (one JNI call per batch, none per element); the native session copies
+  * them into the engine's pinned staging buffer.  Lifecycle as FfmSampler: `isOpen` tracked here, the
   * single-use `result()` destroys the session at once. */
 private[reservoir] final class JniSampler[A, B](
     kind: Int,
@@ -103,12 +108,13 @@ private[reservoir] final class JniSampler[A, B](
     extends Sampler[A, B] {
   private[this] final val Batch = 65536
   private[this] val isLong      = keys.width == 8
+  private[this] val isUuid      = keys eq KeyKind.UuidKey
   private[this] val precomputed = kind == Abi.KindDistinct && hashKind == Abi.HashPrecomputed
   private[this] val session =
     new JniSession(Jni.create(kind, maxSampleSize, keys.width, reusable, engine, hashKind, Abi.OrderAuto, seed, 0L, -1))
   JniCleaner.register(this, session)
-  private[this] val longs  = if (isLong) new Array[Long](Batch) else null
-  private[this] val ints   = if (isLong) null else new Array[Int](Batch)
+  private[this] val longs  = if (isLong) new Array[Long](Batch) else if (isUuid) new Array[Long](2 * Batch) else null
+  private[this] val ints   = if (isLong || isUuid) null else new Array[Int](Batch)
   private[this] val hashes = if (precomputed) new Array[Long](Batch) else null
   private[this] var n      = 0
   private[this] var open   = true
@@ -120,7 +126,9 @@ private[reservoir] final class JniSampler[A, B](
 
   private[this] def flush(): Unit =
     if (n > 0) {
-      if (isLong) Jni.sampleLongs(session.get, longs, hashes, n) else Jni.sampleInts(session.get, ints, hashes, n)
+      if (isUuid) Jni.sampleWords(session.get, longs, hashes, n)
+      else if (isLong) Jni.sampleLongs(session.get, longs, hashes, n)
+      else Jni.sampleInts(session.get, ints, hashes, n)
       n = 0
       fence = 1
     }
@@ -128,7 +136,12 @@ private[reservoir] final class JniSampler[A, B](
   def sample(element: A): Unit = {
     if (!open) throw new IllegalStateException(Abi.ClosedMessage)
     val b = map(element)
-    if (isLong) longs(n) = b.asInstanceOf[Long] else ints(n) = b.asInstanceOf[Int]
+    if (isUuid) {
+      val u = b.asInstanceOf[java.util.UUID]
+      longs(2 * n) = u.getMostSignificantBits
+      longs(2 * n + 1) = u.getLeastSignificantBits
+    } else if (isLong) longs(n) = b.asInstanceOf[Long]
+    else ints(n) = b.asInstanceOf[Int]
     if (precomputed) hashes(n) = hash(b)
     n += 1
     if (n == Batch) flush()
@@ -144,24 +157,46 @@ private[reservoir] final class JniSampler[A, B](
       flush()
       val offsets = new Array[Long](maxSampleSize)
       Jni.sampleIndexed(session.get, seq.length.toLong, offsets)
-      if (isLong) {
-        val ks = new Array[Long](maxSampleSize)
-        var j  = 0
-        while (j < maxSampleSize) {
-          val o = offsets(j)
-          if (o >= 0) ks(j) = map(seq(o.toInt)).asInstanceOf[Long]
-          j += 1
+      // a throwing `map` drops the batch (the sampler stays usable) and propagates, as the
+      // reference's sampleIndexed propagates it
+      try {
+        if (isUuid) {
+          val ks = new Array[Long](2 * maxSampleSize)
+          var j  = 0
+          while (j < maxSampleSize) {
+            val o = offsets(j)
+            if (o >= 0) {
+              val u = map(seq(o.toInt)).asInstanceOf[java.util.UUID]
+              ks(2 * j) = u.getMostSignificantBits
+              ks(2 * j + 1) = u.getLeastSignificantBits
+            }
+            j += 1
+          }
+          Jni.fillWords(session.get, ks)
+        } else if (isLong) {
+          val ks = new Array[Long](maxSampleSize)
+          var j  = 0
+          while (j < maxSampleSize) {
+            val o = offsets(j)
+            if (o >= 0) ks(j) = map(seq(o.toInt)).asInstanceOf[Long]
+            j += 1
+          }
+          Jni.fillLongs(session.get, ks)
+        } else {
+          val ks = new Array[Int](maxSampleSize)
+          var j  = 0
+          while (j < maxSampleSize) {
+            val o = offsets(j)
+            if (o >= 0) ks(j) = map(seq(o.toInt)).asInstanceOf[Int]
+            j += 1
+          }
+          Jni.fillInts(session.get, ks)
         }
-        Jni.fillLongs(session.get, ks)
-      } else {
-        val ks = new Array[Int](maxSampleSize)
-        var j  = 0
-        while (j < maxSampleSize) {
-          val o = offsets(j)
-          if (o >= 0) ks(j) = map(seq(o.toInt)).asInstanceOf[Int]
-          j += 1
-        }
-        Jni.fillInts(session.get, ks)
+      } catch {
+        case t: Throwable =>
+          Jni.abortIndexed(session.get)
+          fence = 1
+          throw t
       }
       fence = 1
     case _ => super.sampleAll(elements)
@@ -171,7 +206,11 @@ private[reservoir] final class JniSampler[A, B](
     if (!open) throw new IllegalStateException(Abi.ClosedMessage)
     flush()
     val res =
-      if (isLong) {
+      if (isUuid) {
+        val out = new Array[Long](2 * maxSampleSize)
+        val m   = Jni.resultWords(session.get, out)
+        ArraySeq.unsafeWrapArray(Array.tabulate(m)(i => new java.util.UUID(out(2 * i), out(2 * i + 1))))
+      } else if (isLong) {
         val out = new Array[Long](maxSampleSize)
         val m   = Jni.resultLongs(session.get, out)
         ArraySeq.unsafeWrapArray(if (m == out.length) out else Arrays.copyOf(out, m))

@@ -50,6 +50,7 @@ private[reservoir] object Native {
   val rsvSampleIndexed: MethodHandle =
     downcall("rsv_sample_indexed", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS))
   val rsvFillSlots: MethodHandle = downcall("rsv_fill_slots", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS))
+  val rsvAbortIndexed: MethodHandle = downcall("rsv_abort_indexed", FunctionDescriptor.of(JAVA_INT, ADDRESS))
 
   val cleaner: Cleaner = Cleaner.create()
 
@@ -61,7 +62,7 @@ private[reservoir] object Native {
     }
 }
 
-/** A GPU-backed `Sampler[A, B]` over Panama FFM, B = Long or Int.  `map` writes each key straight into
+/** A GPU-backed `Sampler[A, B]` over Panama FFM, B = Long, Int or UUID ([mostSigBits | leastSigBits]).  `map` writes each key straight into
   * the engine's pinned staging buffer (rsv_stage_acquire / rsv_stage_commit: zero copy, double
   * buffered, flushed to the GPU asynchronously): one downcall per ~1 Mi keys and none per element.
   * `isOpen` is tracked here (no downcall); a single-use `result()` destroys the handle at once and
@@ -83,6 +84,7 @@ private[reservoir] final class FfmSampler[A, B](
 
   private[this] val arena       = Arena.ofShared() // akka may call from different (sequential) threads
   private[this] val isLong      = keys.width == 8
+  private[this] val isUuid      = keys eq KeyKind.UuidKey
   private[this] val precomputed = kind == Abi.KindDistinct && hashKind == Abi.HashPrecomputed
   private[this] val handle: MemorySegment = {
     val cfg = arena.allocate(Config)
@@ -129,11 +131,19 @@ private[reservoir] final class FfmSampler[A, B](
     if (precomputed) stageHash = hashesOut.get(ADDRESS, 0L).reinterpret(cap * 8)
   }
 
+  /** a UUID key at index i of a key segment: [mostSigBits | leastSigBits] */
+  private[this] def put(seg: MemorySegment, i: Long, b: B): Unit = {
+    val u = b.asInstanceOf[java.util.UUID]
+    seg.setAtIndex(JAVA_LONG, 2 * i, u.getMostSignificantBits)
+    seg.setAtIndex(JAVA_LONG, 2 * i + 1, u.getLeastSignificantBits)
+  }
+
   def sample(element: A): Unit = {
     if (!open) throw new IllegalStateException(Abi.ClosedMessage)
     if (filled == cap) nextStage()
     val b = map(element)
-    if (isLong) stage.setAtIndex(JAVA_LONG, filled, b.asInstanceOf[Long])
+    if (isUuid) put(stage, filled, b)
+    else if (isLong) stage.setAtIndex(JAVA_LONG, filled, b.asInstanceOf[Long])
     else stage.setAtIndex(JAVA_INT, filled, b.asInstanceOf[Int])
     if (precomputed) stageHash.setAtIndex(JAVA_LONG, filled, hash(b))
     filled += 1
@@ -158,14 +168,21 @@ private[reservoir] final class FfmSampler[A, B](
         check(rsvSampleIndexed.invoke(handle, seq.length.toLong, offsets).asInstanceOf[Int])
         val ks = tmp.allocate(keys.width.toLong * maxSampleSize, 8L)
         var j  = 0
-        while (j < maxSampleSize) {
-          val o = offsets.getAtIndex(JAVA_LONG, j.toLong)
-          if (o >= 0) {
-            val b = map(seq(o.toInt))
-            if (isLong) ks.setAtIndex(JAVA_LONG, j.toLong, b.asInstanceOf[Long])
-            else ks.setAtIndex(JAVA_INT, j.toLong, b.asInstanceOf[Int])
+        try {
+          while (j < maxSampleSize) {
+            val o = offsets.getAtIndex(JAVA_LONG, j.toLong)
+            if (o >= 0) {
+              val b = map(seq(o.toInt))
+              if (isUuid) put(ks, j.toLong, b)
+              else if (isLong) ks.setAtIndex(JAVA_LONG, j.toLong, b.asInstanceOf[Long])
+              else ks.setAtIndex(JAVA_INT, j.toLong, b.asInstanceOf[Int])
+            }
+            j += 1
           }
-          j += 1
+        } catch { // `map` threw: drop the batch, keep the sampler usable, propagate (sampleIndexed does)
+          case t: Throwable =>
+            check(rsvAbortIndexed.invoke(handle).asInstanceOf[Int])
+            throw t
         }
         check(rsvFillSlots.invoke(handle, ks).asInstanceOf[Int])
       } finally tmp.close()
@@ -187,8 +204,11 @@ private[reservoir] final class FfmSampler[A, B](
         val n   = tmp.allocate(JAVA_LONG)
         check(rsvResult.invoke(handle, out, maxSampleSize.toLong, n).asInstanceOf[Int])
         val len = n.get(JAVA_LONG, 0L)
-        // Sampler.scala:330 wraps the samples array the same way (ArraySeq.ofLong / ofInt)
-        if (isLong) ArraySeq.unsafeWrapArray(out.asSlice(0L, len * 8).toArray(JAVA_LONG))
+        // Sampler.scala:330 wraps the samples array the same way (ArraySeq.ofLong / ofInt / ofRef)
+        if (isUuid) {
+          val w = out.asSlice(0L, len * 16).toArray(JAVA_LONG)
+          ArraySeq.unsafeWrapArray(Array.tabulate(len.toInt)(i => new java.util.UUID(w(2 * i), w(2 * i + 1))))
+        } else if (isLong) ArraySeq.unsafeWrapArray(out.asSlice(0L, len * 8).toArray(JAVA_LONG))
         else ArraySeq.unsafeWrapArray(out.asSlice(0L, len * 4).toArray(JAVA_INT))
       } finally tmp.close()
     if (!reusable) { // SingleUse.close: destroy now; `open` keeps every later call off the handle

@@ -9,9 +9,13 @@
  *
  * Conventions
  *   - plain C: no C++ or torch types; opaque handle; every call returns rsv_status.
- *   - keys are primitive fixed-width values (Int -> key_width 4, Long -> key_width 8; for the
- *     element sampler also fixed-width byte keys of 16..256 bytes, e.g. UUIDs) that the host
- *     extracted with the sampler's `map` (S:115-116: map may be called more than k times).
+ *   - keys are primitive fixed-width values (Int -> key_width 4, Long -> key_width 8, or
+ *     fixed-width byte keys of 16..256 bytes in steps of 8: java.util.UUID -> 16 bytes laid out
+ *     [mostSigBits | leastSigBits] as little-endian Longs, or a case class of primitives) that the
+ *     host extracted with the sampler's `map` (S:115-116: map may be called more than k times).
+ *     Byte keys must have value equality (B.equals = equal bytes): a distinct sampler dedups by
+ *     the bytes, as the reference's `elements.contains` (S:398, S:403) does for such a B.  An
+ *     Array[Byte] (reference equality in a Scala Set) must stay on the JVM sampler.
  *   - "device" pointers are HIP device pointers on the handle's device; "host" pointers are
  *     ordinary (pageable or pinned) memory.  The caller owns every buffer it passes in.
  *   - one handle is single-threaded (S:18-19); distinct handles are independent.
@@ -36,7 +40,8 @@ typedef enum rsv_status {
     RSV_E_NULL_POINTER = 3,     /* NullPointerException: a required pointer is NULL (S:82, S:94) */
     RSV_E_DEVICE = 4,           /* HIP runtime / kernel failure -> RuntimeException (fails the akka Future, SI:43-46) */
     RSV_E_OUT_OF_MEMORY = 5,    /* device or pinned allocation failed -> OutOfMemoryError */
-    RSV_E_UNSUPPORTED = 6       /* valid request this build does not implement (message says which) */
+    RSV_E_UNSUPPORTED = 6       /* request this build does not implement (message says which): a key_width
+                                 * other than 4, 8, 16..256 in steps of 8; a hash kind byte keys lack */
 } rsv_status;
 
 typedef enum rsv_kind {
@@ -56,7 +61,9 @@ typedef enum rsv_engine {
 } rsv_engine;
 
 typedef enum rsv_hash_kind {
-    RSV_HASH_DEFAULT = 0,     /* B#hashCode().toLong (S:75): JAVA_INT for key_width 4, JAVA_LONG for 8 */
+    RSV_HASH_DEFAULT = 0,     /* B#hashCode().toLong (S:75): JAVA_INT for key_width 4, JAVA_LONG for 8,
+                               * java.util.UUID.hashCode for 16 ((int)(hilo >>> 32) ^ (int)hilo, hilo =
+                               * msb ^ lsb); other byte widths take PRECOMPUTED */
     RSV_HASH_IDENTITY = 1,    /* hash = key as a signed Long (a bijection: bit-exact distinct sets) */
     RSV_HASH_JAVA_LONG = 2,   /* java.lang.Long.hashCode: (int)(v ^ v>>>32), sign-extended */
     RSV_HASH_JAVA_INT = 3,    /* java.lang.Integer.hashCode: v, sign-extended */
@@ -85,7 +92,7 @@ typedef struct rsv_config {
     uint32_t struct_size;     /* = sizeof(rsv_config) */
     int32_t  kind;            /* rsv_kind */
     int32_t  max_sample_size; /* k: S:130 maxSampleSize / S:173 */
-    int32_t  key_width;       /* 4 (Int) or 8 (Long); ELEMENTS also fixed-width byte keys: a multiple of 8 up to 256 */
+    int32_t  key_width;       /* 4 (Int), 8 (Long), or fixed-width byte keys: a multiple of 8 in 16..256 */
     int32_t  reusable;        /* S:130/S:173 reusable: result() may be called repeatedly (S:353-381, S:430-433) */
     int32_t  pre_allocate;    /* S:130 preAllocate: accepted; device slots are always preallocated */
     int32_t  engine;          /* rsv_engine (ELEMENTS only) */
@@ -144,6 +151,13 @@ rsv_status rsv_sample_indexed(rsv_sampler* s, int64_t n, int64_t* slot_offsets_h
 /* The keys owed after rsv_sample_indexed: keys_host holds k keys in slot order; entry j is read
  * only where slot_offsets_host[j] >= 0 (the rest may be anything). */
 rsv_status rsv_fill_slots(rsv_sampler* s, const void* keys_host);
+/* Drop the pending rsv_sample_indexed batch (the caller's `map` threw on an element it owed the
+ * engine): the handle returns to its state before that call -- count, slots, result -- and takes
+ * calls again; a binding then rethrows the exception, as the reference's sampleIndexed propagates
+ * it (S:261-273).  The batch goes as a whole, where the reference keeps what it mapped before the
+ * throw: after a throwing `map` the two differ in which of the batch's elements count.
+ * RSV_E_ILLEGAL_STATE without a pending rsv_sample_indexed. */
+rsv_status rsv_abort_indexed(rsv_sampler* s);
 
 /* Sampler.result() (S:59-60; resultImpl S:318-331; RandomValues.result S:411).  Writes
  * min(count, k) keys (ELEMENTS: slot order, which is part of the reference result) or the distinct
@@ -255,8 +269,10 @@ rsv_status rsv_merge_log(rsv_sampler* s, const int64_t* hashes_host, const void*
  *   ELEMENTS: row_dev[0..k) = global index per slot (-1 = empty), row_dev[k..2k) = the slot's key
  *     widened to int64 (sign-extended for 4-byte keys); for wide keys (key_width > 8) the k keys
  *     follow as key_width/8 int64 words each.
- *   DISTINCT: 2k + 6 words: [keys widened to int64 (k) | scrambled hashes (k) | n, count, tied,
- *     max_hash, log_retained, ordered] -- the set ascending by (hash, key), n entries valid. */
+ *   DISTINCT: [keys (k) | scrambled hashes (k) | n, count, tied, max_hash, log_retained, ordered] --
+ *     the set ascending by (hash, key), n entries valid; keys widened to int64 (2k + 6 words), or for
+ *     byte keys key_width / 8 words each (k (key_width / 8 + 1) + 6 words, ascending by (hash, key
+ *     words compared as unsigned 64-bit, word 0 first)). */
 rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev);
 /* Merge `parts` packed rows (row p at rows_dev + p*row_stride, row_stride >= the row length), e.g. the output
  * of an all-gather of every rank's rsv_export_packed row.
@@ -265,7 +281,8 @@ rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev);
  *     kernels, no host wait: the set's size and tie state are read back at the next call on the
  *     handle); `tied` as rsv_merge_state.  On a caller stream the rows must stay valid and
  *     unchanged until the next call on the handle returns (a degenerate hash that overflows the
- *     merge's buckets is redone from them then). */
+ *     merge's buckets is redone from them then).  Byte-key DISTINCT samplers merge before the call
+ *     returns (the host reads the rows' meta words). */
 rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t parts, int64_t row_stride,
                             int64_t total_count);
 

@@ -354,6 +354,183 @@ int64_t or_distinct_r0(const or_distinct* d) { return d->r0; }
 int64_t or_distinct_r1(const or_distinct* d) { return d->r1; }
 
 /* ------------------------------------------------------------------------------------------ */
+/* RandomValues over fixed-width byte keys (Sampler.scala:383-412 with B = UUID / a case class) */
+/* ------------------------------------------------------------------------------------------ */
+/* java.util.UUID.hashCode (JDK): long hilo = mostSigBits ^ leastSigBits;
+ * return ((int)(hilo >> 32)) ^ (int) hilo;  -- widened by .toLong (Sampler.scala:75) */
+int64_t or_uuid_hashcode(uint64_t msb, uint64_t lsb) {
+    uint64_t hilo = msb ^ lsb;
+    return (int64_t)(int32_t)((uint32_t)(hilo >> 32) ^ (uint32_t)hilo);
+}
+
+/* The element set of B: open addressing over member ids with tombstones (FNV-1a of the key
+ * words picks the home slot; equality compares every word), rebuilt when half full. */
+typedef struct { int64_t* ids; uint64_t cap, used; } rowset; /* ids: -1 free, -2 tombstone */
+
+struct or_distinct_rows {
+    int32_t  k, words, uuid;
+    int64_t  r0, r1;
+    pq_ent*  heap;     /* 1-indexed max-heap of (member id, h), scala PriorityQueue order */
+    int64_t  size;
+    uint64_t* store;   /* member id -> key words; ids recycled through `free_ids` */
+    int64_t* free_ids;
+    int64_t  n_free, n_ids, cap_ids;
+    rowset   set;
+    int64_t  max_hash;
+};
+
+static uint64_t row_fnv(const uint64_t* r, int32_t words) {
+    uint64_t x = 0xcbf29ce484222325ULL;
+    for (int32_t w = 0; w < words; w++)
+        for (int b = 0; b < 8; b++) { x ^= (r[w] >> (8 * b)) & 0xFF; x *= 0x100000001b3ULL; }
+    return x;
+}
+static const uint64_t* drow(const or_distinct_rows* d, int64_t id) { return d->store + (size_t)id * d->words; }
+static int rows_equal(const uint64_t* a, const uint64_t* b, int32_t words) {
+    return memcmp(a, b, (size_t)words * 8) == 0;
+}
+static void rowset_init(rowset* s, uint64_t cap) {
+    s->cap = cap; s->used = 0;
+    s->ids = (int64_t*)malloc(cap * sizeof(int64_t));
+    for (uint64_t i = 0; i < cap; i++) s->ids[i] = -1;
+}
+static void rowset_put(or_distinct_rows* d, int64_t id) {
+    uint64_t p = row_fnv(drow(d, id), d->words) & (d->set.cap - 1);
+    while (d->set.ids[p] >= 0) p = (p + 1) & (d->set.cap - 1);
+    d->set.ids[p] = id; d->set.used++;
+}
+static void rowset_rebuild(or_distinct_rows* d) {  /* drops tombstones */
+    free(d->set.ids);
+    uint64_t cap = 16;
+    while (cap < 4 * (uint64_t)(d->size + 2)) cap <<= 1;
+    rowset_init(&d->set, cap);
+    for (int64_t i = 1; i <= d->size; i++) rowset_put(d, d->heap[i].elem);
+}
+static int rowset_contains(const or_distinct_rows* d, const uint64_t* r) {
+    for (uint64_t p = row_fnv(r, d->words) & (d->set.cap - 1);; p = (p + 1) & (d->set.cap - 1)) {
+        int64_t id = d->set.ids[p];
+        if (id == -1) return 0;
+        if (id >= 0 && rows_equal(drow(d, id), r, d->words)) return 1;
+    }
+}
+static void rowset_remove(or_distinct_rows* d, int64_t id) {
+    for (uint64_t p = row_fnv(drow(d, id), d->words) & (d->set.cap - 1);; p = (p + 1) & (d->set.cap - 1))
+        if (d->set.ids[p] == id) { d->set.ids[p] = -2; return; }
+}
+
+or_distinct_rows* or_drows_new(int32_t k, int64_t seed, int32_t words, int uuid) {
+    if (k <= 0 || words <= 0) return NULL;
+    or_distinct_rows* d = (or_distinct_rows*)calloc(1, sizeof(*d));
+    d->k = k; d->words = words; d->uuid = uuid;
+    or_jrandom r;
+    or_jr_init(&r, seed);
+    d->r0 = or_jr_next_long(&r); /* Sampler.scala:385-388 */
+    d->r1 = or_jr_next_long(&r);
+    d->heap = (pq_ent*)malloc(((size_t)k + 2) * sizeof(pq_ent));
+    d->cap_ids = 1024;
+    d->store = (uint64_t*)malloc((size_t)d->cap_ids * words * 8);
+    d->free_ids = (int64_t*)malloc((size_t)d->cap_ids * 8);
+    rowset_init(&d->set, 64);
+    d->max_hash = INT64_MIN;
+    return d;
+}
+
+void or_drows_free(or_distinct_rows* d) {
+    if (!d) return;
+    free(d->heap); free(d->store); free(d->free_ids); free(d->set.ids); free(d);
+}
+
+static int64_t drows_new_id(or_distinct_rows* d, const uint64_t* r) {
+    int64_t id;
+    if (d->n_free) id = d->free_ids[--d->n_free];
+    else {
+        if (d->n_ids == d->cap_ids) {
+            d->cap_ids *= 2;
+            d->store = (uint64_t*)realloc(d->store, (size_t)d->cap_ids * d->words * 8);
+            d->free_ids = (int64_t*)realloc(d->free_ids, (size_t)d->cap_ids * 8);
+        }
+        id = d->n_ids++;
+    }
+    memcpy(d->store + (size_t)id * d->words, r, (size_t)d->words * 8);
+    return id;
+}
+
+/* the same heap moves as pq_add / pq_dequeue above (scala 2.13 PriorityQueue), on (id, h) */
+static void drows_pq_add(or_distinct_rows* d, pq_ent e) {
+    int64_t m = ++d->size;
+    d->heap[m] = e;
+    while (m > 1 && d->heap[m / 2].h < d->heap[m].h) {
+        pq_ent t = d->heap[m]; d->heap[m] = d->heap[m / 2]; d->heap[m / 2] = t;
+        m /= 2;
+    }
+}
+static pq_ent drows_pq_dequeue(or_distinct_rows* d) {
+    pq_ent res = d->heap[1];
+    d->heap[1] = d->heap[d->size];
+    d->size--;
+    int64_t n = d->size, k = 1;
+    while (n >= 2 * k) {
+        int64_t j = 2 * k;
+        if (j < n && d->heap[j].h < d->heap[j + 1].h) j++;
+        if (d->heap[k].h >= d->heap[j].h) break;
+        pq_ent t = d->heap[k]; d->heap[k] = d->heap[j]; d->heap[j] = t;
+        k = j;
+    }
+    return res;
+}
+
+void or_drows_sample(or_distinct_rows* d, const uint64_t* row, int64_t hash) {
+    /* RandomValues.sample, Sampler.scala:394-409 */
+    if (d->uuid) hash = or_uuid_hashcode(row[0], row[1]);
+    int64_t h = or_distinct_scramble(d->r0, d->r1, hash);
+    if (d->size < d->k) {
+        if (!rowset_contains(d, row)) {
+            if (4 * (d->set.used + 1) > 2 * d->set.cap) rowset_rebuild(d); /* before the new member */
+            pq_ent e = {drows_new_id(d, row), h};
+            drows_pq_add(d, e);
+            rowset_put(d, e.elem);
+            if (h > d->max_hash) d->max_hash = h;
+        }
+    } else if (h < d->max_hash && !rowset_contains(d, row)) {
+        pq_ent old = drows_pq_dequeue(d);        /* elements -= samples.dequeue()._1 */
+        rowset_remove(d, old.elem);
+        d->free_ids[d->n_free++] = old.elem;
+        if (4 * (d->set.used + 1) > 2 * d->set.cap) rowset_rebuild(d);
+        pq_ent e = {drows_new_id(d, row), h};    /* samples += ((elem, elemHash)) */
+        drows_pq_add(d, e);
+        rowset_put(d, e.elem);                   /* elements += elem */
+        d->max_hash = d->heap[1].h;
+    }
+}
+
+void or_drows_sample_array(or_distinct_rows* d, const uint64_t* rows, const int64_t* hashes, int64_t n) {
+    for (int64_t i = 0; i < n; i++) or_drows_sample(d, rows + (size_t)i * d->words, hashes ? hashes[i] : 0);
+}
+
+static const or_distinct_rows* g_cmp_rows; /* qsort context (the oracle is single-threaded here) */
+static int cmp_row_ent(const void* a, const void* b) {
+    const pq_ent* x = (const pq_ent*)a; const pq_ent* y = (const pq_ent*)b;
+    if (x->h != y->h) return x->h < y->h ? -1 : 1;
+    const uint64_t* p = drow(g_cmp_rows, x->elem); const uint64_t* q = drow(g_cmp_rows, y->elem);
+    for (int32_t w = 0; w < g_cmp_rows->words; w++)
+        if (p[w] != q[w]) return p[w] < q[w] ? -1 : 1;
+    return 0;
+}
+
+int64_t or_drows_result(const or_distinct_rows* d, uint64_t* out_rows, int64_t* out_hash) {
+    pq_ent* tmp = (pq_ent*)malloc(((size_t)d->size + 1) * sizeof(pq_ent));
+    memcpy(tmp, d->heap + 1, (size_t)d->size * sizeof(pq_ent));
+    g_cmp_rows = d;
+    qsort(tmp, (size_t)d->size, sizeof(pq_ent), cmp_row_ent);
+    for (int64_t i = 0; i < d->size; i++) {
+        if (out_rows) memcpy(out_rows + (size_t)i * d->words, drow(d, tmp[i].elem), (size_t)d->words * 8);
+        if (out_hash) out_hash[i] = tmp[i].h;
+    }
+    free(tmp);
+    return d->size;
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* Philox4x32-10 (Salmon et al., SC'11; Random123 philox.h) and draw format R2                 */
 /* ------------------------------------------------------------------------------------------ */
 void or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {

@@ -81,6 +81,19 @@ int64_t or_distinct_r0(const or_distinct* d);
 int64_t or_distinct_r1(const or_distinct* d);
 int64_t or_distinct_scramble(int64_t r0, int64_t r1, int64_t hashed);
 
+/* ---- RandomValues over fixed-width byte keys (B with value equality: java.util.UUID, a case
+ * class of primitives; `words` 64-bit words per key).  hash(elem) is the caller's per-element
+ * value (a JVM `hash: B => Long`), or with uuid != 0 java.util.UUID.hashCode of the key laid out
+ * [mostSigBits | leastSigBits].  Equality = equal words (Sampler.scala:398, :403). ---- */
+typedef struct or_distinct_rows or_distinct_rows;
+or_distinct_rows* or_drows_new(int32_t k, int64_t seed, int32_t words, int uuid);
+void    or_drows_free(or_distinct_rows* d);
+void    or_drows_sample(or_distinct_rows* d, const uint64_t* row, int64_t hash);
+void    or_drows_sample_array(or_distinct_rows* d, const uint64_t* rows, const int64_t* hashes, int64_t n);
+/* the set sorted by (signed scrambled hash, key words as unsigned, word 0 first); returns its size */
+int64_t or_drows_result(const or_distinct_rows* d, uint64_t* out_rows, int64_t* out_hash);
+int64_t or_uuid_hashcode(uint64_t msb, uint64_t lsb);
+
 /* ---- Philox4x32-10 (Random123) and the build's own Algorithm-R draw format "R2" ---- */
 void     or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 uint64_t or_draw_u64(uint64_t seed, uint64_t stream, uint64_t i);          /* U_i */

@@ -68,6 +68,13 @@ def lib():
     L.or_distinct_r1.argtypes = [C.c_void_p]; L.or_distinct_r1.restype = C.c_int64
     L.or_distinct_scramble.argtypes = [C.c_int64, C.c_int64, C.c_int64]
     L.or_distinct_scramble.restype = C.c_int64
+    u64v = C.c_void_p
+    L.or_drows_new.argtypes = [C.c_int32, C.c_int64, C.c_int32, C.c_int]; L.or_drows_new.restype = C.c_void_p
+    L.or_drows_free.argtypes = [C.c_void_p]
+    L.or_drows_sample.argtypes = [C.c_void_p, u64v, C.c_int64]
+    L.or_drows_sample_array.argtypes = [C.c_void_p, u64v, u64v, C.c_int64]
+    L.or_drows_result.argtypes = [C.c_void_p, u64v, u64v]; L.or_drows_result.restype = C.c_int64
+    L.or_uuid_hashcode.argtypes = [C.c_uint64, C.c_uint64]; L.or_uuid_hashcode.restype = C.c_int64
     L.or_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.or_draw_u64.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]; L.or_draw_u64.restype = C.c_uint64
     L.or_draw_j.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]; L.or_draw_j.restype = C.c_uint64
@@ -195,6 +202,48 @@ class Distinct:
     @property
     def r1(self) -> int:
         return lib().or_distinct_r1(self._d)
+
+
+class DistinctRows:
+    """RandomValues over fixed-width byte keys (Sampler.scala:383-412 with B = UUID / a case class of
+    primitives): rows of ``width`` bytes, equality = equal bytes.  ``hash`` is "precomputed" (the
+    caller's per-element Long, passed to sample_all) or "uuid" (java.util.UUID.hashCode of the row,
+    laid out [mostSigBits | leastSigBits] as little-endian Longs)."""
+
+    def __init__(self, k: int, seed: int, width: int, hash: str = "precomputed"):
+        if width % 8 or width <= 0:
+            raise ValueError("width must be a positive multiple of 8")
+        self.k, self.width = k, width
+        self._d = lib().or_drows_new(k, seed, width // 8, 1 if hash == "uuid" else 0)
+        if not self._d:
+            raise ValueError("bad k")
+
+    def __del__(self):
+        try:
+            lib().or_drows_free(self._d)
+        except Exception:
+            pass
+
+    def sample_all(self, rows, hashes=None) -> None:
+        r = np.ascontiguousarray(np.asarray(rows, dtype=np.uint8).reshape(-1, self.width))
+        hp = None
+        if hashes is not None:
+            h = np.ascontiguousarray(np.asarray(hashes, dtype=np.int64))
+            if h.size != r.shape[0]:
+                raise ValueError("one hash per row")
+            hp = h.ctypes.data
+        lib().or_drows_sample_array(self._d, r.ctypes.data, hp, r.shape[0])
+
+    def result(self):
+        """(rows uint8 [m, width], scrambled hashes) sorted by (hash, key words)."""
+        rows = np.zeros((self.k, self.width), dtype=np.uint8)
+        hs = np.zeros(self.k, dtype=np.int64)
+        m = lib().or_drows_result(self._d, rows.ctypes.data, hs.ctypes.data)
+        return rows[:m].copy(), hs[:m].copy()
+
+
+def uuid_hashcode(msb: int, lsb: int) -> int:
+    return lib().or_uuid_hashcode(msb & (2**64 - 1), lsb & (2**64 - 1))
 
 
 def byteswap64(v: int) -> int:

@@ -203,7 +203,17 @@ __host__ __device__ __forceinline__ int64_t scramble(int64_t r0, int64_t r1, int
     return byteswap64(r1 ^ byteswap64(r0 ^ hashed));
 }
 
-enum HashKind : int { kHashIdentity = 1, kHashJavaLong = 2, kHashJavaInt = 3, kHashPrecomputed = 4 };
+enum HashKind : int { kHashIdentity = 1, kHashJavaLong = 2, kHashJavaInt = 3, kHashPrecomputed = 4, kHashUuid = 5 };
+
+// java.util.UUID.hashCode (JDK: hilo = mostSigBits ^ leastSigBits; (int)(hilo >> 32) ^ (int) hilo),
+// widened like `.toLong`, of a 16-byte key laid out [mostSigBits | leastSigBits], little-endian Longs
+__host__ __device__ __forceinline__ int64_t uuid_hash_code(uint64_t msb, uint64_t lsb) {
+    const uint64_t hilo = msb ^ lsb;
+    return (int64_t)(int32_t)((uint32_t)(hilo >> 32) ^ (uint32_t)hilo);
+}
+
+// where a wide-key distinct sampler's hash comes from (rsv_wide.hip)
+enum WideSrc : int { kWideSrcHashes = 0, kWideSrcUuid = 1 };
 
 template <typename KeyT, int HASH>
 __host__ __device__ __forceinline__ int64_t hash_of(KeyT key) {

@@ -2051,13 +2051,19 @@ struct DistinctState {
     int64_t pend_stride = 0;
     uint32_t* mstart = nullptr;  // [(parts + 1) x (B + 1)] bucket starts of every run
     int64_t mstart_cap = 0;
+    // key_width > 8 (fixed-width byte keys): the whole sampler is rsv_wide.hip's; every entry point
+    // below forwards to it
+    WideDistinct* wide = nullptr;
 };
 
 // <= 2 GB of host archive (12-16 B per candidate): beyond it rsv_export_log reports the log as not
 // retained
 constexpr int64_t kArchMax = (int64_t)1 << 27;
 
-void distinct_set_timer(DistinctState* d, KernelTimer* t) { d->timer = t; }
+void distinct_set_timer(DistinctState* d, KernelTimer* t) {
+    d->timer = t;
+    if (d->wide) wide_set_timer(d->wide, t);
+}
 
 template <typename KeyT>
 static hipError_t temp_bytes_for(int64_t cap, size_t* bytes) {
@@ -2143,6 +2149,19 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
                                int* status) {
     DistinctState* d = new DistinctState();
     d->ordered = ordered;
+    if (key_width > 8) {  // fixed-width byte keys: rsv_wide.hip
+        d->k = k;
+        d->kw = key_width;
+        d->hash_kind = hash_kind;
+        d->spec_min = INT64_MAX;  // no speculative publication
+        d->wide = wide_create(k, key_width, hash_kind == kHashUuid ? kWideSrcUuid : kWideSrcHashes, r0, r1, ordered,
+                              status);
+        if (!d->wide) {
+            delete d;
+            return nullptr;
+        }
+        return d;
+    }
     if (ordered) d->rep.reset(k);
     d->k = k;
     d->kw = key_width;
@@ -2209,6 +2228,11 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
 
 void distinct_destroy(DistinctState* d) {
     if (!d) return;
+    if (d->wide) {
+        wide_destroy(d->wide);
+        delete d;
+        return;
+    }
     void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->ctl, d->bh, d->bk, d->mh0, d->mh1, d->mk0,
                   d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp, d->log_h, d->log_k, d->log_i,
                   d->perm, d->sorted_i, d->ord_h, d->ord_k, d->sdev, d->sctl, d->sbh, d->sbk, d->sbi, d->vacc,
@@ -2224,12 +2248,12 @@ void distinct_destroy(DistinctState* d) {
     delete d;
 }
 
-int64_t distinct_size(const DistinctState* d) { return d->m; }
-const void* distinct_keys_dev(const DistinctState* d) { return d->set_k; }
+int64_t distinct_size(const DistinctState* d) { return d->wide ? wide_size(d->wide) : d->m; }
+const void* distinct_keys_dev(const DistinctState* d) { return d->wide ? wide_keys_dev(d->wide) : d->set_k; }
 
 void distinct_spec_target(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t* gen_counter) {
     // the bucketed merge only: set mode behind ctl_publish, ordered mode behind the scheduled pass
-    if (d->log_bmax < 0) return;
+    if (d->log_bmax < 0 || d->wide) return;
     d->spec_dst = dst_host_dev;
     d->spec_flag = flag_dev;
     d->spec_gen_ctr = gen_counter;
@@ -2248,6 +2272,7 @@ bool distinct_spec_take(DistinctState* d, uint32_t* gen) {
 }
 
 int distinct_publish(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st) {
+    if (d->wide) return wide_publish(d->wide, dst_host_dev, flag_dev, gen, st);
     RSV_HIP_TRY(launch_publish_multi(d->set_k, d->m * d->kw, dst_host_dev, flag_dev, gen, (uint32_t*)(d->ctl + 4), st));
     return RSV_OK;
 }
@@ -3276,6 +3301,7 @@ static int ordered_sample_impl(DistinctState* d, const KeyT* keys, const int64_t
 
 int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* hashes, int64_t n,
                            hipStream_t st) {
+    if (d->wide) return wide_sample_device(d->wide, keys, hashes, n, st);
     if (int rc = distinct_settle(d, st)) return rc;
     if (d->merged && n > 0) {  // sampling on after a merge: the pre-merge candidates are history
         d->merged = false;
@@ -3291,6 +3317,7 @@ int distinct_sample_device(DistinctState* d, const void* keys, const int64_t* ha
 }
 
 int distinct_finalize(DistinctState* d, hipStream_t st) {
+    if (d->wide) return wide_finalize(d->wide, st);
     if (int rc = distinct_settle(d, st)) return rc;
     if (!d->ordered || d->exact) return RSV_OK;
     const auto t0 = std::chrono::steady_clock::now();
@@ -3311,6 +3338,7 @@ int distinct_finalize(DistinctState* d, hipStream_t st) {
 }
 
 int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStream_t st) {
+    if (d->wide) return wide_export(d->wide, keys_dev, hash_dev, st);
     if (d->m == 0) return RSV_OK;
     if (keys_dev) RSV_HIP_TRY(hipMemcpyAsync(keys_dev, d->set_k, d->m * d->kw, hipMemcpyDeviceToDevice, st));
     if (hash_dev) RSV_HIP_TRY(hipMemcpyAsync(hash_dev, d->set_h, d->m * 8, hipMemcpyDeviceToDevice, st));
@@ -3319,6 +3347,11 @@ int distinct_export(DistinctState* d, void* keys_dev, int64_t* hash_dev, hipStre
 
 void distinct_info(const DistinctState* d, int32_t* ordered, int32_t* tied, int32_t* retained, int64_t* size,
                    int64_t* max_hash, int64_t* log_entries, int64_t* sched_passes, int64_t* sched_fallbacks) {
+    if (d->wide) {
+        *sched_passes = *sched_fallbacks = 0;
+        wide_info(d->wide, ordered, tied, retained, size, max_hash, log_entries);
+        return;
+    }
     *sched_passes = d->sched_passes;
     *sched_fallbacks = d->sched_fallbacks;
     *ordered = d->ordered;
@@ -3352,6 +3385,7 @@ static void merged_bookkeeping(DistinctState* d) {
 // keeps its logged candidates for rsv_export_log until it samples again.
 int distinct_merge_parts(DistinctState* d, const void* keys_dev, const int64_t* hash_dev, const int64_t* part_n,
                          int32_t parts, int64_t part_len, hipStream_t st) {
+    if (d->wide) return wide_merge_parts(d->wide, keys_dev, hash_dev, part_n, parts, part_len, st);
     int64_t total = 0;
     for (int32_t p = 0; p < parts; ++p) total += std::max<int64_t>(0, std::min(part_n[p], part_len));
     if (int rc = distinct_settle(d, st)) return rc;
@@ -3386,6 +3420,7 @@ int distinct_merge_parts(DistinctState* d, const void* keys_dev, const int64_t* 
 // ---- packed rows (rsv_export_packed / rsv_merge_packed) ----------------------------------------
 
 int distinct_export_row(DistinctState* d, int64_t* row, int64_t count, hipStream_t st) {
+    if (d->wide) return wide_export_row(d->wide, row, count, st);
     if (int rc = distinct_settle(d, st)) return rc;
     if (int rc = distinct_finalize(d, st)) return rc;
     const int64_t k = d->k;
@@ -3487,7 +3522,7 @@ static int settle_impl(DistinctState* d, hipStream_t st) {
 }
 
 int distinct_settle(DistinctState* d, hipStream_t st) {
-    if (!d->pend) return RSV_OK;
+    if (!d->pend) return RSV_OK;  // (wide-key merges complete before they return: never pending)
     return d->kw == 8 ? settle_impl<int64_t>(d, st) : settle_impl<int32_t>(d, st);
 }
 
@@ -3538,6 +3573,7 @@ static int merge_rows_impl(DistinctState* d, const int64_t* rows, int32_t parts,
 }
 
 int distinct_merge_rows(DistinctState* d, const int64_t* rows, int32_t parts, int64_t stride, hipStream_t st) {
+    if (d->wide) return parts > 0 ? wide_merge_rows(d->wide, rows, parts, stride, st) : RSV_OK;
     if (int rc = distinct_settle(d, st)) return rc;
     if (parts <= 0) return RSV_OK;
     if (int rc = distinct_finalize(d, st)) return rc;  // an ordered set must be exact before it merges
@@ -3546,6 +3582,7 @@ int distinct_merge_rows(DistinctState* d, const int64_t* rows, int32_t parts, in
 }
 
 void distinct_retain_log(DistinctState* d, bool on) {
+    if (d->wide) return wide_retain_log(d->wide, on);
     if (on && !d->retain && d->seen > 0) d->arch_ok = false;  // earlier candidates are gone
     d->retain = on;
     if (!on) archive_drop(d);
@@ -3587,6 +3624,7 @@ static int log_export_impl(DistinctState* d, int64_t bound, int64_t* out_h, KeyT
 
 int distinct_log_export(DistinctState* d, int64_t bound, int64_t* out_h, void* out_k, int64_t cap, int64_t* out_n,
                         hipStream_t st) {
+    if (d->wide) return wide_log_export(d->wide, bound, out_h, out_k, cap, out_n, st);
     if (int rc = distinct_settle(d, st)) return rc;
     if (!d->ordered || !d->retain || !d->arch_ok) {
         set_error(!d->ordered  ? "rsv_export_log needs an RSV_DISTINCT_ORDERED sampler"
@@ -3604,6 +3642,7 @@ int distinct_log_export(DistinctState* d, int64_t bound, int64_t* out_h, void* o
 // the sampler's state, as if it had seen the whole stream.
 int distinct_log_merge(DistinctState* d, const int64_t* h, const void* keys, int64_t n, int64_t seen,
                        hipStream_t st) {
+    if (d->wide) return wide_log_merge(d->wide, h, keys, n, seen, st);
     if (!d->ordered) {
         set_error("rsv_merge_log needs an RSV_DISTINCT_ORDERED sampler");
         return RSV_E_UNSUPPORTED;

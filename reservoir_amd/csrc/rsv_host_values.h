@@ -30,6 +30,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -221,6 +222,163 @@ struct HostValues {
         has_empty = false;
         set_ok = true;
         set_reserve(std::min<int64_t>(kk, 1 << 16));
+    }
+};
+
+// The same replica for fixed-width byte keys (B = java.util.UUID or a case class of primitives,
+// `words` 64-bit words each): the heap orders (hash, member slot) with the scala PriorityQueue tie
+// behaviour above; members live in a slot pool of rows; the element set probes by the scrambled hash
+// (equal keys have equal hashes) and compares the rows -- `elements.contains(elem)` is B.equals,
+// which for these types is equality of the bytes.
+struct HostValuesWide {
+    int64_t k = 0, words = 0;
+    int64_t n = 0;                 // heap size
+    std::vector<int64_t> hh;       // heap hashes, 1-indexed, index n + 1 = fixDown slack
+    std::vector<int32_t> hs;       // heap member slots
+    std::vector<uint64_t> rows;    // slot s: rows[s * words ..)
+    std::vector<int64_t> slot_h;   // hash of the member in slot s
+    std::vector<int32_t> free_slots;
+    std::vector<int32_t> tab;      // open addressing over member slots, -1 = free
+    uint64_t mask = 0;
+    int64_t max_hash = INT64_MIN;  // Sampler.scala:392
+
+    static uint64_t mix(int64_t h) {
+        uint64_t z = (uint64_t)h * 0x9E3779B97F4A7C15ull;
+        return z ^ (z >> 31);
+    }
+    const uint64_t* row(int32_t s) const { return rows.data() + (size_t)s * words; }
+    bool same(int32_t s, int64_t h, const uint64_t* r) const {
+        if (slot_h[(size_t)s] != h) return false;
+        const uint64_t* a = row(s);
+        for (int64_t w = 0; w < words; ++w)
+            if (a[w] != r[w]) return false;
+        return true;
+    }
+    void rehash(uint64_t cap) {
+        tab.assign(cap, -1);
+        mask = cap - 1;
+        for (int64_t i = 1; i <= n; ++i) tab_add(hs[(size_t)i]);
+    }
+    void tab_add(int32_t s) {
+        uint64_t q = mix(slot_h[(size_t)s]) & mask;
+        while (tab[q] >= 0) q = (q + 1) & mask;
+        tab[q] = s;
+    }
+    bool contains(int64_t h, const uint64_t* r) const {
+        for (uint64_t q = mix(h) & mask;; q = (q + 1) & mask) {
+            const int32_t s = tab[q];
+            if (s < 0) return false;
+            if (same(s, h, r)) return true;
+        }
+    }
+    void tab_remove(int32_t s) {
+        uint64_t p = mix(slot_h[(size_t)s]) & mask;
+        while (tab[p] != s) p = (p + 1) & mask;
+        tab[p] = -1;
+        for (uint64_t q = (p + 1) & mask; tab[q] >= 0; q = (q + 1) & mask) {  // backward-shift deletion
+            const uint64_t home = mix(slot_h[(size_t)tab[q]]) & mask;
+            const bool move = p <= q ? (home <= p || home > q) : (home <= p && home > q);
+            if (move) {
+                tab[p] = tab[q];
+                tab[q] = -1;
+                p = q;
+            }
+        }
+    }
+    int32_t alloc(int64_t h, const uint64_t* r) {
+        int32_t s;
+        if (!free_slots.empty()) {
+            s = free_slots.back();
+            free_slots.pop_back();
+        } else {
+            s = (int32_t)slot_h.size();
+            slot_h.push_back(0);
+            rows.resize(rows.size() + (size_t)words);
+        }
+        slot_h[(size_t)s] = h;
+        std::copy(r, r + words, rows.begin() + (std::ptrdiff_t)((size_t)s * words));
+        return s;
+    }
+    void pq_add(int32_t s, int64_t h) {  // addOne + fixUp: parent < child -> swap
+        if (n + 2 >= (int64_t)hh.size()) {
+            const size_t cap = (size_t)std::min<int64_t>(k + 2, std::max<int64_t>(1024, 2 * (n + 2)));
+            hh.resize(cap, INT64_MIN);
+            hs.resize(cap, -1);
+        }
+        int64_t m = ++n;
+        while (m > 1 && hh[(size_t)(m >> 1)] < h) {
+            hh[(size_t)m] = hh[(size_t)(m >> 1)];
+            hs[(size_t)m] = hs[(size_t)(m >> 1)];
+            m >>= 1;
+        }
+        hh[(size_t)m] = h;
+        hs[(size_t)m] = s;
+    }
+    int32_t pq_dequeue() {  // dequeue + fixDown: larger child (left on ties), stop when parent >= child
+        const int32_t res = hs[1];
+        const int64_t h = hh[(size_t)n];
+        const int32_t e = hs[(size_t)n];
+        const int64_t nn = --n;
+        if (nn == 0) return res;
+        int64_t kk = 1;
+        while (nn >= 2 * kk) {
+            int64_t j = 2 * kk;
+            if (j < nn && hh[(size_t)j] < hh[(size_t)j + 1]) ++j;
+            if (h >= hh[(size_t)j]) break;
+            hh[(size_t)kk] = hh[(size_t)j];
+            hs[(size_t)kk] = hs[(size_t)j];
+            kk = j;
+        }
+        hh[(size_t)kk] = h;
+        hs[(size_t)kk] = e;
+        return res;
+    }
+    void insert(int64_t h, const uint64_t* r) {
+        if ((uint64_t)(n + 1) * 2 + 2 > mask + 1) rehash(std::max<uint64_t>(16, (mask + 1) * 2));
+        const int32_t s = alloc(h, r);
+        pq_add(s, h);
+        tab_add(s);
+    }
+    // RandomValues.sample for one element with scrambled hash h and row r (Sampler.scala:394-409)
+    void sample(int64_t h, const uint64_t* r) {
+        if (n < k) {
+            if (!contains(h, r)) {
+                insert(h, r);
+                if (h > max_hash) max_hash = h;
+            }
+        } else if (h < max_hash && !contains(h, r)) {
+            const int32_t old = pq_dequeue();  // elements -= samples.dequeue()._1
+            tab_remove(old);
+            free_slots.push_back(old);
+            insert(h, r);
+            max_hash = hh[1];
+        }
+    }
+    // the members as (hash, row) ascending by (hash, row words) -- the device set's order
+    void members(std::vector<int64_t>& out_h, std::vector<uint64_t>& out_rows) const {
+        std::vector<int32_t> ord(hs.begin() + 1, hs.begin() + 1 + n);
+        std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
+            if (slot_h[(size_t)a] != slot_h[(size_t)b]) return slot_h[(size_t)a] < slot_h[(size_t)b];
+            return std::lexicographical_compare(row(a), row(a) + words, row(b), row(b) + words);
+        });
+        out_h.resize((size_t)n);
+        out_rows.resize((size_t)(n * words));
+        for (int64_t i = 0; i < n; ++i) {
+            out_h[(size_t)i] = slot_h[(size_t)ord[(size_t)i]];
+            std::copy(row(ord[(size_t)i]), row(ord[(size_t)i]) + words, out_rows.begin() + (std::ptrdiff_t)(i * words));
+        }
+    }
+    void reset(int64_t kk, int64_t wwords) {
+        k = kk;
+        words = wwords;
+        n = 0;
+        hh.assign((size_t)std::min<int64_t>(kk + 2, 1 << 12), INT64_MIN);
+        hs.assign(hh.size(), -1);
+        rows.clear();
+        slot_h.clear();
+        free_slots.clear();
+        max_hash = INT64_MIN;
+        rehash(16);
     }
 };
 

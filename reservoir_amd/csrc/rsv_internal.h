@@ -188,4 +188,30 @@ int distinct_settle(DistinctState* d, hipStream_t st);
 // ordered samplers: keep every replayed candidate on the host for rsv_export_log (opt-in)
 void distinct_retain_log(DistinctState* d, bool on);
 
+// ---- distinct over fixed-width byte keys (rsv_wide.hip; key_width 16..256, a multiple of 8) ------
+// The same contract as the distinct_* functions above (which forward here for key_width > 8); keys
+// are rows of key_width / 8 int64 words, hashes precomputed (src kWideSrcHashes) or UUID.hashCode of
+// 16-byte rows (kWideSrcUuid).  Every call completes its device work before it returns.
+struct WideDistinct;
+WideDistinct* wide_create(int32_t k, int key_width, int src, int64_t r0, int64_t r1, bool ordered, int* status);
+void wide_destroy(WideDistinct* d);
+void wide_set_timer(WideDistinct* d, KernelTimer* t);
+int64_t wide_size(const WideDistinct* d);
+const void* wide_keys_dev(const WideDistinct* d);
+bool wide_is_ordered(const WideDistinct* d);
+int wide_sample_device(WideDistinct* d, const void* keys, const int64_t* hashes, int64_t n, hipStream_t st);
+int wide_finalize(WideDistinct* d, hipStream_t st);
+int wide_publish(WideDistinct* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st);
+int wide_export(WideDistinct* d, void* keys_dev, int64_t* hash_dev, hipStream_t st);
+void wide_info(const WideDistinct* d, int32_t* ordered, int32_t* tied, int32_t* retained, int64_t* size,
+               int64_t* max_hash, int64_t* log_entries);
+int wide_merge_parts(WideDistinct* d, const void* keys_dev, const int64_t* hash_dev, const int64_t* part_n,
+                     int32_t parts, int64_t part_len, hipStream_t st);
+int wide_export_row(WideDistinct* d, int64_t* row, int64_t count, hipStream_t st);
+int wide_merge_rows(WideDistinct* d, const int64_t* rows, int32_t parts, int64_t stride, hipStream_t st);
+void wide_retain_log(WideDistinct* d, bool on);
+int wide_log_export(WideDistinct* d, int64_t bound, int64_t* out_h, void* out_k, int64_t cap, int64_t* out_n,
+                    hipStream_t st);
+int wide_log_merge(WideDistinct* d, const int64_t* h, const void* keys, int64_t n, int64_t seen, hipStream_t st);
+
 }  // namespace rsv

@@ -128,6 +128,11 @@ struct rsv_sampler {
     // whether the caller still owes those elements' keys (rsv_fill_slots)
     int64_t* idx_offs_d = nullptr;
     bool keys_owed = false;
+    // rsv_abort_indexed: the slot indices before the pending index-only batch, and its start
+    int64_t* idx_bak_d = nullptr;
+    bool idx_fresh = false;
+    int64_t idx_base = 0;
+    AlgoLState idx_algo_l;  // JAVA_L: java.util.Random and W before the batch's events
     // DISTINCT
     DistinctState* distinct = nullptr;
     int hash_kind = kHashIdentity;
@@ -482,7 +487,7 @@ rsv_status flush_stage(rsv_sampler* s) {
 void free_all(rsv_sampler* s) {
     // callers have synchronized the stream: nothing queued touches these any more
     if (s->slots && s->win_zero && give_clean_slots(s->slots, s->k, s->kw, s->device)) s->slots = nullptr;
-    void* ds[] = {s->slots, s->ev_pos_d, s->ev_slot_d, s->chunk_d, s->chunk_hash_d, s->idx_offs_d};
+    void* ds[] = {s->slots, s->ev_pos_d, s->ev_slot_d, s->chunk_d, s->chunk_hash_d, s->idx_offs_d, s->idx_bak_d};
     for (void* p : ds) pool_device_free(p);
     for (int b = 0; b < 2; ++b) {
         pool_host_free(s->stage_h[b]);
@@ -503,7 +508,8 @@ int resolve_hash_kind(int32_t hk, int kw) {
     case RSV_HASH_JAVA_LONG: return kHashJavaLong;
     case RSV_HASH_JAVA_INT: return kHashJavaInt;
     case RSV_HASH_PRECOMPUTED: return kHashPrecomputed;
-    default: return kw == 4 ? kHashJavaInt : kHashJavaLong;  // B#hashCode (Sampler.scala:75)
+    default:  // B#hashCode (Sampler.scala:75): Integer / Long / java.util.UUID
+        return kw == 4 ? kHashJavaInt : kw == 16 ? kHashUuid : kHashJavaLong;
     }
 }
 
@@ -549,12 +555,19 @@ rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out) {
     // validateSharedParams, Sampler.scala:79-83
     if (cfg->max_sample_size > kMaxSize) return fail(RSV_E_ILLEGAL_ARGUMENT, "maxSampleSize exceeds VM limit");
     if (cfg->max_sample_size <= 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "maxSampleSize must be positive");
-    const bool wide = cfg->key_width > 8 && cfg->key_width <= 256 && cfg->key_width % 8 == 0;
-    if (cfg->key_width != 4 && cfg->key_width != 8 && !(wide && cfg->kind == RSV_KIND_ELEMENTS))
-        return fail(RSV_E_ILLEGAL_ARGUMENT,
-                    "key_width must be 4 or 8 (ELEMENTS also: a multiple of 8 up to 256 bytes)");
     if (cfg->kind != RSV_KIND_ELEMENTS && cfg->kind != RSV_KIND_DISTINCT)
         return fail(RSV_E_ILLEGAL_ARGUMENT, "unknown sampler kind");
+    // key widths: Int (4), Long (8), fixed-width byte keys (a multiple of 8 in 16..256: UUID = 16).
+    // Any other width is a request this build does not implement (the reference has no width).
+    const bool wide = cfg->key_width > 8 && cfg->key_width <= 256 && cfg->key_width % 8 == 0;
+    if (cfg->key_width != 4 && cfg->key_width != 8 && !wide)
+        return fail(RSV_E_UNSUPPORTED, "key_width must be 4, 8 or a multiple of 8 in 16..256 bytes");
+    // byte keys have no Long/Int hashCode: DISTINCT takes the caller's hash (PRECOMPUTED) or, for
+    // 16-byte keys, java.util.UUID.hashCode (DEFAULT)
+    if (wide && cfg->kind == RSV_KIND_DISTINCT && cfg->hash_kind != RSV_HASH_PRECOMPUTED &&
+        !(cfg->hash_kind == RSV_HASH_DEFAULT && cfg->key_width == 16))
+        return fail(RSV_E_UNSUPPORTED, "DISTINCT over byte keys needs RSV_HASH_PRECOMPUTED (or RSV_HASH_DEFAULT = "
+                                       "java.util.UUID.hashCode for 16-byte keys)");
     if (cfg->kind == RSV_KIND_ELEMENTS && cfg->engine != RSV_ENGINE_PHILOX_R && cfg->engine != RSV_ENGINE_JAVA_L)
         return fail(RSV_E_ILLEGAL_ARGUMENT, "unknown engine");
     if (cfg->hash_kind < RSV_HASH_DEFAULT || cfg->hash_kind > RSV_HASH_PRECOMPUTED)
@@ -607,7 +620,8 @@ rsv_status rsv_create(const rsv_config* cfg, rsv_sampler** out) {
         switch (cfg->distinct_order) {
         case RSV_DISTINCT_SET: ordered = false; break;
         case RSV_DISTINCT_ORDERED: ordered = true; break;
-        default: ordered = s->hash_kind == kHashJavaLong || s->hash_kind == kHashPrecomputed;  // may collide
+        default:  // hashes that may collide
+            ordered = s->hash_kind == kHashJavaLong || s->hash_kind == kHashPrecomputed || s->hash_kind == kHashUuid;
         }
         s->distinct = distinct_create((int32_t)s->k, s->kw, s->hash_kind, r0, r1, ordered, &st);
         if (!s->distinct) {
@@ -724,6 +738,7 @@ rsv_status rsv_sample_indexed(rsv_sampler* s, int64_t n, int64_t* slot_offsets_h
     DeviceGuard g(s->device);
     if (rsv_status st = flush_stage(s)) return st;  // keep global index order
     if (!s->idx_offs_d) RSV_HIP_TRY(pool_device_alloc((void**)&s->idx_offs_d, (size_t)s->k * 8));
+    if (!s->idx_bak_d) RSV_HIP_TRY(pool_device_alloc((void**)&s->idx_bak_d, (size_t)s->k * 8));
     touch(s);
     const int64_t base = s->count;
     if (!s->win_zero) {  // never-used block: full init
@@ -732,6 +747,12 @@ rsv_status rsv_sample_indexed(rsv_sampler* s, int64_t n, int64_t* slot_offsets_h
     }
     const bool fresh = !s->slots_init;
     s->win_zero = false;
+    // the state rsv_abort_indexed restores (a throwing `map` leaves the slots consistent)
+    s->idx_fresh = fresh;
+    s->idx_base = base;
+    s->idx_algo_l = s->algo_l;
+    if (!fresh)
+        RSV_HIP_TRY(hipMemcpyAsync(s->idx_bak_d, s->slot_idx, (size_t)s->k * 8, hipMemcpyDeviceToDevice, s->stream));
     if (s->cfg.engine == RSV_ENGINE_JAVA_L) {  // the reference's own events (S:261-273 skips by them)
         s->ev_pos_h.clear();
         s->ev_slot_h.clear();
@@ -783,6 +804,24 @@ rsv_status rsv_fill_slots(rsv_sampler* s, const void* keys_host) {
     }
     RSV_HIP_TRY(e);
     RSV_HIP_TRY(sync_stream(s));  // the caller's buffer is theirs again
+    s->keys_owed = false;
+    return RSV_OK;
+}
+
+rsv_status rsv_abort_indexed(rsv_sampler* s) {
+    if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
+    if (!s->keys_owed) return fail(RSV_E_ILLEGAL_STATE, "rsv_abort_indexed without a pending rsv_sample_indexed");
+    DeviceGuard g(s->device);
+    touch(s);
+    if (s->idx_fresh)  // the slots were never initialised before the batch: empty them again
+        RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream, s->k1_ticket));
+    else  // the changed slots still hold their old keys: their old indices make them whole again
+        RSV_HIP_TRY(hipMemcpyAsync(s->slot_idx, s->idx_bak_d, (size_t)s->k * 8, hipMemcpyDeviceToDevice, s->stream));
+    RSV_HIP_TRY(sync_stream(s));
+    s->slots_init = s->win_zero = true;
+    s->pub_valid = false;
+    s->count = s->idx_base;
+    s->algo_l = s->idx_algo_l;
     s->keys_owed = false;
     return RSV_OK;
 }
@@ -1132,7 +1171,9 @@ rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t par
     if (rsv_status st = check_open(s)) return st;
     if (parts < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative parts");
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
-        if (row_stride < 2 * (int64_t)s->k + 6) return fail(RSV_E_ILLEGAL_ARGUMENT, "row_stride shorter than a packed row");
+        // [keys (k, as int64 words: key_width / 8 each for byte keys) | hashes (k) | 6 meta words]
+        const int64_t row_len = (int64_t)s->k * (1 + (s->kw > 8 ? s->kw / 8 : 1)) + 6;
+        if (row_stride < row_len) return fail(RSV_E_ILLEGAL_ARGUMENT, "row_stride shorter than a packed row");
         if (parts > 0 && !rows_dev) return fail(RSV_E_NULL_POINTER, "rows_dev is NULL");
         DeviceGuard g(s->device);
         touch(s);

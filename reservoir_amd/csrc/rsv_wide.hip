@@ -1,0 +1,998 @@
+// rsv_wide.hip -- Sampler.distinct over fixed-width byte keys (RandomValues, Sampler.scala:383-412,
+// for a B of key_width = 16..256 bytes with value equality: java.util.UUID, a case class of
+// primitives).  The hash is the caller's `hash: B => Long` (RSV_HASH_PRECOMPUTED, int64 per element
+// beside the keys) or, for 16-byte keys, java.util.UUID.hashCode of the row (RSV_HASH_DEFAULT).
+//
+// The reference keeps the k distinct elements with the smallest scrambled hash
+// h = byteswap64(r1 ^ byteswap64(r0 ^ hash(e))) (Sampler.scala:396-407); `elements.contains` is
+// B.equals, i.e. equality of the key bytes.  Layout and passes (DESIGN.md §5 "wide distinct"):
+//   filter   one streaming pass per chunk over the HASHES (8 B per element; the key rows are not
+//            read): h <= bound (the set's maximum once full, inclusive) -> (h, batch offset)
+//            staged per wave in LDS, appended B at a time
+//   gather   the candidates' rows (key_width bytes each) -- the only key bytes that move
+//   merge    set + candidates -> radix sort by h -> runs of equal h ordered by the key words
+//            (one thread per run; a run longer than 64 entries takes a comparison merge sort of the
+//            whole merge instead) -> drop equal (h, key) -> the first k are the new set, ascending by
+//            (h, key words as unsigned 64-bit, word 0 first)
+// The chunks grow geometrically (each ~4 seen lengths long, so ~4k candidates a chunk), so a 5e8-key
+// batch takes ~6 chunks.  Ordered mode (the reference's sequential semantics for any hash) logs every
+// candidate (h, global index, row) on the device; when the set's boundary hash bucket holds more
+// distinct elements than the set keeps, the log is replayed in arrival order through the host replica
+// HostValuesWide (scala PriorityQueue tie order) -- the same scheme as rsv_distinct.hip's ordered mode.
+#include <rocprim/device/device_merge_sort.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/reservoir_hip.h"
+#include "rsv_device.h"
+#include "rsv_host_values.h"
+#include "rsv_internal.h"
+
+namespace rsv {
+
+namespace {
+
+constexpr int kWBlock = 256;
+constexpr int kRunMax = 64;         // longest run of equal h ordered by one thread
+constexpr int kWideU = 8;           // 16-B loads in flight per lane in the filter
+constexpr int64_t kWideGrid = 256 * 32;
+typedef long long w2i64 __attribute__((ext_vector_type(2)));
+
+inline unsigned wgrid(int64_t n, int64_t cap = 65535) {
+    return (unsigned)std::min<int64_t>(std::max<int64_t>((n + kWBlock - 1) / kWBlock, 1), cap);
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt_w() {
+    const uint32_t lane = threadIdx.x & 63;
+    return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+template <int SRC>
+__device__ __forceinline__ int64_t wide_hash(const int64_t* hashes, const uint64_t* rows, int64_t i) {
+    if constexpr (SRC == kWideSrcHashes) return hashes[i];
+    else return uuid_hash_code(rows[2 * i], rows[2 * i + 1]);
+}
+
+// Candidate output of the filter: each wave stages (h, offset) in LDS and appends B at a time under
+// one reservation atomic (the counter is a single contended word); the workgroup's leftovers go out
+// under one atomic at the end.
+struct WideOut {
+    static constexpr uint32_t B = 128;
+    static constexpr uint32_t Q = B + 64;
+    int64_t* qh;
+    int64_t* qi;
+    uint32_t qn;
+    int64_t* cand_h;
+    int64_t* cand_i;
+    unsigned long long* counter;
+    int64_t cap;
+
+    __device__ __forceinline__ void write_at(unsigned long long base, uint32_t from, uint32_t cnt) {
+        const uint32_t lane = threadIdx.x & 63;
+        for (uint32_t j = lane; j < cnt; j += 64) {
+            const unsigned long long pos = base + j;
+            if ((int64_t)pos < cap) {
+                cand_h[pos] = qh[from + j];
+                cand_i[pos] = qi[from + j];
+            }
+        }
+    }
+    __device__ __forceinline__ void push(bool c, int64_t h, int64_t idx) {
+        const unsigned long long bal = __ballot(c);
+        if (bal == 0) return;
+        if (c) {
+            const uint32_t pos = qn + __popcll(bal & lanemask_lt_w());
+            qh[pos] = h;
+            qi[pos] = idx;
+        }
+        qn += (uint32_t)__popcll(bal);
+        if (qn >= B) {
+            qn -= B;
+            __builtin_amdgcn_wave_barrier();
+            unsigned long long base = 0;
+            if ((threadIdx.x & 63) == 0) base = atomicAdd(counter, (unsigned long long)B);
+            base = __shfl(base, 0);
+            write_at(base, qn, B);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __device__ __forceinline__ void flush_block(uint32_t* s_q, unsigned long long* s_base) {
+        const uint32_t w = threadIdx.x >> 6;
+        __builtin_amdgcn_wave_barrier();
+        if ((threadIdx.x & 63) == 0) s_q[w] = qn;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (int i = 0; i < kWBlock / 64; ++i) tot += s_q[i];
+            *s_base = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+        }
+        __syncthreads();
+        uint32_t pre = 0;
+        for (uint32_t i = 0; i < w; ++i) pre += s_q[i];
+        if (qn) write_at(*s_base + pre, 0, qn);
+        qn = 0;
+    }
+};
+
+// The filter over precomputed hashes: 16-B non-temporal loads (two hashes each), kWideU in flight per
+// lane; the <= 1 head element before the first 16-B boundary and the odd tail go through the scalar
+// loops.  Loop bounds are wave-uniform (tile starts), so the ballots see every lane.
+__global__ __launch_bounds__(kWBlock) void wide_filter_hashes(const int64_t* __restrict__ hashes, int64_t n, int64_t r0,
+                                                              int64_t r1, int64_t bound, int64_t* __restrict__ cand_h,
+                                                              int64_t* __restrict__ cand_i,
+                                                              unsigned long long* __restrict__ counter, int64_t cap) {
+    __shared__ int64_t sh_h[kWBlock / 64][WideOut::Q];
+    __shared__ int64_t sh_i[kWBlock / 64][WideOut::Q];
+    __shared__ uint32_t s_q[kWBlock / 64];
+    __shared__ unsigned long long s_base;
+    WideOut out{sh_h[threadIdx.x >> 6], sh_i[threadIdx.x >> 6], 0u, cand_h, cand_i, counter, cap};
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t head = std::min<int64_t>(n, (int64_t)(((16u - ((uintptr_t)hashes & 15u)) & 15u) / 8u));
+    const w2i64* hv = reinterpret_cast<const w2i64*>(hashes + head);
+    const int64_t n_vec = (n - head) / 2;
+    for (int64_t t0 = 0; t0 < n_vec; t0 += T * kWideU) {
+        w2i64 x[kWideU];
+#pragma unroll
+        for (int u = 0; u < kWideU; ++u) {
+            const int64_t v = t0 + u * T + tid;
+            x[u] = __builtin_nontemporal_load(hv + (v < n_vec ? v : n_vec - 1));
+        }
+        int64_t h[kWideU][2];
+        bool c[kWideU][2];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < kWideU; ++u) {
+            const bool ok = t0 + u * T + tid < n_vec;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                h[u][e] = scramble(r0, r1, x[u][e]);
+                c[u][e] = ok && h[u][e] <= bound;
+                any |= c[u][e];
+            }
+        }
+        if (__any(any)) {
+#pragma unroll
+            for (int u = 0; u < kWideU; ++u)
+#pragma unroll
+                for (int e = 0; e < 2; ++e) out.push(c[u][e], h[u][e], head + (t0 + u * T + tid) * 2 + e);
+        }
+    }
+    for (int64_t i0 = 0; i0 < head; i0 += T) {
+        const int64_t i = i0 + tid;
+        const int64_t hh = i < head ? scramble(r0, r1, hashes[i]) : 0;
+        out.push(i < head && hh <= bound, hh, i);
+    }
+    for (int64_t i0 = head + 2 * n_vec; i0 < n; i0 += T) {
+        const int64_t i = i0 + tid;
+        const int64_t hh = i < n ? scramble(r0, r1, hashes[i]) : 0;
+        out.push(i < n && hh <= bound, hh, i);
+    }
+    out.flush_block(s_q, &s_base);
+}
+
+// The filter over 16-byte UUID rows (the hash is UUID.hashCode of the row): two 8-B non-temporal
+// loads per row (rows need only 8-B alignment), kWideU rows in flight per lane.
+__global__ __launch_bounds__(kWBlock) void wide_filter_uuid(const uint64_t* __restrict__ rows, int64_t n, int64_t r0,
+                                                            int64_t r1, int64_t bound, int64_t* __restrict__ cand_h,
+                                                            int64_t* __restrict__ cand_i,
+                                                            unsigned long long* __restrict__ counter, int64_t cap) {
+    __shared__ int64_t sh_h[kWBlock / 64][WideOut::Q];
+    __shared__ int64_t sh_i[kWBlock / 64][WideOut::Q];
+    __shared__ uint32_t s_q[kWBlock / 64];
+    __shared__ unsigned long long s_base;
+    WideOut out{sh_h[threadIdx.x >> 6], sh_i[threadIdx.x >> 6], 0u, cand_h, cand_i, counter, cap};
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t t0 = 0; t0 < n; t0 += T * kWideU) {
+        uint64_t a[kWideU], b[kWideU];
+#pragma unroll
+        for (int u = 0; u < kWideU; ++u) {
+            const int64_t i = std::min<int64_t>(t0 + u * T + tid, n - 1);
+            a[u] = __builtin_nontemporal_load(rows + 2 * i);
+            b[u] = __builtin_nontemporal_load(rows + 2 * i + 1);
+        }
+        int64_t h[kWideU];
+        bool c[kWideU];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < kWideU; ++u) {
+            h[u] = scramble(r0, r1, uuid_hash_code(a[u], b[u]));
+            c[u] = t0 + u * T + tid < n && h[u] <= bound;
+            any |= c[u];
+        }
+        if (__any(any)) {
+#pragma unroll
+            for (int u = 0; u < kWideU; ++u) out.push(c[u], h[u], t0 + u * T + tid);
+        }
+    }
+    out.flush_block(s_q, &s_base);
+}
+
+// No bound (the set still filling): every element is a candidate, element i goes to place i
+template <int SRC>
+__global__ __launch_bounds__(kWBlock) void wide_hash_all(const int64_t* __restrict__ hashes,
+                                                         const uint64_t* __restrict__ rows, int64_t n, int64_t r0,
+                                                         int64_t r1, int64_t* __restrict__ out_h,
+                                                         int64_t* __restrict__ out_i) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        out_h[i] = scramble(r0, r1, wide_hash<SRC>(hashes, rows, i));
+        out_i[i] = i;
+    }
+}
+
+// candidate rows: out[j] = keys[idx[j]] (one thread per 8-B word: a row's words are adjacent lanes)
+__global__ __launch_bounds__(kWBlock) void wide_gather_rows(const uint64_t* __restrict__ keys,
+                                                            const int64_t* __restrict__ idx, int64_t c, int32_t words,
+                                                            uint64_t* __restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t total = c * words;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+        const int64_t j = t / words;
+        out[t] = keys[idx[j] * words + (t - j * words)];
+    }
+}
+
+// ordered mode: the chunk's candidates onto the log as (h, global index, row)
+__global__ __launch_bounds__(kWBlock) void wide_log_append(const int64_t* __restrict__ ch, const int64_t* __restrict__ ci,
+                                                           const uint64_t* __restrict__ ck, int64_t c, int32_t words,
+                                                           int64_t base, int64_t* __restrict__ lh,
+                                                           int64_t* __restrict__ lg, uint64_t* __restrict__ lk) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < c * words; t += stride) {
+        lk[t] = ck[t];
+        if (t < c) {
+            lh[t] = ch[t];
+            lg[t] = base + ci[t];
+        }
+    }
+}
+
+// entries of a merge: [0, m) the set, [m, N) the candidates
+struct WRows {
+    const uint64_t* set_k;
+    const uint64_t* cand_k;
+    int64_t m;
+    int32_t words;
+    __host__ __device__ const uint64_t* operator()(uint32_t e) const {
+        return (int64_t)e < m ? set_k + (size_t)e * words : cand_k + ((size_t)e - (size_t)m) * words;
+    }
+};
+
+__host__ __device__ inline int row_cmp(const uint64_t* a, const uint64_t* b, int32_t words) {
+    for (int32_t w = 0; w < words; ++w)
+        if (a[w] != b[w]) return a[w] < b[w] ? -1 : 1;
+    return 0;
+}
+
+// the comparison sort of the fallback: (h, key words)
+struct WLess {
+    const int64_t* h;
+    WRows R;
+    __host__ __device__ bool operator()(uint32_t a, uint32_t b) const {
+        if (h[a] != h[b]) return h[a] < h[b];
+        return row_cmp(R(a), R(b), R.words) < 0;
+    }
+};
+
+__global__ __launch_bounds__(kWBlock) void wide_merge_init(const int64_t* __restrict__ set_h,
+                                                           const int64_t* __restrict__ cand_h, int64_t m, int64_t N,
+                                                           int64_t* __restrict__ eh, uint32_t* __restrict__ ev) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += stride) {
+        eh[e] = e < m ? set_h[e] : cand_h[e - m];
+        ev[e] = (uint32_t)e;
+    }
+}
+
+// after the radix sort by h: each run of equal h (almost always one entry; a run is one key's
+// duplicates, or distinct keys whose hashes collide) is ordered by its key words, in place, by the
+// thread at its start.  A run longer than kRunMax sets ctl[1]: the merge redoes its order with the
+// comparison sort.
+__global__ __launch_bounds__(kWBlock) void wide_run_fix(const int64_t* __restrict__ eh, uint32_t* __restrict__ ev,
+                                                        int64_t N, WRows R, int64_t* __restrict__ ctl) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += stride) {
+        const int64_t h = eh[p];
+        if (p > 0 && eh[p - 1] == h) continue;  // not a run start
+        if (p + 1 >= N || eh[p + 1] != h) continue;
+        int64_t L = 2;
+        while (p + L < N && eh[p + L] == h && L <= kRunMax) ++L;
+        if (L > kRunMax) {
+            atomicOr((unsigned long long*)(ctl + 1), 1ull);
+            continue;
+        }
+        for (int64_t i = 1; i < L; ++i) {
+            const uint32_t x = ev[p + i];
+            int64_t j = i;
+            while (j > 0 && row_cmp(R(ev[p + j - 1]), R(x), R.words) > 0) {
+                ev[p + j] = ev[p + j - 1];
+                --j;
+            }
+            ev[p + j] = x;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kWBlock) void wide_gather_h(const int64_t* __restrict__ eh_by_entry,
+                                                         const uint32_t* __restrict__ ev, int64_t N,
+                                                         int64_t* __restrict__ eh) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += stride) eh[p] = eh_by_entry[ev[p]];
+}
+
+// flag = first of each run of identical (h, key)
+__global__ __launch_bounds__(kWBlock) void wide_flags(const int64_t* __restrict__ eh, const uint32_t* __restrict__ ev,
+                                                      int64_t N, WRows R, uint32_t* __restrict__ flags) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += stride)
+        flags[p] = (p == 0 || eh[p] != eh[p - 1] || row_cmp(R(ev[p]), R(ev[p - 1]), R.words) != 0) ? 1u : 0u;
+}
+
+// the first k distinct entries -> the new set; ctl[2] = distinct count, ctl[3] = the largest kept h,
+// ctl[4] = rank k ties rank k - 1 on h (the boundary bucket holds more distinct elements than kept)
+__global__ __launch_bounds__(kWBlock) void wide_emit(const int64_t* __restrict__ eh, const uint32_t* __restrict__ ev,
+                                                     const uint32_t* __restrict__ flags, const uint32_t* __restrict__ pos,
+                                                     int64_t N, int64_t k, WRows R, int64_t* __restrict__ out_h,
+                                                     uint64_t* __restrict__ out_k, int64_t* __restrict__ ctl) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += stride) {
+        const int64_t r = pos[p];
+        if (flags[p]) {
+            if (r < k) {
+                out_h[r] = eh[p];
+                const uint64_t* src = R(ev[p]);
+                for (int32_t w = 0; w < R.words; ++w) out_k[r * R.words + w] = src[w];
+                if (r == k - 1) ctl[3] = eh[p];
+            } else if (r == k && eh[p - 1] == eh[p]) {
+                ctl[4] = 1;
+            }
+        }
+        if (p == N - 1) {
+            const int64_t nd = r + (int64_t)flags[p];
+            ctl[2] = nd;
+            if (nd <= k) ctl[3] = eh[p];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kWBlock) void wide_iota(uint32_t* __restrict__ v, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) v[i] = (uint32_t)i;
+}
+
+// the log in arrival order: out[j] = log[perm[j]]
+__global__ __launch_bounds__(kWBlock) void wide_log_permute(const uint32_t* __restrict__ perm,
+                                                            const int64_t* __restrict__ lh,
+                                                            const uint64_t* __restrict__ lk, int64_t n, int32_t words,
+                                                            int64_t* __restrict__ oh, uint64_t* __restrict__ ok) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n * words; t += stride) {
+        const int64_t j = t / words;
+        const int64_t src = perm[j];
+        ok[t] = lk[src * words + (t - j * words)];
+        if (t < n) oh[t] = lh[perm[t]];
+    }
+}
+
+// packed row: [key words (k x words) | hashes (k) | n, count, tied, max_hash, log_retained, ordered]
+__global__ __launch_bounds__(kWBlock) void wide_export_row(const int64_t* __restrict__ set_h,
+                                                           const uint64_t* __restrict__ set_k, int64_t m, int64_t k,
+                                                           int32_t words, int64_t* __restrict__ row, int64_t count,
+                                                           int64_t tied, int64_t mx, int64_t retained,
+                                                           int64_t ordered) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t kw = k * words;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < kw + k; t += stride) {
+        if (t < kw) row[t] = t < m * words ? (int64_t)set_k[t] : 0;
+        else row[t] = t - kw < m ? set_h[t - kw] : 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int64_t* meta = row + kw + k;
+        meta[0] = m;
+        meta[1] = count;
+        meta[2] = tied;
+        meta[3] = mx;
+        meta[4] = retained;
+        meta[5] = ordered;
+    }
+}
+
+}  // namespace
+
+struct WideDistinct {
+    int32_t k = 0;
+    int32_t words = 0;  // key_width / 8
+    int src = kWideSrcHashes;
+    int64_t r0 = 0, r1 = 0;
+    bool ordered = false;
+    int64_t m = 0;                // set size
+    int64_t top = INT64_MIN;      // the set's largest h (valid when m > 0)
+    bool tied = false;            // full, and the boundary hash bucket holds more distinct elements
+    bool exact = true;            // ordered: the set arrays hold the reference's set
+    int64_t seen = 0;             // elements sampled (chunk sizing)
+    KernelTimer* timer = nullptr;
+    // device
+    int64_t* set_h = nullptr;     // [set_cap] ascending (h, key words)
+    uint64_t* set_k = nullptr;
+    int64_t* set_h2 = nullptr;    // the merge's output (swapped in)
+    uint64_t* set_k2 = nullptr;
+    int64_t set_cap = 0;
+    int64_t* cand_h = nullptr;    // [cand_cap] candidates: h, batch offset, row
+    int64_t* cand_i = nullptr;
+    uint64_t* cand_k = nullptr;
+    int64_t cand_cap = 0;
+    int64_t *eh0 = nullptr, *eh1 = nullptr;  // [merge_cap] merge entries
+    uint32_t *ev0 = nullptr, *ev1 = nullptr, *flags = nullptr, *pos = nullptr;
+    int64_t merge_cap = 0;
+    void* temp = nullptr;
+    size_t temp_bytes = 0;
+    int64_t* ctl = nullptr;       // [8]: [0] candidate counter [1] long run [2] distinct [3] top [4] tie
+    int64_t* hctl = nullptr;      // pinned copy
+    // ordered mode: the candidate log since the replica's state (h, global index, row), device
+    int64_t* log_h = nullptr;
+    int64_t* log_g = nullptr;
+    uint64_t* log_k = nullptr;
+    int64_t log_n = 0, log_cap = 0, log_limit = 0;
+    HostValuesWide rep;           // the exact RandomValues state before the log's first entry
+    bool rep_stale = false;       // a merge replaced the set: rebuild the replica from it first
+    bool merged = false;          // the log still describes the pre-merge history (rsv_export_log)
+    bool retain = false;          // keep the consumed log on the host (rsv_retain_log)
+    bool arch_ok = true;
+    std::vector<int64_t> arch_h;  // consumed candidates in arrival order
+    std::vector<uint64_t> arch_k;
+};
+
+namespace {
+
+hipError_t walloc(void** p, size_t bytes) { return pool_device_alloc(p, bytes ? bytes : 16); }
+
+// replace a device buffer by a larger one (contents kept when `keep`); the stream is synchronized
+// before the old block goes back to the pool
+hipError_t wgrow(void** p, size_t old_bytes, size_t new_bytes, bool keep, hipStream_t st) {
+    void* q = nullptr;
+    hipError_t e = walloc(&q, new_bytes);
+    if (e != hipSuccess) return e;
+    if (keep && *p && old_bytes) e = hipMemcpyAsync(q, *p, old_bytes, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess && *p) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        pool_device_free(q);
+        return e;
+    }
+    pool_device_free(*p);
+    *p = q;
+    return hipSuccess;
+}
+
+int64_t wgrown(int64_t cur, int64_t need) {
+    int64_t c = std::max<int64_t>(cur, 1024);
+    while (c < need) c *= 2;
+    return c;
+}
+
+hipError_t ensure_set(WideDistinct* d, int64_t need, hipStream_t st) {
+    need = std::min<int64_t>(need, d->k);
+    if (need <= d->set_cap) return hipSuccess;
+    const int64_t c = std::min<int64_t>(wgrown(d->set_cap, need), d->k);
+    const size_t W = (size_t)d->words * 8;
+    hipError_t e;
+    if ((e = wgrow((void**)&d->set_h, (size_t)d->m * 8, (size_t)c * 8, true, st))) return e;
+    if ((e = wgrow((void**)&d->set_k, (size_t)d->m * W, (size_t)c * W, true, st))) return e;
+    if ((e = wgrow((void**)&d->set_h2, 0, (size_t)c * 8, false, st))) return e;
+    if ((e = wgrow((void**)&d->set_k2, 0, (size_t)c * W, false, st))) return e;
+    d->set_cap = c;
+    return hipSuccess;
+}
+
+hipError_t ensure_cand(WideDistinct* d, int64_t need, hipStream_t st) {
+    if (need <= d->cand_cap) return hipSuccess;
+    const int64_t c = wgrown(d->cand_cap, need);
+    hipError_t e;
+    if ((e = wgrow((void**)&d->cand_h, 0, (size_t)c * 8, false, st))) return e;
+    if ((e = wgrow((void**)&d->cand_i, 0, (size_t)c * 8, false, st))) return e;
+    if ((e = wgrow((void**)&d->cand_k, 0, (size_t)c * d->words * 8, false, st))) return e;
+    d->cand_cap = c;
+    return hipSuccess;
+}
+
+hipError_t ensure_merge(WideDistinct* d, int64_t N, hipStream_t st) {
+    if (N <= d->merge_cap) return hipSuccess;
+    const int64_t c = wgrown(d->merge_cap, N);
+    hipError_t e;
+    if ((e = wgrow((void**)&d->eh0, 0, (size_t)c * 8, false, st))) return e;
+    if ((e = wgrow((void**)&d->eh1, 0, (size_t)c * 8, false, st))) return e;
+    if ((e = wgrow((void**)&d->ev0, 0, (size_t)c * 4, false, st))) return e;
+    if ((e = wgrow((void**)&d->ev1, 0, (size_t)c * 4, false, st))) return e;
+    if ((e = wgrow((void**)&d->flags, 0, (size_t)c * 4, false, st))) return e;
+    if ((e = wgrow((void**)&d->pos, 0, (size_t)c * 4, false, st))) return e;
+    size_t a = 0, b = 0, g = 0;
+    if ((e = rocprim::radix_sort_pairs(nullptr, a, (int64_t*)nullptr, (int64_t*)nullptr, (uint32_t*)nullptr,
+                                       (uint32_t*)nullptr, (size_t)c)))
+        return e;
+    if ((e = rocprim::exclusive_scan(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)c,
+                                     rocprim::plus<uint32_t>())))
+        return e;
+    if ((e = rocprim::radix_sort_pairs(nullptr, g, (int64_t*)nullptr, (int64_t*)nullptr, (uint32_t*)nullptr,
+                                       (uint32_t*)nullptr, (size_t)c)))
+        return e;
+    const size_t tb = std::max(a, std::max(b, g));
+    if (tb > d->temp_bytes) {
+        if ((e = wgrow(&d->temp, 0, tb, false, st))) return e;
+        d->temp_bytes = tb;
+    }
+    d->merge_cap = c;
+    return hipSuccess;
+}
+
+hipError_t ensure_temp(WideDistinct* d, size_t bytes, hipStream_t st) {
+    if (bytes <= d->temp_bytes) return hipSuccess;
+    hipError_t e = wgrow(&d->temp, 0, bytes, false, st);
+    if (e == hipSuccess) d->temp_bytes = bytes;
+    return e;
+}
+
+hipError_t read_ctl(WideDistinct* d, hipStream_t st) {
+    hipError_t e = hipMemcpyAsync(d->hctl, d->ctl, 8 * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e;
+}
+
+// set ∪ candidates [0, c) -> bottom-k by (h, key words), distinct by (h, key); `tied` from this merge
+hipError_t merge_cands(WideDistinct* d, int64_t c, hipStream_t st) {
+    if (c <= 0) return hipSuccess;
+    const int64_t N = d->m + c;
+    hipError_t e;
+    if ((e = ensure_merge(d, N, st))) return e;
+    if ((e = ensure_set(d, std::min<int64_t>(N, d->k), st))) return e;
+    const WRows R{d->set_k, d->cand_k, d->m, d->words};
+    const unsigned g = wgrid(N, 4096);
+    hipLaunchKernelGGL(wide_merge_init, dim3(g), dim3(kWBlock), 0, st, d->set_h, d->cand_h, d->m, N, d->eh0, d->ev0);
+    size_t tb = d->temp_bytes;
+    if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->eh0, d->eh1, d->ev0, d->ev1, (size_t)N, 0, 64, st))) return e;
+    if ((e = hipMemsetAsync(d->ctl, 0, 8 * 8, st))) return e;
+    hipLaunchKernelGGL(wide_run_fix, dim3(g), dim3(kWBlock), 0, st, d->eh1, d->ev1, N, R, d->ctl);
+    auto finish = [&]() -> hipError_t {
+        hipLaunchKernelGGL(wide_flags, dim3(g), dim3(kWBlock), 0, st, d->eh1, d->ev1, N, R, d->flags);
+        size_t sb = d->temp_bytes;
+        hipError_t e2 = rocprim::exclusive_scan(d->temp, sb, d->flags, d->pos, 0u, (size_t)N, rocprim::plus<uint32_t>(),
+                                                st);
+        if (e2) return e2;
+        hipLaunchKernelGGL(wide_emit, dim3(g), dim3(kWBlock), 0, st, d->eh1, d->ev1, d->flags, d->pos, N,
+                           (int64_t)d->k, R, d->set_h2, d->set_k2, d->ctl);
+        if ((e2 = hipGetLastError())) return e2;
+        return read_ctl(d, st);
+    };
+    if ((e = finish())) return e;
+    if (d->hctl[1]) {  // a run of > kRunMax equal hashes: the comparison sort orders the whole merge
+        size_t mb = 0;
+        const WLess less{d->eh0, R};
+        if ((e = rocprim::merge_sort(nullptr, mb, d->ev1, d->ev1, (size_t)N, less, st))) return e;
+        if ((e = ensure_temp(d, mb, st))) return e;
+        hipLaunchKernelGGL(wide_iota, dim3(g), dim3(kWBlock), 0, st, d->ev0, N);
+        mb = d->temp_bytes;
+        if ((e = rocprim::merge_sort(d->temp, mb, d->ev0, d->ev1, (size_t)N, less, st))) return e;
+        hipLaunchKernelGGL(wide_gather_h, dim3(g), dim3(kWBlock), 0, st, d->eh0, d->ev1, N, d->eh1);
+        if ((e = hipMemsetAsync(d->ctl, 0, 8 * 8, st))) return e;
+        if ((e = finish())) return e;
+    }
+    const int64_t nd = d->hctl[2];
+    d->m = std::min<int64_t>(nd, d->k);
+    d->top = d->hctl[3];
+    d->tied = d->m == d->k && d->hctl[4] != 0;
+    std::swap(d->set_h, d->set_h2);
+    std::swap(d->set_k, d->set_k2);
+    return hipSuccess;
+}
+
+// the device set := the replica's members (ascending (h, key words))
+hipError_t upload_replica(WideDistinct* d, hipStream_t st) {
+    std::vector<int64_t> hs;
+    std::vector<uint64_t> rows;
+    d->rep.members(hs, rows);
+    hipError_t e;
+    if ((e = ensure_set(d, (int64_t)hs.size(), st))) return e;
+    d->m = (int64_t)hs.size();
+    if (d->m) {
+        if ((e = hipMemcpyAsync(d->set_h, hs.data(), hs.size() * 8, hipMemcpyHostToDevice, st))) return e;
+        if ((e = hipMemcpyAsync(d->set_k, rows.data(), rows.size() * 8, hipMemcpyHostToDevice, st))) return e;
+        d->top = hs.back();
+    }
+    return hipStreamSynchronize(st);  // the host vectors are the copies' sources
+}
+
+// the replica from the device set (after a merge replaced it): its members inserted in (h, key) order
+hipError_t rebuild_replica(WideDistinct* d, hipStream_t st) {
+    d->rep.reset(d->k, d->words);
+    d->rep_stale = false;
+    if (!d->m) return hipSuccess;
+    std::vector<int64_t> hs((size_t)d->m);
+    std::vector<uint64_t> rows((size_t)(d->m * d->words));
+    hipError_t e = hipMemcpyAsync(hs.data(), d->set_h, hs.size() * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(rows.data(), d->set_k, rows.size() * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    for (int64_t i = 0; i < d->m; ++i) d->rep.sample(hs[(size_t)i], rows.data() + (size_t)i * d->words);
+    return hipSuccess;
+}
+
+// the log in arrival order on the host: sort by global index on the device, permute, copy back
+hipError_t log_to_host(WideDistinct* d, std::vector<int64_t>& oh, std::vector<uint64_t>& ok, hipStream_t st) {
+    const int64_t n = d->log_n;
+    oh.resize((size_t)n);
+    ok.resize((size_t)(n * d->words));
+    if (!n) return hipSuccess;
+    hipError_t e;
+    if ((e = ensure_merge(d, n, st))) return e;
+    if ((e = ensure_cand(d, n, st))) return e;
+    const unsigned g = wgrid(n, 4096);
+    hipLaunchKernelGGL(wide_iota, dim3(g), dim3(kWBlock), 0, st, d->ev0, n);
+    size_t tb = d->temp_bytes;
+    if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->log_g, d->eh1, d->ev0, d->ev1, (size_t)n, 0, 64, st)))
+        return e;
+    hipLaunchKernelGGL(wide_log_permute, dim3(g), dim3(kWBlock), 0, st, d->ev1, d->log_h, d->log_k, n, d->words,
+                       d->cand_h, d->cand_k);
+    if ((e = hipGetLastError())) return e;
+    if ((e = hipMemcpyAsync(oh.data(), d->cand_h, (size_t)n * 8, hipMemcpyDeviceToHost, st))) return e;
+    if ((e = hipMemcpyAsync(ok.data(), d->cand_k, (size_t)n * d->words * 8, hipMemcpyDeviceToHost, st))) return e;
+    return hipStreamSynchronize(st);
+}
+
+// Consume the log: replay it in arrival order through the replica (the reference's sequential
+// RandomValues), archive it if retained, and make the device set the replica's (exact) set.
+hipError_t replay_log(WideDistinct* d, hipStream_t st) {
+    hipError_t e;
+    if (d->rep_stale && (e = rebuild_replica(d, st))) return e;
+    std::vector<int64_t> oh;
+    std::vector<uint64_t> ok;
+    if ((e = log_to_host(d, oh, ok, st))) return e;
+    for (size_t t = 0; t < oh.size(); ++t) d->rep.sample(oh[t], ok.data() + t * d->words);
+    if (d->retain && d->arch_ok) {
+        if ((int64_t)(d->arch_h.size() + oh.size()) > ((int64_t)1 << 27)) {
+            d->arch_ok = false;
+            d->arch_h.clear();
+            d->arch_k.clear();
+        } else {
+            d->arch_h.insert(d->arch_h.end(), oh.begin(), oh.end());
+            d->arch_k.insert(d->arch_k.end(), ok.begin(), ok.end());
+        }
+    }
+    d->log_n = 0;
+    if ((e = upload_replica(d, st))) return e;
+    d->exact = true;
+    return hipSuccess;
+}
+
+hipError_t ensure_log(WideDistinct* d, int64_t need, hipStream_t st) {
+    if (need <= d->log_cap) return hipSuccess;
+    const int64_t c = wgrown(d->log_cap, need);
+    const size_t W = (size_t)d->words * 8;
+    hipError_t e;
+    if ((e = wgrow((void**)&d->log_h, (size_t)d->log_n * 8, (size_t)c * 8, true, st))) return e;
+    if ((e = wgrow((void**)&d->log_g, (size_t)d->log_n * 8, (size_t)c * 8, true, st))) return e;
+    if ((e = wgrow((void**)&d->log_k, (size_t)d->log_n * W, (size_t)c * W, true, st))) return e;
+    d->log_cap = c;
+    return hipSuccess;
+}
+
+// one chunk [off, off + L) of the batch: filter, rows, log, merge
+hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes, int64_t off, int64_t L,
+                        int64_t gbase, hipStream_t st) {
+    const uint64_t* rows = (const uint64_t*)keys + (size_t)off * d->words;
+    const int64_t* hv = hashes ? hashes + off : nullptr;
+    hipError_t e;
+    int64_t c;
+    // bounded log: replay what it holds before this chunk's candidates take the scratch buffers
+    if (d->ordered && d->log_n > 0 && d->log_n + std::min<int64_t>(L, 8 * (int64_t)d->k + 4096) > d->log_limit)
+        if ((e = replay_log(d, st))) return e;
+    if (d->m < d->k) {  // still filling: every element is a candidate
+        if ((e = ensure_cand(d, L, st))) return e;
+        if (d->src == kWideSrcHashes)
+            hipLaunchKernelGGL(wide_hash_all<kWideSrcHashes>, dim3(wgrid(L, 8192)), dim3(kWBlock), 0, st, hv, rows, L,
+                               d->r0, d->r1, d->cand_h, d->cand_i);
+        else
+            hipLaunchKernelGGL(wide_hash_all<kWideSrcUuid>, dim3(wgrid(L, 8192)), dim3(kWBlock), 0, st, hv, rows, L,
+                               d->r0, d->r1, d->cand_h, d->cand_i);
+        if ((e = hipGetLastError())) return e;
+        c = L;
+    } else {
+        const int64_t bound = d->top;  // inclusive: the boundary bucket's members stay candidates
+        if ((e = ensure_cand(d, 8 * (int64_t)d->k + 4096, st))) return e;
+        const unsigned g = (unsigned)std::min<int64_t>(
+            std::max<int64_t>((L / (d->src == kWideSrcHashes ? 2 * kWideU : kWideU) + kWBlock - 1) / kWBlock, 1),
+            kWideGrid);
+        for (;;) {
+            if ((e = hipMemsetAsync(d->ctl, 0, 8, st))) return e;
+            if (d->timer) d->timer->mark(st);
+            if (d->src == kWideSrcHashes)
+                hipLaunchKernelGGL(wide_filter_hashes, dim3(g), dim3(kWBlock), 0, st, hv, L, d->r0, d->r1, bound,
+                                   d->cand_h, d->cand_i, (unsigned long long*)d->ctl, d->cand_cap);
+            else
+                hipLaunchKernelGGL(wide_filter_uuid, dim3(g), dim3(kWBlock), 0, st, rows, L, d->r0, d->r1, bound,
+                                   d->cand_h, d->cand_i, (unsigned long long*)d->ctl, d->cand_cap);
+            if (d->timer) d->timer->mark(st);
+            if ((e = hipGetLastError())) return e;
+            if ((e = read_ctl(d, st))) return e;
+            c = d->hctl[0];
+            if (c <= d->cand_cap) break;
+            if ((e = ensure_cand(d, c, st))) return e;  // more candidates than room: again, with room
+        }
+    }
+    if (c == 0) return hipSuccess;
+    hipLaunchKernelGGL(wide_gather_rows, dim3(wgrid(c * d->words, 8192)), dim3(kWBlock), 0, st, (const uint64_t*)keys +
+                       (size_t)off * d->words, d->cand_i, c, d->words, d->cand_k);
+    if ((e = hipGetLastError())) return e;
+    if (d->ordered) {
+        if ((e = ensure_log(d, d->log_n + c, st))) return e;
+        hipLaunchKernelGGL(wide_log_append, dim3(wgrid(c * d->words, 8192)), dim3(kWBlock), 0, st, d->cand_h,
+                           d->cand_i, d->cand_k, c, d->words, gbase + off, d->log_h + d->log_n, d->log_g + d->log_n,
+                           d->log_k + (size_t)d->log_n * d->words);
+        if ((e = hipGetLastError())) return e;
+        d->log_n += c;
+    }
+    if ((e = merge_cands(d, c, st))) return e;
+    if (d->ordered) d->exact = !d->tied;  // an uncut boundary bucket leaves one possible set
+    return hipSuccess;
+}
+
+int fail_hip(hipError_t e, const char* what) {
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? RSV_E_OUT_OF_MEMORY : RSV_E_DEVICE;
+}
+
+// a merge of external entries (rows of other ranks, exported states): bottom-k of the union; the
+// replica restarts from the union when next needed (a merged set has no single arrival order --
+// rsv_merge_log is the exact form), the log stays readable for rsv_export_log until the next sample
+int merge_external(WideDistinct* d, const std::vector<std::pair<const int64_t*, const uint64_t*>>& src,
+                   const std::vector<int64_t>& counts, const std::vector<int64_t>& tops,
+                   const std::vector<int32_t>& part_tied, hipStream_t st) {
+    // the tie rule across full runs: the smallest maximum among full parts, tied there
+    int64_t T = d->m == d->k ? d->top : INT64_MAX;
+    bool tiedT = d->m == d->k && d->tied;
+    for (size_t p = 0; p < counts.size(); ++p) {
+        if (counts[p] != d->k) continue;
+        if (tops[p] < T) {
+            T = tops[p];
+            tiedT = part_tied[p] != 0;
+        } else if (tops[p] == T) {
+            tiedT = tiedT || part_tied[p] != 0;
+        }
+    }
+    bool tie = d->m == d->k && d->tied;
+    for (size_t p = 0; p < src.size(); ++p) {
+        const int64_t n = counts[p];
+        for (int64_t off = 0; off < n;) {
+            const int64_t c = std::min<int64_t>(n - off, 8 * (int64_t)d->k + 4096);
+            hipError_t e;
+            if ((e = ensure_cand(d, c, st))) return fail_hip(e, "distinct merge");
+            if ((e = hipMemcpyAsync(d->cand_h, src[p].first + off, (size_t)c * 8, hipMemcpyDeviceToDevice, st)))
+                return fail_hip(e, "distinct merge");
+            if ((e = hipMemcpyAsync(d->cand_k, src[p].second + (size_t)off * d->words, (size_t)c * d->words * 8,
+                                    hipMemcpyDeviceToDevice, st)))
+                return fail_hip(e, "distinct merge");
+            const int64_t old_top = d->top;
+            const bool was_full = d->m == d->k;
+            if ((e = merge_cands(d, c, st))) return fail_hip(e, "distinct merge");
+            tie = d->m == d->k && (d->tied || (tie && was_full && d->top == old_top));
+            off += c;
+        }
+    }
+    d->tied = d->m == d->k && (tie || (tiedT && d->top == T));
+    if (d->ordered) {
+        d->rep_stale = true;
+        d->exact = true;
+        d->merged = true;
+    }
+    return RSV_OK;
+}
+
+}  // namespace
+
+// ---- entry points (rsv_internal.h) -------------------------------------------------------------
+
+WideDistinct* wide_create(int32_t k, int key_width, int src, int64_t r0, int64_t r1, bool ordered, int* status) {
+    WideDistinct* d = new WideDistinct();
+    d->k = k;
+    d->words = key_width / 8;
+    d->src = src;
+    d->r0 = r0;
+    d->r1 = r1;
+    d->ordered = ordered;
+    d->log_limit = std::min<int64_t>(std::max<int64_t>(32 * (int64_t)k + 65536, (int64_t)1 << 22), (int64_t)1 << 27);
+    if (const char* v = std::getenv("RSV_ORDERED_LOG_LIMIT"))  // test hook: force eager replays
+        d->log_limit = std::max<int64_t>(1, std::atoll(v));
+    if (ordered) d->rep.reset(k, d->words);
+    hipError_t e = walloc((void**)&d->ctl, 8 * 8);
+    if (e == hipSuccess) e = pool_host_alloc((void**)&d->hctl, 8 * 8, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        *status = fail_hip(e, "distinct_create (wide keys)");
+        wide_destroy(d);
+        return nullptr;
+    }
+    *status = RSV_OK;
+    return d;
+}
+
+void wide_destroy(WideDistinct* d) {
+    if (!d) return;
+    void* ps[] = {d->set_h, d->set_k, d->set_h2, d->set_k2, d->cand_h, d->cand_i, d->cand_k, d->eh0, d->eh1,
+                  d->ev0, d->ev1, d->flags, d->pos, d->temp, d->ctl, d->log_h, d->log_g, d->log_k};
+    for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
+    pool_host_free(d->hctl);
+    delete d;
+}
+
+void wide_set_timer(WideDistinct* d, KernelTimer* t) { d->timer = t; }
+int64_t wide_size(const WideDistinct* d) { return d->m; }
+const void* wide_keys_dev(const WideDistinct* d) { return d->set_k; }
+bool wide_is_ordered(const WideDistinct* d) { return d->ordered; }
+
+int wide_sample_device(WideDistinct* d, const void* keys, const int64_t* hashes, int64_t n, hipStream_t st) {
+    if (n <= 0) return RSV_OK;
+    if (d->merged) {  // sampling on after a merge: the pre-merge candidates are history
+        d->merged = false;
+        d->log_n = 0;
+        d->arch_h.clear();
+        d->arch_k.clear();
+        d->arch_ok = false;
+    }
+    for (int64_t off = 0; off < n;) {
+        // filling: enough for the set plus slack; full: ~4 seen lengths (~4k candidates a chunk)
+        const int64_t L = d->m < d->k ? std::min<int64_t>(n - off, 4 * ((int64_t)d->k - d->m) + 4096)
+                                      : std::min<int64_t>(n - off, std::max<int64_t>(4 * d->seen, 1 << 16));
+        if (hipError_t e = sample_chunk(d, keys, hashes, off, L, d->seen - off, st)) return fail_hip(e, "distinct sample");
+        off += L;
+        d->seen += L;
+    }
+    return RSV_OK;
+}
+
+int wide_finalize(WideDistinct* d, hipStream_t st) {
+    if (!d->ordered || d->exact) return RSV_OK;
+    if (hipError_t e = replay_log(d, st)) return fail_hip(e, "distinct (ordered) replay");
+    return RSV_OK;
+}
+
+int wide_publish(WideDistinct* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st) {
+    RSV_HIP_TRY(launch_publish(d->set_k, d->m * d->words * 8, dst_host_dev, flag_dev, gen, st));
+    return RSV_OK;
+}
+
+int wide_export(WideDistinct* d, void* keys_dev, int64_t* hash_dev, hipStream_t st) {
+    if (d->m == 0) return RSV_OK;
+    if (keys_dev)
+        RSV_HIP_TRY(hipMemcpyAsync(keys_dev, d->set_k, (size_t)d->m * d->words * 8, hipMemcpyDeviceToDevice, st));
+    if (hash_dev) RSV_HIP_TRY(hipMemcpyAsync(hash_dev, d->set_h, (size_t)d->m * 8, hipMemcpyDeviceToDevice, st));
+    return RSV_OK;
+}
+
+void wide_info(const WideDistinct* d, int32_t* ordered, int32_t* tied, int32_t* retained, int64_t* size,
+               int64_t* max_hash, int64_t* log_entries) {
+    *ordered = d->ordered;
+    *tied = d->m == d->k && d->tied;
+    *retained = d->ordered && d->retain && d->arch_ok;
+    *size = d->m;
+    *max_hash = d->m ? d->top : INT64_MIN;
+    *log_entries = d->ordered ? (int64_t)d->arch_h.size() + d->log_n : 0;
+}
+
+int wide_merge_parts(WideDistinct* d, const void* keys_dev, const int64_t* hash_dev, const int64_t* part_n,
+                     int32_t parts, int64_t part_len, hipStream_t st) {
+    if (int rc = wide_finalize(d, st)) return rc;
+    std::vector<std::pair<const int64_t*, const uint64_t*>> src;
+    std::vector<int64_t> counts, tops;
+    std::vector<int32_t> ties;
+    for (int32_t p = 0; p < parts; ++p) {
+        const int64_t n = std::max<int64_t>(0, std::min(part_n[p], part_len));
+        src.emplace_back(hash_dev + (size_t)p * part_len, (const uint64_t*)keys_dev + (size_t)p * part_len * d->words);
+        counts.push_back(n);
+        tops.push_back(INT64_MAX);  // no per-part tie information in this form
+        ties.push_back(0);
+    }
+    return merge_external(d, src, counts, tops, ties, st);
+}
+
+int wide_export_row(WideDistinct* d, int64_t* row, int64_t count, hipStream_t st) {
+    if (int rc = wide_finalize(d, st)) return rc;
+    const int64_t k = d->k;
+    const int64_t tied = d->m == k && d->tied, mx = d->m ? d->top : INT64_MIN;
+    const int64_t ret = d->ordered && d->retain && d->arch_ok;
+    hipLaunchKernelGGL(wide_export_row, dim3(wgrid(k * (d->words + 1), 4096)), dim3(kWBlock), 0, st, d->set_h,
+                       d->set_k, d->m, k, d->words, row, count, tied, mx, ret, (int64_t)d->ordered);
+    RSV_HIP_TRY(hipGetLastError());
+    return RSV_OK;
+}
+
+int wide_merge_rows(WideDistinct* d, const int64_t* rows, int32_t parts, int64_t stride, hipStream_t st) {
+    if (int rc = wide_finalize(d, st)) return rc;
+    const int64_t k = d->k, kw = k * d->words;
+    std::vector<int64_t> meta((size_t)parts * 6);
+    for (int32_t p = 0; p < parts; ++p)
+        RSV_HIP_TRY(hipMemcpyAsync(meta.data() + (size_t)p * 6, rows + (size_t)p * stride + kw + k, 6 * 8,
+                                   hipMemcpyDeviceToHost, st));
+    RSV_HIP_TRY(hipStreamSynchronize(st));
+    std::vector<std::pair<const int64_t*, const uint64_t*>> src;
+    std::vector<int64_t> counts, tops;
+    std::vector<int32_t> ties;
+    for (int32_t p = 0; p < parts; ++p) {
+        const int64_t* mt = meta.data() + (size_t)p * 6;
+        const int64_t* r = rows + (size_t)p * stride;
+        src.emplace_back(r + kw, (const uint64_t*)r);
+        counts.push_back(std::min(std::max<int64_t>(mt[0], 0), k));
+        tops.push_back(mt[3]);
+        ties.push_back(mt[2] != 0);
+    }
+    return merge_external(d, src, counts, tops, ties, st);
+}
+
+void wide_retain_log(WideDistinct* d, bool on) {
+    if (on && !d->retain && d->seen > 0) d->arch_ok = false;  // earlier candidates are gone
+    d->retain = on;
+    if (!on) {
+        d->arch_h.clear();
+        d->arch_k.clear();
+    }
+}
+
+int wide_log_export(WideDistinct* d, int64_t bound, int64_t* out_h, void* out_k, int64_t cap, int64_t* out_n,
+                    hipStream_t st) {
+    if (!d->ordered || !d->retain || !d->arch_ok) {
+        set_error(!d->ordered  ? "rsv_export_log needs an RSV_DISTINCT_ORDERED sampler"
+                  : !d->retain ? "rsv_export_log: the candidate log was not retained (rsv_retain_log before sampling)"
+                               : "rsv_export_log: the candidate log was not retained (archive limit, or sampled "
+                                 "after a merge)");
+        return RSV_E_UNSUPPORTED;
+    }
+    std::vector<int64_t> lh;
+    std::vector<uint64_t> lk;
+    if (hipError_t e = log_to_host(d, lh, lk, st)) return fail_hip(e, "rsv_export_log");
+    const bool all = bound == INT64_MAX;
+    const int64_t W = d->words;
+    uint64_t* ok = (uint64_t*)out_k;
+    int64_t cnt = 0;
+    auto emit = [&](int64_t h, const uint64_t* r) {
+        if (all || h < bound) {
+            if (cnt < cap) {
+                out_h[cnt] = h;
+                std::memcpy(ok + cnt * W, r, (size_t)W * 8);
+            }
+            ++cnt;
+        }
+    };
+    for (size_t i = 0; i < d->arch_h.size(); ++i) emit(d->arch_h[i], d->arch_k.data() + i * W);
+    for (size_t i = 0; i < lh.size(); ++i) emit(lh[i], lk.data() + i * W);
+    *out_n = cnt;
+    if (cnt > cap && cap > 0) {
+        set_error("rsv_export_log: cap is smaller than the number of candidates (*out_n)");
+        return RSV_E_ILLEGAL_ARGUMENT;
+    }
+    return RSV_OK;
+}
+
+int wide_log_merge(WideDistinct* d, const int64_t* h, const void* keys, int64_t n, int64_t seen, hipStream_t st) {
+    if (!d->ordered) {
+        set_error("rsv_merge_log needs an RSV_DISTINCT_ORDERED sampler");
+        return RSV_E_UNSUPPORTED;
+    }
+    d->rep.reset(d->k, d->words);
+    d->rep_stale = false;
+    const uint64_t* kk = (const uint64_t*)keys;
+    for (int64_t t = 0; t < n; ++t) d->rep.sample(h[t], kk + (size_t)t * d->words);
+    d->log_n = 0;
+    d->arch_h.clear();
+    d->arch_k.clear();
+    if (hipError_t e = upload_replica(d, st)) return fail_hip(e, "rsv_merge_log");
+    d->tied = false;
+    d->exact = true;
+    d->merged = true;
+    d->seen = std::max(d->seen, seen);
+    return RSV_OK;
+}
+
+}  // namespace rsv

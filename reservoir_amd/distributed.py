@@ -88,7 +88,8 @@ def combine(sampler, group=None, device=None, total_count: int | None = None, ma
     _mark(marks)
     rows = flat.view(world, width)
     k = sampler.max_sample_size
-    total = int(rows[:, 2 * k + 1].sum().item()) if total_count is None else int(total_count)
+    mo = _meta_off(sampler)
+    total = int(rows[:, mo + 1].sum().item()) if total_count is None else int(total_count)
     sampler.merge_packed(rows, total)
     _mark(marks)
     if not sampler.is_ordered:
@@ -96,19 +97,20 @@ def combine(sampler, group=None, device=None, total_count: int | None = None, ma
     meta = _ordered_replay_meta(sampler, rows)
     if meta is None:
         return False
-    bounds = replay_bounds(rows, meta, k)
+    w = _key_words(sampler)
+    bounds = replay_bounds(rows, meta, k, w)
     h, keys = sampler.export_log(bounds[rank])
-    part = torch.from_numpy(np.concatenate([h, keys.astype(np.int64)])).to(device)
+    part = torch.from_numpy(np.concatenate([h, _as_words(keys)])).to(device)
     sizes = torch.empty(world, dtype=torch.int64, device=device)
     dist.all_gather_into_tensor(sizes, torch.tensor([h.size], dtype=torch.int64).to(device), group=group)
     sz = sizes.cpu().numpy()
     parts = []
     for r in range(world):  # exact sizes, one broadcast per rank (no padding to the largest log)
-        buf = part if r == rank else torch.empty(2 * int(sz[r]), dtype=torch.int64, device=device)
+        buf = part if r == rank else torch.empty((1 + w) * int(sz[r]), dtype=torch.int64, device=device)
         if sz[r]:
             dist.broadcast(buf, src=dist.get_global_rank(group, r) if group is not None else r, group=group)
         lg = buf.cpu().numpy()
-        parts.append((lg[: sz[r]], lg[sz[r]:]))
+        parts.append((lg[: sz[r]], lg[sz[r]:]))  # hashes, then the keys' int64 words
     _merge_logs(sampler, parts)
     return True
 
@@ -128,24 +130,42 @@ def merge_local(target, shards, total_count: int | None = None) -> bool:
         target.merge_packed(rows, total)
         return False
     k = target.max_sample_size
-    total = int(rows[:, 2 * k + 1].sum().item()) if total_count is None else int(total_count)
+    mo = _meta_off(target)
+    total = int(rows[:, mo + 1].sum().item()) if total_count is None else int(total_count)
     target.merge_packed(rows, total)
     if not target.is_ordered:
         return False
     meta = _ordered_replay_meta(target, rows)
     if meta is None:
         return False
-    bounds = replay_bounds(rows, meta, k)
+    bounds = replay_bounds(rows, meta, k, _key_words(target))
     parts = []
     for r, s in enumerate(shards):
         h, keys = s.export_log(bounds[r])
-        parts.append((h, keys.astype(np.int64)))
+        parts.append((h, _as_words(keys)))
     _merge_logs(target, parts)
     return True
 
 
-# distinct row (rsv_export_packed): [keys(k) | hashes(k) | n, count, tied, max_hash, log_retained, ordered]
+# distinct row (rsv_export_packed): [keys(k) | hashes(k) | n, count, tied, max_hash, log_retained, ordered];
+# a key is one int64 word (Int / Long, widened) or key_width / 8 words (fixed-width byte keys)
 _META = 6
+
+
+def _key_words(sampler) -> int:
+    return int(getattr(sampler, "key_words", 1))
+
+
+def _meta_off(sampler) -> int:
+    return sampler.max_sample_size * (_key_words(sampler) + 1)
+
+
+def _as_words(keys) -> np.ndarray:
+    """Host keys as int64 words: Int / Long keys widened, byte keys (dtype VN) N / 8 words each."""
+    keys = np.ascontiguousarray(keys)
+    if keys.dtype.kind == "V":
+        return keys.view(np.int64).reshape(-1)
+    return keys.astype(np.int64)
 
 
 def _ordered_replay_meta(sampler, rows):
@@ -156,8 +176,7 @@ def _ordered_replay_meta(sampler, rows):
     info = sampler.distinct_info()  # settles the merge: one wait for its published words
     if not info["tied"]:
         return None
-    k = sampler.max_sample_size
-    meta = rows[:, 2 * k:].cpu().numpy()
+    meta = rows[:, _meta_off(sampler):].cpu().numpy()
     if not all(int(m[5]) for m in meta):
         return None  # some rank ran in set mode: the (hash, key) set is the defined result
     if not all(int(m[4]) for m in meta):
@@ -168,34 +187,35 @@ def _ordered_replay_meta(sampler, rows):
     return meta
 
 
-def replay_bounds(rows, meta, k: int) -> list:
+def replay_bounds(rows, meta, k: int, key_words: int = 1) -> list:
     """Per rank r, the bound its exported candidates must stay under: the k-th smallest hash of the
     distinct elements in the pieces before it (from the gathered bottom-k sets), else no bound.
     Inside rank r's piece the reference's heap maximum is at most that hash, and it admits only
-    elements strictly below its maximum (Sampler.scala:403)."""
+    elements strictly below its maximum (Sampler.scala:403).  Elements are distinct by (hash, key
+    words); equal keys have equal hashes."""
     world = rows.shape[0]
-    h_all = rows[:, k:2 * k].cpu().numpy()
-    k_all = rows[:, :k].cpu().numpy()
+    kw = k * key_words
+    h_all = rows[:, kw:kw + k].cpu().numpy()
+    k_all = rows[:, :kw].cpu().numpy().reshape(world, k, key_words)
     no_bound = np.iinfo(np.int64).max
     bounds = [no_bound]
-    ph = np.empty(0, dtype=np.int64)
-    pk = np.empty(0, dtype=np.int64)
+    acc = np.empty((0, key_words + 1), dtype=np.int64)  # rows [h, key words...], bottom-k so far
     for r in range(1, world):
         n = int(meta[r - 1][0])
-        uk, first = np.unique(np.concatenate([pk, k_all[r - 1, :n]]), return_index=True)
-        uh = np.concatenate([ph, h_all[r - 1, :n]])[first]
-        order = np.lexsort((uk, uh))[:k]
-        ph, pk = uh[order], uk[order]
-        bounds.append(int(ph[k - 1]) if ph.size == k else no_bound)
+        ent = np.concatenate([h_all[r - 1, :n, None], k_all[r - 1, :n]], axis=1)
+        acc = np.unique(np.concatenate([acc, ent]), axis=0)[:k]  # sorted by (h, key words)
+        bounds.append(int(acc[k - 1, 0]) if acc.shape[0] == k else no_bound)
     return bounds
 
 
 def _merge_logs(sampler, parts) -> None:
     """Exact ordered merge: every rank's exported candidates, concatenated in rank order, through a
-    fresh replica of the reference's RandomValues (rsv_merge_log)."""
+    fresh replica of the reference's RandomValues (rsv_merge_log).  ``parts``: (hashes, key words)."""
     h = np.concatenate([np.asarray(p[0], dtype=np.int64) for p in parts]) if parts else np.empty(0, np.int64)
-    keys = np.concatenate([np.asarray(p[1], dtype=np.int64) for p in parts]) if parts else np.empty(0, np.int64)
-    sampler.merge_log(h, keys.astype(sampler.key_dtype), int(sampler.count))
+    words = np.concatenate([np.asarray(p[1], dtype=np.int64) for p in parts]) if parts else np.empty(0, np.int64)
+    dt = np.dtype(sampler.key_dtype)
+    keys = np.ascontiguousarray(words).view(dt) if dt.kind == "V" else words.astype(dt)
+    sampler.merge_log(h, keys, int(sampler.count))
 
 
 def _combine_elements(sampler, world, group, device, total_count) -> None:

@@ -18,9 +18,12 @@ to the GPU in batches.  Keys already resident in HBM (a torch CUDA tensor) are s
 
 Extensions (keyword-only, defaulted so reference-style calls are unchanged):
     key_type  "long" (B = Long, 8-byte keys, default), "int" (B = Int, 4-byte keys), or "bytesN"
-              (element samplers: fixed-width byte keys, N a multiple of 8 in 16..256, e.g.
-              "bytes16" for UUIDs; numpy arrays of shape (n, N) uint8 or dtype "VN", torch
-              CUDA uint8 tensors of shape (n, N))
+              (fixed-width byte keys with value equality, N a multiple of 8 in 16..256, e.g.
+              "bytes16" for java.util.UUID laid out [mostSigBits | leastSigBits] as little-endian
+              Longs; numpy arrays of shape (n, N) uint8 or dtype "VN", torch CUDA uint8 tensors of
+              shape (n, N)).  Sampler.distinct over byte keys dedups by the bytes and takes a
+              callable ``hash`` (the JVM's ``hash: B => Long``) -- or, for "bytes16", the default
+              java.util.UUID.hashCode
     engine    "philox_r" (default: data-parallel Algorithm R) or "java_l" (the reference's own
               Algorithm L over java.util.Random(seed): bit-identical results to the reference)
     seed      RNG seed (default: fresh entropy, like ``new Random()`` at Sampler.scala:199)
@@ -251,8 +254,15 @@ class GpuSampler:
         N.check(self._L.rsv_sample(self._h, C.c_char_p(kbuf),
                                    C.byref(hv) if hv is not None else None))
 
-    def sample_all(self, elements: Iterable) -> None:
-        """Sampler.sampleAll (Sampler.scala:49-50): same result as sample() on each element."""
+    def sample_all(self, elements: Iterable, hashes=None) -> None:
+        """Sampler.sampleAll (Sampler.scala:49-50): same result as sample() on each element.
+
+        ``hashes``: a distinct sampler with a callable ``hash`` over device-resident keys takes the
+        hashes precomputed as an int64 CUDA tensor (one per key, e.g. computed by torch on the
+        device) instead of calling ``hash`` per element on the host."""
+        if hashes is not None:
+            self._sample_device_hashed(elements, hashes)
+            return
         if _is_torch_cuda(elements) and self._map is identity and not self._precomputed:
             # device fast path; checkOpen() first, as the reference does before any other work
             # (Sampler.scala:186, :417-419): a single-use sampler closed by result() keeps its handle
@@ -262,7 +272,7 @@ class GpuSampler:
             t = elements if elements.is_contiguous() else elements.contiguous()
             cur = _current_raw_stream(torch, t)
             if cur != self._stream:
-                torch.cuda.current_stream(t.device).synchronize()  # produced on torch's stream
+                self._wait_torch(t)  # produced on torch's stream
                 # and torch must not hand the block to another tensor while this handle's stream
                 # still reads it (the caller may drop `elements` as soon as we return)
                 t.record_stream(torch.cuda.ExternalStream(self._stream, device=t.device))
@@ -299,6 +309,38 @@ class GpuSampler:
 
     sampleAll = sample_all
 
+    def _sample_device_hashed(self, keys, hashes) -> None:
+        """Device keys + their precomputed hashes (RSV_HASH_PRECOMPUTED) in one rsv_sample_batch."""
+        if self._h is None or not self._L.rsv_is_open(self._h):
+            raise IllegalStateException("use of sampler after calling `result()`")
+        if not self._precomputed:
+            raise IllegalArgumentException("hashes= needs a distinct sampler with a callable hash")
+        if not (_is_torch_cuda(keys) and _is_torch_cuda(hashes)) or self._map is not identity:
+            raise IllegalArgumentException("hashes= takes device tensors of keys (identity map) and int64 hashes")
+        torch = _torch()
+        t = keys if keys.is_contiguous() else keys.contiguous()
+        hv = hashes if hashes.is_contiguous() else hashes.contiguous()
+        if hv.dtype != torch.int64:
+            raise IllegalArgumentException("hashes must be int64")
+        if self._width <= 8:
+            if t.element_size() != self._width:
+                raise IllegalArgumentException("device tensor dtype does not match key_type")
+            n_keys = t.numel()
+        else:
+            if t.dim() < 2 or t.shape[-1] * t.element_size() != self._width:
+                raise IllegalArgumentException("device tensor rows must hold key_width bytes")
+            n_keys = t.numel() * t.element_size() // self._width
+        if hv.numel() != n_keys:
+            raise IllegalArgumentException("one hash per key")
+        cur = _current_raw_stream(torch, t)
+        if cur != self._stream:
+            self._wait_torch(t)
+            ext = torch.cuda.ExternalStream(self._stream, device=t.device)
+            t.record_stream(ext)
+            hv.record_stream(ext)
+        N.check(self._L.rsv_sample_batch(self._h, C.c_void_p(t.data_ptr()), n_keys, N.MEM_DEVICE,
+                                         C.c_void_p(hv.data_ptr())))
+
     def _sample_indexed(self, seq) -> None:
         """sampleAll over an IndexedSeq (Sampler.scala:289-312 -> sampleIndexed :261-273): the engine
         samples the len(seq) indices, and only the elements that now hold a slot are mapped."""
@@ -309,11 +351,17 @@ class GpuSampler:
             return
         sel = np.flatnonzero(offs >= 0)
         keys = np.zeros(self._k, dtype=self._dtype)
-        if isinstance(seq, np.ndarray) and self._map is identity:
-            keys[sel] = seq[offs[sel]]
-        else:
-            for j in sel.tolist():
-                keys[j] = self._map(seq[int(offs[j])])
+        try:
+            if isinstance(seq, np.ndarray) and self._map is identity:
+                keys[sel] = seq[offs[sel]]
+            else:
+                for j in sel.tolist():
+                    keys[j] = self._map(seq[int(offs[j])])
+        except BaseException:
+            # `map` threw (or a key does not fit the key type): drop the batch, keep the sampler
+            # usable, and propagate the exception as the reference's sampleIndexed does
+            N.check(self._L.rsv_abort_indexed(self._h))
+            raise
         N.check(self._L.rsv_fill_slots(self._h, keys.ctypes.data_as(C.c_void_p)))
 
     def _wide_keys(self, elements) -> np.ndarray:
@@ -364,12 +412,22 @@ class GpuSampler:
 
     def _order_after_torch(self, t) -> None:
         """Device tensors handed to the engine were written (or allocated and filled) by torch on
-        its current stream; unless this handle runs on that stream, wait for it first -- the
-        engine's own stream is not ordered after torch's."""
+        its current stream; unless this handle runs on that stream, order the handle's stream after
+        it first -- the engine's own stream is not ordered after torch's."""
         if _is_torch_cuda(t):
             torch = _torch()
             if _current_raw_stream(torch, t) != self._stream:
-                torch.cuda.current_stream(t.device).synchronize()
+                self._wait_torch(t)
+
+    def _wait_torch(self, t) -> None:
+        """An event recorded on torch's current stream, waited for by this handle's stream
+        (hipStreamWaitEvent): stream-ordered, no host wait.  The event is kept until the next
+        hand-over."""
+        torch = _torch()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(t.device))
+        torch.cuda.ExternalStream(self._stream, device=t.device).wait_event(ev)
+        self._torch_ev = ev
 
     # -- multi-GPU helpers (reservoir_amd.distributed) ------------------------------------------
     @property
@@ -410,11 +468,16 @@ class GpuSampler:
         return idx, keys, hashes, n.value
 
     @property
+    def key_words(self) -> int:
+        """int64 words one key takes in a packed row (1 for Int/Long keys, key_width / 8 for byte keys)."""
+        return self._width // 8 if self._width > 8 else 1
+
+    @property
     def packed_width(self) -> int:
         """Length of this sampler's rsv_export_packed row (int64 words)."""
         if self.is_distinct:
-            return 2 * self._k + 6
-        return self._k * (1 + (self._width // 8 if self._width > 8 else 1))
+            return self._k * (self.key_words + 1) + 6
+        return self._k * (1 + self.key_words)
 
     def export_packed(self, row) -> None:
         """Write the packed row (include/reservoir_hip.h rsv_export_packed) into the int64 device

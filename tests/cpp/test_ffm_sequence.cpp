@@ -103,12 +103,17 @@ struct FfmMirror {
         check(rsv_sample_indexed(handle, n, offsets.data()));
         std::vector<uint8_t> ks((size_t)k * width);
         int64_t mapped = 0;
-        for (int j = 0; j < k; ++j) {
-            const int64_t o = offsets[(size_t)j];
-            if (o >= 0) {
-                key_at(o, ks.data() + (size_t)j * width);
-                ++mapped;
+        try {
+            for (int j = 0; j < k; ++j) {
+                const int64_t o = offsets[(size_t)j];
+                if (o >= 0) {
+                    key_at(o, ks.data() + (size_t)j * width);
+                    ++mapped;
+                }
             }
+        } catch (...) {  // `map` threw: drop the batch, keep the sampler usable, propagate
+            check(rsv_abort_indexed(handle));
+            throw;
         }
         check(rsv_fill_slots(handle, ks.data()));
         return mapped;

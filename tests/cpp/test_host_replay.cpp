@@ -4,7 +4,9 @@
 // mark_first defines them: the key neither occurs earlier in the segment nor is a member when the
 // segment starts).  Both replicas consume the same segments; after every segment their heaps
 // (hash and element arrays, size, maxHash) must be identical.  Set-based calls after a heap-only
-// run (rebuild of the element set) are interleaved.  Exit 0 and "ok <cases>" on success.
+// run (rebuild of the element set) are interleaved.  A third replica, HostValuesWide (the byte-key
+// form of rsv_wide.hip) fed each key as the two-word row [key, ~key], must hold the same heap entry
+// for entry (hash, and the row's first word = the key).  Exit 0 and "ok <cases>" on success.
 //   g++ -std=c++17 -O2 -I reservoir_amd/csrc tests/cpp/test_host_replay.cpp -o test_host_replay
 #include <cstdio>
 #include <cstring>
@@ -27,6 +29,15 @@ static bool same(const rsv::HostValues& a, const rsv::HostValues& b) {
     return true;
 }
 
+static bool same_wide(const rsv::HostValues& a, const rsv::HostValuesWide& c) {
+    if (a.n != c.n || a.max_hash != c.max_hash) return false;
+    for (int64_t i = 1; i <= a.n; ++i) {
+        const uint64_t* r = c.row(c.hs[(size_t)i]);
+        if (a.hh[(size_t)i] != c.hh[(size_t)i] || (uint64_t)a.he[(size_t)i] != r[0] || r[1] != ~r[0]) return false;
+    }
+    return true;
+}
+
 int main() {
     int cases = 0;
     for (const int64_t k : {1, 2, 5, 64, 1000, 4096}) {
@@ -35,8 +46,10 @@ int main() {
                 std::mt19937_64 rng(seed * 7919 + (uint64_t)k * 31 + (uint64_t)buckets);
                 const int64_t universe = std::max<int64_t>(4, 6 * k);  // keys repeat across segments
                 rsv::HostValues a, b;
+                rsv::HostValuesWide cw;
                 a.reset(k);
                 b.reset(k);
+                cw.reset(k, 2);
                 for (int seg = 0; seg < 12; ++seg) {
                     const int64_t c = (int64_t)(rng() % (uint64_t)(3 * k + 50));
                     std::vector<int64_t> ek((size_t)c), eh((size_t)c);
@@ -46,6 +59,10 @@ int main() {
                                                               : (int64_t)(rng() % (uint64_t)universe) - universe / 2;
                         ek[(size_t)t] = key;
                         eh[(size_t)t] = (int64_t)mix64((uint64_t)key % (uint64_t)buckets + 11) ;
+                    }
+                    for (int64_t t = 0; t < c; ++t) {
+                        const uint64_t row[2] = {(uint64_t)ek[(size_t)t], ~(uint64_t)ek[(size_t)t]};
+                        cw.sample(eh[(size_t)t], row);
                     }
                     if (seg % 4 == 3) {  // set-based single calls on both (b rebuilds its set)
                         for (int64_t t = 0; t < c; ++t) {
@@ -61,7 +78,7 @@ int main() {
                         b.sample_run_unique(c, first.data(), [&](int64_t t) { return ek[(size_t)t]; },
                                             [&](int64_t t) { return eh[(size_t)t]; });
                     }
-                    if (!same(a, b)) {
+                    if (!same(a, b) || !same_wide(a, cw)) {
                         std::printf("MISMATCH k=%lld buckets=%lld seed=%llu segment=%d\n", (long long)k,
                                     (long long)buckets, (unsigned long long)seed, seg);
                         return 1;

@@ -128,3 +128,39 @@ def test_keys_owed_state(cuda):
     assert np.array_equal(r, keys)
     d = Sampler.distinct(8)()
     assert L.rsv_sample_indexed(d.handle, 5, offs.ctypes.data_as(C.c_void_p)) == N.E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("engine", ["philox_r", "java_l"])
+def test_throwing_map_aborts_the_batch(cuda, oracle, engine):
+    """A `map` that throws inside sampleAll(IndexedSeq): the exception propagates, the owed batch is
+    dropped (rsv_abort_indexed), and the sampler keeps working -- equal to one that never saw that
+    batch (the handle used to stay stuck in IllegalStateException)."""
+    from reservoir_amd import Sampler
+
+    k = 64
+
+    class Boom(Exception):
+        pass
+
+    def bad(x):
+        if x >= 500:
+            raise Boom(x)
+        return x
+
+    for fresh in (True, False):
+        s = Sampler(k, engine=engine, seed=3, stream_id=4)(bad)
+        ref = Sampler(k, engine=engine, seed=3, stream_id=4)(bad)
+        if not fresh:
+            s.sample_all(range(200))
+            ref.sample_all(range(200))
+        with pytest.raises(Boom):
+            s.sample_all(range(100_000))  # evictions land far past 500: map throws
+        assert s.is_open and s.count == (0 if fresh else 200)
+        s.sample_all(range(300))
+        ref.sample_all(range(300))
+        assert np.array_equal(s.result(), ref.result())
+    from reservoir_amd import _native as N
+
+    L = N.load()
+    s = Sampler(8)()
+    assert L.rsv_abort_indexed(s.handle) == N.E_ILLEGAL_STATE

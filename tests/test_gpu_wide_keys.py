@@ -77,8 +77,6 @@ def test_wide_keys_rejected_where_unsupported(cuda):
     from reservoir_amd import IllegalArgumentException, Sampler
 
     with pytest.raises(IllegalArgumentException):
-        Sampler.distinct(10, key_type="bytes16")()  # distinct hashes Int/Long keys only
-    with pytest.raises(IllegalArgumentException):
         Sampler(10, key_type="bytes12")()
     s = Sampler(4, key_type="bytes16")()
     with pytest.raises(IllegalArgumentException):

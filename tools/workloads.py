@@ -13,6 +13,8 @@ torch int64 arithmetic wraps like Java Long; logical right shifts are emulated w
                                 permutation): one rank's piece of C4's 8-way split
   hash_twins(keys, bits)        keys whose java.lang.Long.hashCode takes only 2^bits values (many
                                 distinct keys per hash bucket: the ordered distinct path's replay)
+  uuid_rows(vals, twin_bits)    16-byte UUID keys, one per distinct value (optionally hash twins)
+  uuid_hash(rows)               java.util.UUID.hashCode of such rows
 """
 from __future__ import annotations
 
@@ -140,3 +142,20 @@ def hash_twins(keys: torch.Tensor, bits: int = 24) -> torch.Tensor:
     hi = _srl(keys, 32)
     lo = (hi ^ (keys & ((1 << bits) - 1))) & 0xFFFFFFFF
     return (hi << 32) | lo
+
+
+def uuid_rows(vals: torch.Tensor, twin_bits: int | None = None) -> torch.Tensor:
+    """16-byte keys (java.util.UUID laid out [mostSigBits | leastSigBits], little-endian Longs) as a
+    (n, 16) uint8 tensor, one distinct row per distinct value v: [v, splitmix64(v ^ 0xAA)].  With
+    twin_bits, [v, v ^ (v & (2^twin_bits - 1))] instead: UUID.hashCode = v & (2^twin_bits - 1), so
+    ~n / 2^twin_bits distinct keys share each hash value (the ordered distinct path's replay)."""
+    lo = smix(vals ^ 0xAA) if twin_bits is None else vals & ~((1 << twin_bits) - 1)
+    return torch.stack([vals, lo], dim=1).contiguous().view(torch.uint8)
+
+
+def uuid_hash(rows: torch.Tensor) -> torch.Tensor:
+    """java.util.UUID.hashCode (.toLong) of (n, 16) uint8 rows, on the device."""
+    w = rows.contiguous().view(torch.int64).view(-1, 2)
+    hilo = w[:, 0] ^ w[:, 1]
+    x = (_srl(hilo, 32) ^ hilo) & 0xFFFFFFFF
+    return (x ^ 0x80000000) - 0x80000000
