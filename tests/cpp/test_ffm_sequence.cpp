@@ -162,7 +162,7 @@ static int64_t make_key(const Case& c, int64_t i, void* dst) {
     if (!c.keys.empty()) {
         std::memcpy(dst, c.keys.data() + i * c.kw, (size_t)c.kw);
         int64_t v = 0;
-        if (c.kw == 8) std::memcpy(&v, dst, 8);
+        if (c.kw >= 8) std::memcpy(&v, dst, 8);  // byte keys: the hash reads the first word
         else {
             int32_t w;
             std::memcpy(&w, dst, 4);
@@ -171,6 +171,12 @@ static int64_t make_key(const Case& c, int64_t i, void* dst) {
         return (int64_t)((uint64_t)v * 31u + 7u);
     }
     const int64_t v = (int64_t)splitmix64(c.base + (uint64_t)i);
+    if (c.kw > 8) {  // byte keys (UUID): [v, ~v], then zero words
+        std::memset(dst, 0, (size_t)c.kw);
+        const uint64_t w[2] = {(uint64_t)v, ~(uint64_t)v};
+        std::memcpy(dst, w, 16);
+        return (int64_t)((uint64_t)v * 31u + 7u);
+    }
     if (c.kw == 8) {
         std::memcpy(dst, &v, 8);
         return (int64_t)((uint64_t)v * 31u + 7u);
@@ -189,7 +195,13 @@ static bool same(const Case& c, std::vector<uint8_t> got, int64_t n) {
     if (c.kind == RSV_KIND_DISTINCT) {  // HashSet order in the reference: compare as sets
         auto sort_keys = [&](std::vector<uint8_t>& b) {
             if (c.kw == 8) std::sort((int64_t*)b.data(), (int64_t*)b.data() + n);
-            else std::sort((int32_t*)b.data(), (int32_t*)b.data() + n);
+            else if (c.kw == 4) std::sort((int32_t*)b.data(), (int32_t*)b.data() + n);
+            else {  // byte keys: sort the rows as strings
+                std::vector<std::string> rows((size_t)n);
+                for (int64_t i = 0; i < n; ++i) rows[(size_t)i].assign((const char*)b.data() + i * c.kw, (size_t)c.kw);
+                std::sort(rows.begin(), rows.end());
+                for (int64_t i = 0; i < n; ++i) std::memcpy(b.data() + i * c.kw, rows[(size_t)i].data(), (size_t)c.kw);
+            }
         };
         sort_keys(got);
         sort_keys(want);
@@ -214,7 +226,7 @@ static rsv_config config_of(const Case& c) {
 
 static void run_ffm(const Case& c) {
     FfmMirror s(config_of(c));
-    uint8_t key[8];
+    uint8_t key[256];
     for (int64_t i = 0; i < c.n; ++i) {
         const int64_t h = make_key(c, i, key);
         s.sample(key, h);
@@ -264,7 +276,7 @@ static void run_jni(const Case& c) {
         st = rsv_jvm_sample_array(&s, buf.data(), s.precomputed ? hb.data() : nullptr, B);
         EXPECT(st == RSV_OK, c.name.c_str());
     }
-    uint8_t key[8];
+    uint8_t key[256];
     for (; i < c.n; ++i) {
         const int64_t h = make_key(c, i, key);
         st = rsv_jvm_sample(&s, key, h);
@@ -302,7 +314,7 @@ static void run_abi(const Case& c) {  // per-element rsv_sample: the engine stag
     const rsv_config cfg = config_of(c);
     rsv_sampler* h = nullptr;
     check(rsv_create(&cfg, &h));
-    uint8_t key[8];
+    uint8_t key[256];
     for (int64_t i = 0; i < c.n; ++i) {
         int64_t hv = make_key(c, i, key);
         rsv_status st = rsv_sample(h, key, &hv);
@@ -324,7 +336,7 @@ static void run_abi(const Case& c) {  // per-element rsv_sample: the engine stag
 // sequence is virtual (key i = make_key(c, i)): no key buffer exists for it.
 static void run_indexed(const Case& c, bool ffm) {
     const int64_t pre = std::min<int64_t>(c.n, 5);
-    uint8_t key[8];
+    uint8_t key[256];
     int64_t mapped = 0;
     std::vector<uint8_t> out;
     int64_t n = 0;

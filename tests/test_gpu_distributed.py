@@ -37,6 +37,17 @@ def _colliding_vals(seed):
     return np.concatenate([v, v[rng.integers(0, v.size, 100_000)]])
 
 
+def _wide_stream():
+    """24-byte keys (ids with repeats) and a colliding precomputed hash (97 values): the ordered
+    combine's boundary bucket ties"""
+    rng = np.random.default_rng(17)
+    ids = np.concatenate([np.arange(120_000), rng.integers(0, 120_000, 40_000)])
+    rng.shuffle(ids)
+    words = np.stack([ids, ids * 7 + 1, ~ids], axis=1).astype(np.int64)
+    rows = np.ascontiguousarray(words).view(np.uint8).reshape(-1, 24)
+    return rows, {"set": (ids * 1_000_003 + 17).astype(np.int64), "ordered": (ids % 97 - 48).astype(np.int64)}
+
+
 def _worker(rank, world, port, q):
     sys.path.insert(0, ROOT)
     import torch
@@ -92,6 +103,18 @@ def _worker(rank, world, port, q):
             o.sample_all(torch.from_numpy(cv[clo:chi]).to(dev))
             replayed = D.combine(o, device=dev)
             out[f"ordered{seed}"] = (o.result().tolist(), o.count, bool(replayed))
+        # fixed-width byte keys (24 B): set mode under a 64-bit hash, ordered mode under a colliding
+        # one (the exact replay's broadcasts carry the key words)
+        rows, hs = _wide_stream()
+        wlo, whi = D.shard_range(rows.shape[0], rank, world)
+        rd = torch.from_numpy(rows[wlo:whi]).to(dev)
+        for order, hv in hs.items():
+            w = Sampler.distinct(700, key_type="bytes24", seed=3, order=order,
+                                 retain_log=order == "ordered")(hash=lambda b: 0)
+            w.sample_all(rd, hashes=torch.from_numpy(hv[wlo:whi]).to(dev))
+            replayed = D.combine(w, device=dev)
+            got = sorted(bytes(r) for r in w.result())
+            out[f"wide_{order}"] = (got, w.count, bool(replayed))
         q.put((rank, out))
     except BaseException as ex:  # noqa: BLE001 -- reported to the parent
         q.put((rank, repr(ex)))
@@ -141,3 +164,13 @@ def test_gloo_ranks_real_engine(cuda, oracle, world):
             assert got == ref.result()[0].tolist() and cnt == cv.size, (rank, seed)
             replays += replayed
     assert replays > 0
+    rows, hs = _wide_stream()
+    for order, hv in hs.items():
+        ref = oracle.DistinctRows(700, 3, 24)
+        ref.sample_all(rows, hv)
+        want = sorted(bytes(r) for r in ref.result()[0])
+        for rank, out in outs:
+            got, cnt, replayed = out[f"wide_{order}"]
+            assert got == want and cnt == rows.shape[0], (rank, order)
+            if order == "ordered":
+                assert replayed, rank

@@ -97,6 +97,37 @@ def test_ffm_and_jni_call_sequences(tmp_path, cuda, oracle):
         xs.tofile(kf)
         cases.append(f"{name} {path} 1 {k} {kw} 0 {hash_kind} 0 0 {seed} 0 {xs.size} 0 {f} {kf}")
 
+    # java.util.UUID keys (KeyKind.UuidKey, 16 bytes [msb | lsb]): the harness writes key i as
+    # [v_i, ~v_i], v_i = splitmix64(base + i); the default hash is UUID.hashCode (on the GPU), a
+    # precomputed one 31 v + 7
+    def uuid_distinct(hash_kind, seed, k, n, base, path):
+        v = oracle.splitmix_keys(base, n)
+        v = np.concatenate([v, v[: n // 3]])
+        rows = np.stack([v, ~v], axis=1)
+        if hash_kind == HASH_DEFAULT:
+            ref = oracle.DistinctRows(k, seed, 16, "uuid")
+            ref.sample_all(rows.view(np.uint8))
+        else:
+            ref = oracle.DistinctRows(k, seed, 16)
+            ref.sample_all(rows.view(np.uint8), v * 31 + 7)
+        name = f"{path}_distinct_uuid_hash{hash_kind}"
+        f = tmp_path / f"{name}.bin"
+        ref.result()[0].tofile(f)
+        kf = tmp_path / f"{name}.keys"
+        rows.tofile(kf)
+        cases.append(f"{name} {path} 1 {k} 16 0 {hash_kind} 0 0 {seed} 0 {v.size} 0 {f} {kf}")
+
+    for path in ("ffm", "jni"):
+        uuid_distinct(HASH_DEFAULT, 8, 3000, 400_000, 35, path)
+        uuid_distinct(HASH_PRECOMPUTED, 9, 1000, 300_000, 36, path)
+    # UUID element samplers: key i = [v_i, ~v_i]
+    for path in ("ffm", "jni"):
+        v = oracle.splitmix_keys(37, 1_000_000)
+        win = oracle.algo_r_last_writers(11, 12, 500, 0, v.size)
+        want = np.stack([v[win], ~v[win]], axis=1)
+        f = tmp_path / f"{path}_elements_uuid.bin"
+        want.tofile(f)
+        cases.append(f"{path}_elements_uuid {path} 0 500 16 0 0 0 0 11 12 {v.size} 37 {f}")
     for path in ("ffm", "jni"):
         distinct(8, HASH_DEFAULT, 3, 5000, 600_000, 31, path)
         distinct(8, HASH_IDENTITY, 4, 4096, 500_000, 32, path)
