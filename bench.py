@@ -181,7 +181,9 @@ def secondary(dev) -> list:
             ("C4 default/ordered", lambda: P.c4(dev, "default")),
             ("C4 default/ordered replay branch", lambda: P.c4_replay(dev)),
             ("C2 java_l", lambda: P.c2l(dev)), ("C2 indexed", lambda: P.c2_indexed(dev)),
-            ("C4 combine", lambda: P.c4_merge(dev))]
+            ("C4 combine", lambda: P.c4_merge(dev)),
+            ("C4 16-byte UUID keys, set", lambda: P.c4_wide(dev, "set")),
+            ("C4 16-byte UUID keys, ordered", lambda: P.c4_wide(dev, "uuid"))]
     for name, fn in jobs:
         try:
             rs = fn()
@@ -306,7 +308,7 @@ def c4_leg(args, rank: int, world: int, dev, backend: str) -> dict:
 
 def load_traffic(n: int):
     """HBM bytes per K1 launch from the committed PMC pass (profiles/), if one matches n."""
-    for path in (os.path.join(ROOT, "profiles", r, "pmc_k1.json") for r in ("r03", "r02", "")):
+    for path in (os.path.join(ROOT, "profiles", r, "pmc_k1.json") for r in ("r05", "r04", "r03", "r02", "")):
         try:
             d = json.load(open(path))
             if int(d.get("n", -1)) == n:

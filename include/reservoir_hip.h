@@ -146,7 +146,12 @@ rsv_status rsv_sample_batch(rsv_sampler* s, const void* keys, int64_t n, int32_t
  * the slot did not change.  The caller maps exactly those elements (seq(offset)) and passes their
  * keys to rsv_fill_slots; until then every other call on the handle returns RSV_E_ILLEGAL_STATE.
  * ELEMENTS samplers only (Sampler.distinct maps every element: its sampleAll is the trait default,
- * S:50).  One K1 pass over the index range, k x 8 B back over PCIe -- no key crosses the link. */
+ * S:50).  One K1 pass over the index range, k x 8 B back over PCIe -- no key crosses the link.
+ * `map` then runs once per slot that changed, on its final holder: for a pure map the reservoir is
+ * the reference's.  The reference calls map on every fill-phase element and on every evicting
+ * element in order (S:241, :244, :269), so an impure map (side effects, call counts) or one that
+ * throws midway observes fewer calls here; such a map belongs on the keyed path (rsv_sample_batch
+ * with its keys), and a throw while keys are owed is undone with rsv_abort_indexed. */
 rsv_status rsv_sample_indexed(rsv_sampler* s, int64_t n, int64_t* slot_offsets_host);
 /* The keys owed after rsv_sample_indexed: keys_host holds k keys in slot order; entry j is read
  * only where slot_offsets_host[j] >= 0 (the rest may be anything). */
@@ -279,9 +284,9 @@ rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev);
  *   ELEMENTS: per slot the largest global index wins.
  *   DISTINCT: the bottom-k by (hash, key) of the union with the sampler's set, on the device (four
  *     kernels, no host wait: the set's size and tie state are read back at the next call on the
- *     handle); `tied` as rsv_merge_state.  On a caller stream the rows must stay valid and
- *     unchanged until the next call on the handle returns (a degenerate hash that overflows the
- *     merge's buckets is redone from them then).  Byte-key DISTINCT samplers merge before the call
+ *     handle); `tied` as rsv_merge_state.  The rows are the caller's again once the merge has run
+ *     in stream order (the engine keeps its own copy for a degenerate hash that overflows the
+ *     merge's buckets, redone at the next call).  Byte-key DISTINCT samplers merge before the call
  *     returns (the host reads the rows' meta words). */
 rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t parts, int64_t row_stride,
                             int64_t total_count);

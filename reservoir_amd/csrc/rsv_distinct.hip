@@ -922,43 +922,6 @@ __global__ __launch_bounds__(kBlock) void sched_filter(const KeyT* __restrict__ 
 // the scheduled merge's bucket filing, after the pass: the set's members (tag 0; backed up first,
 // restored if a bound fails verification) and the pass's logged candidates (tag 1 + batch index,
 // their count from the pass's counter ctl[0], at most cap).  Grid-stride over all of them.
-template <typename KeyT>
-__global__ __launch_bounds__(kBlock) void sched_file(const SchedDev* __restrict__ sd, const int64_t* __restrict__ cand_h,
-                                                     const KeyT* __restrict__ cand_k, const uint32_t* __restrict__ cand_i,
-                                                     int64_t* __restrict__ ctl, int64_t cap, const int64_t* __restrict__ set_h,
-                                                     const KeyT* __restrict__ set_k, int64_t m, int64_t* __restrict__ bh,
-                                                     KeyT* __restrict__ bk, uint32_t* __restrict__ bi,
-                                                     int64_t* __restrict__ bak_h, KeyT* __restrict__ bak_k) {
-    __shared__ int64_t stt[kMaxRanges];
-    const int nr = sd->nr;
-    if (nr < 2) return;
-    const int64_t off = sd->off;
-    cand_h += off;
-    cand_k += off;
-    cand_i += off;
-    for (int i = threadIdx.x; i < nr; i += blockDim.x) stt[i] = sd->t[i];
-    __syncthreads();
-    const uint32_t B_lo = sd->B_lo;
-    const uint64_t q = sd->lo_mult;
-    SchedSink<KeyT> sink{SchedMap{sd, stt, sd->B, B_lo, (uint32_t)nr, stt[nr - 1], q > UINT64_MAX / B_lo ? UINT64_MAX : q * B_lo},
-                         bucket_count(ctl), bh, bk, bi, ctl + 1};
-    const int64_t c = std::min<int64_t>((int64_t)__hip_atomic_load((const unsigned long long*)ctl, __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_AGENT), cap);
-    const int64_t total = m + c, stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
-        if (t < m) {
-            const int64_t h = set_h[t];
-            const KeyT key = set_k[t];
-            bak_h[t] = h;
-            bak_k[t] = key;
-            sink.put(h, key, 0u);
-        } else {
-            const int64_t e = t - m;
-            sink.put(cand_h[e], cand_k[e], cand_i[e] + 1u);
-        }
-    }
-}
-
 // ---- the plan (host: sched_sample; device: ctl_plan, the fused first chunk + pass) ------------
 __host__ __device__ inline double sched_ufrac(int64_t t) {  // fraction of the hash range at or below t
     return ((double)((uint64_t)t - (uint64_t)INT64_MIN) + 1.0) / 18446744073709551616.0;
@@ -1303,52 +1266,6 @@ __device__ __forceinline__ uint32_t wave_sort_bucket_tagged(const Src src, int64
         prev_k_last = shfl_any(k[r], 63);
     }
     return base;
-}
-
-// (dev builds only, -DRSV_SCHED_FINE: sched_file + sched_sort, the round-3 form of the scheduled
-// merge -- one returning atomic per entry, one wave per fine bucket from global memory)
-template <typename KeyT>
-__global__ __launch_bounds__(kBlock) void sched_sort(int64_t m, int64_t cand_cap, int64_t* __restrict__ ctl,
-                                                     int32_t log_bmax, int64_t* __restrict__ bh, KeyT* __restrict__ bk,
-                                                     uint32_t* __restrict__ bi, const SchedDev* __restrict__ sd,
-                                                     int* __restrict__ vacc) {
-    __shared__ int64_t sb[kMaxRanges + 1], stt[kMaxRanges];
-    __shared__ int sdiff[kMaxRanges + 1];
-    const int64_t c = ctl[0];
-    const int nr = sd->nr;
-    if (c > cand_cap || ctl[1] || nr < 2) return;  // uniform over the grid
-    for (int i = threadIdx.x; i <= nr; i += blockDim.x) {
-        sb[i] = sd->b[i];
-        sdiff[i] = 0;
-        if (i < nr) stt[i] = sd->t[i];
-    }
-    __syncthreads();
-    const uint32_t b = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    if (b < sd->B) {
-        uint32_t* bcnt = bucket_count(ctl) + (size_t)b * kCountStride;
-        uint32_t* bdist = bucket_distinct(ctl, log_bmax) + b;
-        const uint32_t n = *bcnt;
-        int64_t* gh = bh + (size_t)b * kBucketCap;
-        KeyT* gk = bk + (size_t)b * kBucketCap;
-        uint32_t* gi = bi + (size_t)b * kBucketCap;
-        uint32_t nd = 0;
-        if (n > 0)
-        {
-            const BucketSrc<KeyT> src{gh, gk, gi};
-            nd = n <= 64    ? wave_sort_bucket_tagged<KeyT, 1>(src, gh, gk, n, sb, stt, nr, sdiff)
-                 : n <= 128 ? wave_sort_bucket_tagged<KeyT, 2>(src, gh, gk, n, sb, stt, nr, sdiff)
-                            : wave_sort_bucket_tagged<KeyT, 4>(src, gh, gk, n, sb, stt, nr, sdiff);
-        }
-        if ((threadIdx.x & 63) == 0) {
-            *bdist = nd;
-            if (nd) atomicAdd(bucket_group(ctl, log_bmax) + (b >> 4), nd);
-            *bcnt = 0;
-        }
-    }
-    __syncthreads();
-    int* acc = vacc + (size_t)(blockIdx.x % kVerifyCopies) * (kMaxRanges + 1);
-    for (int i = threadIdx.x; i <= nr; i += blockDim.x)
-        if (sdiff[i]) atomicAdd(&acc[i], sdiff[i]);
 }
 
 // ---- the scheduled merge by coarse bins (sched_bin_file -> sched_bin_sort) -------------------
@@ -2046,7 +1963,9 @@ struct DistinctState {
     bool pend = false;
     uint32_t pend_gen = 0;
     uint32_t pend_lb = 0;
-    const int64_t* pend_rows = nullptr;  // caller rows, valid until the settle (overflow fallback)
+    const int64_t* pend_rows = nullptr;  // the rows' snapshot (rows_copy) a bucket overflow redoes the merge from
+    int64_t* rows_copy = nullptr;        // engine-owned copy of the last merged rows (the caller may reuse theirs)
+    int64_t rows_copy_cap = 0;           // words
     int32_t pend_parts = 0;
     int64_t pend_stride = 0;
     uint32_t* mstart = nullptr;  // [(parts + 1) x (B + 1)] bucket starts of every run
@@ -2236,7 +2155,7 @@ void distinct_destroy(DistinctState* d) {
     void* ps[] = {d->set_h, d->set_k, d->cand_h, d->cand_k, d->ctl, d->bh, d->bk, d->mh0, d->mh1, d->mk0,
                   d->mk1, d->flags, d->pos, d->d_count, d->samp, d->temp, d->log_h, d->log_k, d->log_i,
                   d->perm, d->sorted_i, d->ord_h, d->ord_k, d->sdev, d->sctl, d->sbh, d->sbk, d->sbi, d->vacc,
-                  d->bak_h, d->bak_k, d->mstart, d->fk_in, d->fk_out, d->fv, d->fflag};
+                  d->bak_h, d->bak_k, d->mstart, d->fk_in, d->fk_out, d->fv, d->fflag, d->rows_copy};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
     pool_host_free(d->h_pinned);
     pool_host_free(d->hc);
@@ -2970,32 +2889,17 @@ static int sched_launch(DistinctState* d, const KeyT* keys, const int64_t* hashe
         // one entry per thread (the count is on the device: sized for the buffer's capacity, idle
         // threads exit): every bucket atomic in flight at once -- a 1024-workgroup grid-stride over
         // ~1.1 M entries waited on ~4 atomics per thread in sequence (61 us)
-#ifdef RSV_SCHED_FINE  // dev A/B: the per-entry filing and one wave per fine bucket from global memory
-        const unsigned fgrid = (unsigned)std::min<int64_t>((k + cap + kBlock - 1) / kBlock, 16384);
-        hipLaunchKernelGGL(sched_file<KeyT>, dim3(fgrid), dim3(kBlock), 0, st, (const SchedDev*)d->sdev,
-                           (const int64_t*)(d->log_h + lbase), (const KeyT*)lk, (const uint32_t*)(d->log_i + lbase),
-                           d->sctl, cap, (const int64_t*)d->set_h, (const KeyT*)d->set_k, k, d->sbh, bk, d->sbi,
-                           d->bak_h, (KeyT*)d->bak_k);
-#else
         const uint32_t C = 1u << bin_log((uint32_t)lb);
         const unsigned fgrid = (unsigned)((k + cap + kBinFileThreads * kBinTile - 1) / (kBinFileThreads * kBinTile));
         hipLaunchKernelGGL(sched_bin_file<KeyT>, dim3(fgrid), dim3(kBinFileThreads), C * 4, st, (const SchedDev*)d->sdev,
                            (const int64_t*)(d->log_h + lbase), (const KeyT*)lk, (const uint32_t*)(d->log_i + lbase),
                            d->sctl, cap, (const int64_t*)d->set_h, (const KeyT*)d->set_k, k, d->sbh, bk, d->sbi,
                            d->bak_h, (KeyT*)d->bak_k);
-#endif
         STRY(hipGetLastError());
     }
     if (d->timer) d->timer->mark(st);
-#ifdef RSV_SCHED_FINE
-    // the difference array's -1s aggregated per wave (one LDS atomic per bucket, not per element):
-    // sched_sort 64.9 -> 60.4 us (DESIGN.md 5 decision 6)
-    hipLaunchKernelGGL(sched_sort<KeyT>, dim3((B + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, k, cap,
-                       d->sctl, d->log_bmax_s, d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
-#else
     hipLaunchKernelGGL(sched_bin_sort<KeyT>, dim3(1u << bin_log((uint32_t)lb)), dim3(kBinSortThreads), 0, st, cap, d->sctl, d->log_bmax_s,
                        d->sbh, bk, d->sbi, (const SchedDev*)d->sdev, d->vacc);
-#endif
     hipLaunchKernelGGL(bucket_emit<KeyT>, dim3((B + kEmitBuckets - 1) / kEmitBuckets), dim3(kBlock), 0, st, k, cap,
                        d->sctl, d->log_bmax_s, (const int64_t*)d->sbh, (const KeyT*)bk, k, d->set_h, (KeyT*)d->set_k, lb);
     *gen = ++d->sgen;
@@ -3562,12 +3466,22 @@ static int merge_rows_impl(DistinctState* d, const int64_t* rows, int32_t parts,
     const uint32_t gen = ++d->sgen;
     hipLaunchKernelGGL(merge_publish, dim3(1), dim3(64), 0, st, d->sctl, d->shc_dev, (uint32_t*)(d->shc_dev + 12), gen);
     RSV_HIP_TRY(hipGetLastError());
+    // the rows as merged, in engine memory: a degenerate hash that overflows a bucket is redone from
+    // them at the settle, while the caller may already be reusing its gather buffer (stream-ordered
+    // behind the merge kernels: parts x (2k + 6) words, ~8 MB at 8 x 65536)
+    const int64_t rw = 2 * k + kRowMeta;
+    if ((int64_t)parts * rw > d->rows_copy_cap) {
+        RSV_HIP_TRY(grow((void**)&d->rows_copy, 0, (size_t)parts * rw * 8, false, st));
+        d->rows_copy_cap = (int64_t)parts * rw;
+    }
+    RSV_HIP_TRY(hipMemcpy2DAsync(d->rows_copy, (size_t)rw * 8, rows, (size_t)stride * 8, (size_t)rw * 8, (size_t)parts,
+                                 hipMemcpyDeviceToDevice, st));
     d->pend = true;
     d->pend_gen = gen;
     d->pend_lb = (uint32_t)lb;
-    d->pend_rows = rows;
+    d->pend_rows = d->rows_copy;
     d->pend_parts = parts;
-    d->pend_stride = stride;
+    d->pend_stride = rw;
     merged_bookkeeping(d);
     return RSV_OK;
 }

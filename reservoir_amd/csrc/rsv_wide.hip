@@ -681,9 +681,10 @@ hipError_t ensure_log(WideDistinct* d, int64_t need, hipStream_t st) {
     return hipSuccess;
 }
 
-// one chunk [off, off + L) of the batch: filter, rows, log, merge
+// one chunk [off, off + L) of the batch: filter (bound: the set's maximum, or `bound_in` when given),
+// rows, log, merge
 hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes, int64_t off, int64_t L,
-                        int64_t gbase, hipStream_t st) {
+                        int64_t gbase, hipStream_t st, const int64_t* bound_in = nullptr) {
     const uint64_t* rows = (const uint64_t*)keys + (size_t)off * d->words;
     const int64_t* hv = hashes ? hashes + off : nullptr;
     hipError_t e;
@@ -702,7 +703,7 @@ hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes
         if ((e = hipGetLastError())) return e;
         c = L;
     } else {
-        const int64_t bound = d->top;  // inclusive: the boundary bucket's members stay candidates
+        const int64_t bound = bound_in ? *bound_in : d->top;  // inclusive: the boundary bucket stays
         if ((e = ensure_cand(d, 8 * (int64_t)d->k + 4096, st))) return e;
         const unsigned g = (unsigned)std::min<int64_t>(
             std::max<int64_t>((L / (d->src == kWideSrcHashes ? 2 * kWideU : kWideU) + kWBlock - 1) / kWBlock, 1),
@@ -842,11 +843,33 @@ int wide_sample_device(WideDistinct* d, const void* keys, const int64_t* hashes,
         d->arch_k.clear();
         d->arch_ok = false;
     }
+    const int64_t seen0 = d->seen;
+    bool predicted = false;
     for (int64_t off = 0; off < n;) {
+        const int64_t rest = n - off;
+        if (!d->ordered && d->m == d->k && !predicted && rest > 4 * d->seen) {
+            // Set mode, a long rest: ONE pass with the bound the rest's bottom-k is predicted under.
+            // The scrambled hash is uniform, so the k-th smallest of D distinct values sits near
+            // k / D of the range; with the rest's distinct share like the seen part's, the final
+            // maximum is about (top - MIN) seen / (seen + rest) above MIN -- times beta = 2.  The
+            // merge proves it: a full set whose maximum is <= B saw every element under it; else the
+            // rest is filtered again by the chunk loop (duplicate candidates are merged away).
+            predicted = true;
+            const double frac = 2.0 * (double)d->seen / (double)(d->seen + rest);
+            const uint64_t span = (uint64_t)d->top - (uint64_t)INT64_MIN;
+            const int64_t B = frac >= 1.0 ? d->top : (int64_t)((uint64_t)INT64_MIN + (uint64_t)((double)span * frac));
+            if (hipError_t e = sample_chunk(d, keys, hashes, off, rest, seen0, st, &B))
+                return fail_hip(e, "distinct sample");
+            if (d->m == d->k && d->top <= B) {
+                d->seen += rest;
+                break;
+            }
+            continue;  // the prediction was short: the chunk loop below covers the same rest
+        }
         // filling: enough for the set plus slack; full: ~4 seen lengths (~4k candidates a chunk)
-        const int64_t L = d->m < d->k ? std::min<int64_t>(n - off, 4 * ((int64_t)d->k - d->m) + 4096)
-                                      : std::min<int64_t>(n - off, std::max<int64_t>(4 * d->seen, 1 << 16));
-        if (hipError_t e = sample_chunk(d, keys, hashes, off, L, d->seen - off, st)) return fail_hip(e, "distinct sample");
+        const int64_t L = d->m < d->k ? std::min<int64_t>(rest, 4 * ((int64_t)d->k - d->m) + 4096)
+                                      : std::min<int64_t>(rest, std::max<int64_t>(4 * d->seen, 1 << 16));
+        if (hipError_t e = sample_chunk(d, keys, hashes, off, L, seen0, st)) return fail_hip(e, "distinct sample");
         off += L;
         d->seen += L;
     }

@@ -56,7 +56,8 @@ def _mark(marks) -> None:
         marks.append(ev)
 
 
-def combine(sampler, group=None, device=None, total_count: int | None = None, marks: list | None = None) -> bool:
+def combine(sampler, group=None, device=None, total_count: int | None = None, marks: list | None = None,
+            strict: bool = True) -> bool:
     """All-gather the partial states of every rank and merge them into ``sampler`` (on all ranks).
 
     One collective: each rank packs its partial state into one int64 row (rsv_export_packed) --
@@ -69,7 +70,10 @@ def combine(sampler, group=None, device=None, total_count: int | None = None, ma
     Ordered distinct samplers (the reference's default ``hashCode``) read the merged state back
     once; when its boundary hash bucket is oversubscribed they take one more exchange, the exact
     replay: rank r holds the r-th piece of the stream, and the result is the reference's
-    sequential set (every rank needs ``retain_log``).  Returns whether the replay ran.
+    sequential set (every rank needs ``retain_log``; ``sample_shard`` sets it).  When the replay is
+    needed and a rank did not retain its log, ``strict`` (default) raises IllegalStateException --
+    the reference's set cannot be formed -- and ``strict=False`` warns and keeps the (hash, key)
+    bottom-k instead.  Returns whether the replay ran.
     ``marks`` (a list): CUDA events are appended after the export, the all-gather and the merge.
     """
     world = dist.get_world_size(group)
@@ -94,7 +98,7 @@ def combine(sampler, group=None, device=None, total_count: int | None = None, ma
     _mark(marks)
     if not sampler.is_ordered:
         return False
-    meta = _ordered_replay_meta(sampler, rows)
+    meta = _ordered_replay_meta(sampler, rows, strict)
     if meta is None:
         return False
     w = _key_words(sampler)
@@ -115,12 +119,12 @@ def combine(sampler, group=None, device=None, total_count: int | None = None, ma
     return True
 
 
-def merge_local(target, shards, total_count: int | None = None) -> bool:
+def merge_local(target, shards, total_count: int | None = None, strict: bool = True) -> bool:
     """``combine`` without a process group: ``shards`` are samplers that each saw one contiguous
     piece of a stream, in order (shard r = rank r), all on one device; their merged state goes into
     ``target`` (a fresh sampler, or one of the shards).  Same rows, merge kernels and exact ordered
     replay as ``combine`` -- e.g. C4's 8-way split rehearsed on one GPU.  Returns whether the exact
-    ordered replay ran."""
+    ordered replay ran (``strict`` as in ``combine``)."""
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
     rows = torch.empty((len(shards), target.packed_width), dtype=torch.int64, device=dev)
     for r, s in enumerate(shards):
@@ -135,7 +139,7 @@ def merge_local(target, shards, total_count: int | None = None) -> bool:
     target.merge_packed(rows, total)
     if not target.is_ordered:
         return False
-    meta = _ordered_replay_meta(target, rows)
+    meta = _ordered_replay_meta(target, rows, strict)
     if meta is None:
         return False
     bounds = replay_bounds(rows, meta, k, _key_words(target))
@@ -168,7 +172,7 @@ def _as_words(keys) -> np.ndarray:
     return keys.astype(np.int64)
 
 
-def _ordered_replay_meta(sampler, rows):
+def _ordered_replay_meta(sampler, rows, strict: bool = True):
     """After the device merge of an ordered sampler: the per-rank meta (host) when the exact replay
     is needed, else None.  The merged set is the reference's unless more distinct elements share its
     maximum hash than it keeps -- seen in the union, or inside one rank whose own boundary bucket
@@ -180,9 +184,14 @@ def _ordered_replay_meta(sampler, rows):
     if not all(int(m[5]) for m in meta):
         return None  # some rank ran in set mode: the (hash, key) set is the defined result
     if not all(int(m[4]) for m in meta):
-        warnings.warn("ordered distinct combine: a rank did not retain its candidate log (retain_log); the "
-                      "merged set resolves the boundary hash bucket by (hash, key) instead of arrival order",
-                      RuntimeWarning)
+        msg = ("ordered distinct combine: the boundary hash bucket is oversubscribed and a rank did not retain "
+               "its candidate log (Sampler.distinct(..., retain_log=True), or distributed.sample_shard), so the "
+               "reference's arrival-order set cannot be formed")
+        if strict:
+            from ._native import IllegalStateException
+
+            raise IllegalStateException(msg)
+        warnings.warn(msg + "; strict=False: the merged set resolves the bucket by (hash, key)", RuntimeWarning)
         return None
     return meta
 

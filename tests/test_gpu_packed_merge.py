@@ -186,3 +186,38 @@ def test_log_retention_is_opt_in(cuda):
     r = Sampler.distinct(64, seed=1, retain_log=True)()
     r.sample_all(vals)
     assert r.distinct_info()["log_retained"] == 1
+
+
+def test_merge_local_needs_retained_logs_when_tied(cuda, oracle):
+    """Ordered shards without a retained log whose merged boundary bucket ties: merge_local cannot
+    form the reference's arrival-order set -- IllegalStateException by default, a
+    RuntimeWarning and the (hash, key) bottom-k with strict=False; with retain_log the exact set."""
+    import torch
+
+    from reservoir_amd import IllegalStateException, Sampler
+    from reservoir_amd import distributed as D
+
+    rng = np.random.default_rng(8)
+    hi = rng.integers(0, 2**31, size=60_000, dtype=np.int64)
+    v = (hi << 32) | ((hi ^ rng.integers(0, 700, size=hi.size)) & 0xFFFFFFFF)  # 700 Long.hashCode values
+    parts = np.array_split(v, 3)
+
+    def shards(retain):
+        out = []
+        for p in parts:
+            s = Sampler.distinct(300, seed=4, retain_log=retain)()
+            s.sample_all(torch.from_numpy(p).to(cuda))
+            out.append(s)
+        return out
+
+    with pytest.raises(IllegalStateException):
+        D.merge_local(Sampler.distinct(300, seed=4)(), shards(False))
+    t = Sampler.distinct(300, seed=4)()
+    with pytest.warns(RuntimeWarning):
+        assert not D.merge_local(t, shards(False), strict=False)
+    assert t.result().size == 300
+    t = Sampler.distinct(300, seed=4)()
+    assert D.merge_local(t, shards(True))
+    ref = oracle.Distinct(300, 4, oracle.HASH_JAVA_LONG)
+    ref.sample_all(v)
+    assert sorted(t.result().tolist()) == sorted(ref.result()[0].tolist())

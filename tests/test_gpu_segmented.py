@@ -11,9 +11,9 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("k", [1, 5, 64, 100, 1024, 3000, 4400, 4416, 4417, 8192, 65536])
 def test_ragged_parity(cuda, oracle, k):
-    """k = 3000 / 4400: the winner table exceeds 64 KB of dynamic LDS (k2::lds_bytes); 4416 is the
-    largest k whose four tables fit one workgroup's 160 KB; from 4417 on every wave's table is a
-    slice of global scratch (k2_segmented<..., GT = true>, rsv_segmented.hip)."""
+    """k < 512: one wave per stream (k2_segmented); from k = 512 one workgroup per stream with one
+    shared table (k2_segmented_wg): in LDS up to k ~ 29.5k (u32 entries), beyond that a slice of the
+    persistent global scratch (k = 65536)."""
     import torch
 
     from reservoir_amd import batch
@@ -200,3 +200,29 @@ def test_slot_chi_square(cuda):
     chi2 = ((bins - exp) ** 2 / exp).sum()
     # sampling without replacement lowers the variance; dof 63: p(chi2 > 120) < 1e-5
     assert chi2 < 120, chi2
+
+
+def test_wg_global_scratch_reuse(cuda, oracle):
+    """k = 40000: the workgroup form's table lives in the per-device global scratch, zeroed once and
+    left zero by every launch.  Back-to-back launches on one stream, then on a second stream while the
+    first may still run (a private zeroed block), all equal the oracle."""
+    import torch
+
+    from reservoir_amd import batch
+
+    k = 40_000
+    rng = np.random.default_rng(9)
+    lens = rng.integers(0, 3 * k, size=40)
+    lens[:3] = [0, k, 2 * k + 7]
+    offs = np.r_[0, np.cumsum(lens)].astype(np.int64)
+    keys = oracle.splitmix_keys(5, int(offs[-1]))
+    want, wcnt = oracle.algo_r_segmented(3, 9, k, keys, offs)
+    kd, od = torch.from_numpy(keys).to(cuda), torch.from_numpy(offs).to(cuda)
+    outs = [batch.sample_segmented(kd, od, k, seed=3, stream_base=9) for _ in range(2)]
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        outs.append(batch.sample_segmented(kd, od, k, seed=3, stream_base=9))
+    torch.cuda.synchronize()
+    for out, cnt in outs:
+        assert np.array_equal(cnt.cpu().numpy(), wcnt)
+        assert np.array_equal(out.cpu().numpy(), want)

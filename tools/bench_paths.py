@@ -9,6 +9,9 @@
   C3K K2 past the LDS winner table (k = 8192, global tables) beside k = 4096 on 4096 x 2^17 keys
   C4M C4's combine on one GPU: 8 shard sets of k = 65536 merged by distributed.merge_local
       (8 x rsv_export_packed + the device rsv_merge_packed), both hashes
+  C4W C4's share as 16-byte UUID keys (rsv_wide.hip): a precomputed 64-bit hash in set mode (the
+      filter reads the 8-B hashes only), UUID.hashCode in ordered mode (the filter reads the 16-B
+      rows), and UUID hash twins (the ordered host replay)
 
 Prints one JSON line per config with the kernel time (HIP events on the launch stream) and the
 8-B-per-element HBM roofline fraction.  Usage: python tools/bench_paths.py [--only c3,c4,c2l]
@@ -176,6 +179,68 @@ def c4(dev, hash_kind="identity", order="auto", twins=False, seed=7):
             "filter_achieved_GBs": read / kt / 1e9, "hbm_frac_filter": read / kt / 1e9 / HBM}
 
 
+def c4_wide(dev, mode="set"):
+    """C4's share (5e8 keys, 30 % duplicates, k = 65536) as 16-byte UUIDs: mode "set" (precomputed
+    64-bit hash tensor, set mode), "uuid" (default UUID.hashCode, ordered), "twins" (UUID hash twins,
+    ordered: the host replay).  Filter bytes per element: 8 (hashes) or 16 (rows)."""
+    import workloads as W
+
+    from reservoir_amd import Sampler, _native
+
+    n, k = 500_000_000, 65536
+    vals = c4_data(n, dev)
+    rows = W.uuid_rows(vals, 26 if mode == "twins" else None)
+    hs = W.smix(vals ^ 0x5A5A) if mode == "set" else None
+    del vals
+    torch.cuda.synchronize()
+    L = _native.load()
+    times, kern = [], []
+
+    def make():
+        if mode == "set":
+            return Sampler.distinct(k, key_type="bytes16", seed=7, order="set")(hash=lambda b: 0)
+        return Sampler.distinct(k, key_type="bytes16", seed=7)()
+
+    def feed(d):
+        if hs is not None:
+            d.sample_all(rows, hashes=hs)
+        else:
+            d.sample_all(rows)
+
+    for rep in range(7 if mode != "twins" else 4):
+        prof = rep == (6 if mode != "twins" else 3)
+        d = make()
+        d.set_stream(torch.cuda.current_stream().cuda_stream)
+        if prof:
+            _native.check(L.rsv_profile_enable(d.handle, 1))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        feed(d)
+        r = d.result()
+        t1 = time.perf_counter()
+        if prof:
+            ms, cnt = C.c_double(), C.c_int64()
+            _native.check(L.rsv_profile_read(d.handle, C.byref(ms), C.byref(cnt)))
+            kern.append((ms.value / 1e3, cnt.value))
+        elif rep:
+            times.append(t1 - t0)
+        assert r.shape == (k, 16)
+        d.close()
+    t = sorted(times)[len(times) // 2]
+    kt, passes = kern[0]
+    per = 8 if mode == "set" else 16
+    read = n * per  # the filter chunks cover all but the first ~4k + 4096 elements
+    del rows, hs
+    torch.cuda.empty_cache()
+    what = {"set": "precomputed 64-bit hash, set mode (filter reads the 8-B hashes)",
+            "uuid": "default UUID.hashCode, ordered mode (filter reads the 16-B rows)",
+            "twins": "UUID hash twins (~5 keys per hashCode), ordered: the host replay runs"}[mode]
+    return {"config": f"C4 (one GPU's share) distinct 5e8 16-byte UUID keys 30% dup, k=65536, {what}",
+            "elements": n, "seconds_end_to_end": t, "Gelem_s": n / t / 1e9,
+            "filter_launches": passes, "filter_seconds_total": kt, "filter_bytes_per_element": per,
+            "filter_achieved_GBs": read / kt / 1e9, "hbm_frac_filter": read / kt / 1e9 / HBM}
+
+
 def c4_replay(dev):
     """C4's share with hash twins: the ordered mode's host-replay branch, as its own line."""
     return c4(dev, "default", twins=True, seed=11)
@@ -300,6 +365,10 @@ def main():
         for r in c3_large_k(dev):
             print(json.dumps(r), flush=True)
         torch.cuda.empty_cache()
+    if "c4w" in todo:
+        for mode in ("set", "uuid", "twins"):
+            print(json.dumps(c4_wide(dev, mode)), flush=True)
+            torch.cuda.empty_cache()
     if "c4m" in todo:
         for r in c4_merge(dev):
             print(json.dumps(r), flush=True)

@@ -1,13 +1,15 @@
-// rsv_k2.h -- the K2 segmented kernel (rsv_segmented.hip launches it).  See rsv_segmented.hip for
-// the design.  (The cost-probe variants of earlier rounds live in tools/k2_dev_variants.h.)
+// k2_dev_variants.h -- DEVELOPMENT ONLY (tools/micro_k2.hip): the round-4 K2 kernel with its cost-probe
+// variants V (V = 0 was the product kernel; the others produce wrong results on purpose -- no
+// level-1 Philox, candidates dropped, no gather ...).  The product kernel is
+// reservoir_amd/csrc/rsv_k2.h, which carries no variants.
 #pragma once
 #include <algorithm>
 #include <type_traits>
 
-#include "rsv_device.h"
+#include "../reservoir_amd/csrc/rsv_device.h"
 
 namespace rsv {
-namespace k2 {
+namespace k2dev {
 
 constexpr int kWaves = 4;          // waves per workgroup
 constexpr uint32_t kRing = 4;      // level-0 iterations whose block words stay addressable
@@ -18,12 +20,22 @@ constexpr uint32_t kLut = 1024;    // blocks (16 indices each) whose threshold T
 constexpr uint32_t kLutBytes = kLut * 2;
 constexpr int64_t kSmallLen = 1ll << 27;  // streams shorter than this use 32-bit index arithmetic
 
-// bytes of dynamic LDS per workgroup: T table + per wave (stash | FIFO | k-slot table)
-__host__ __device__ inline size_t lds_bytes(uint32_t k) {
-    return kLutBytes + (size_t)kWaves * (kStashBytes + kQueueBytes + (size_t)k * 8);
+// FIFO entries of variant V (tools/micro_k2: V & 128 = the 2048-entry FIFO of r02 up to 696f99e,
+// which held any iteration: 4 workgroups per CU by LDS instead of 6)
+__host__ __device__ constexpr uint32_t qcap_of(int V) { return (V & 128) ? 2048u : kQCap; }
+
+// stash ring of variant V (V & 256: 2 iterations, occupancy probe)
+__host__ __device__ constexpr uint32_t ring_of(int V) { return (V & 256) ? 2u : kRing; }
+
+// bytes of dynamic LDS per workgroup: T table + per wave (stash | FIFO | k-slot table; GT: the
+// table lives in global memory)
+__host__ __device__ inline size_t lds_bytes(uint32_t k, int V = 0, bool GT = false) {
+    return kLutBytes + (size_t)kWaves * (ring_of(V) * 64 * 16 + qcap_of(V) * 2 + (GT ? 0 : (size_t)k * 8));
 }
 
-constexpr size_t kLdsMax = 160 * 1024;  // one workgroup's LDS
+// the LDS table form serves k while lds_bytes fits one workgroup's 160 KB (k <= 4416); above that
+// each wave's k-slot table is a slice of a global scratch buffer (k2_segmented<..., GT = true>)
+constexpr size_t kLdsMax = 160 * 1024;
 
 // T = ceil(256 k / (i0 + 1)), the block threshold of the dense region (T > 255: every byte is a
 // candidate -> 256); 0 marks the sparse region (i0 + 1 >= 256 k: only b == 0 can hit)
@@ -120,15 +132,19 @@ struct Wave {
 // whose high words are wave-uniform (level 0: g < 2^32; level 1: i/2 < 2^32).
 // DEFER (k <= 64): the lane's winner index is returned (-1: none) and the caller gathers its key
 // after storing the previous stream's, so the random gather's latency overlaps the next stream's draws.
-// (k >= kWGMinK takes the workgroup form below, k2_segmented_wg.)
-template <typename KeyT, bool SMALL, bool DEFER>
+// GT: the winner table is the wave's slice of global scratch (large k).  It is all zero when the
+// stream starts (zeroed once before the launch, and the gather below takes every entry with an
+// atomic exchange against 0), and the gather waits for the wave's own atomics (vmcnt counts
+// returnless global atomics on gfx950 until they are performed) before it reads them.
+template <typename KeyT, int V, bool SMALL, bool DEFER, bool GT = false>
 __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restrict__ keys, int64_t off, int64_t len,
                                              uint64_t stream, KeyT* __restrict__ o) {
     using IdxT = typename std::conditional<SMALL, uint32_t, uint64_t>::type;
-    constexpr uint32_t QC = kQCap, RG = kRing, WIN = RG * 1024;  // WIN: indices in the ring
+    constexpr uint32_t QC = qcap_of(V), RG = ring_of(V), WIN = RG * 1024;  // WIN: indices in the ring
     const uint32_t lane = W.lane, k = W.k;
     IdxT* tab = (IdxT*)W.tab;
-    for (uint32_t j = lane; j < k; j += 64) tab[j] = 0;
+    if constexpr (!GT)
+        for (uint32_t j = lane; j < k; j += 64) tab[j] = 0;
     const uint32_t s0 = (uint32_t)stream, s1 = (uint32_t)(stream >> 32);
     const DrawKey dk{W.k0, W.k1, s0, s1};
     const IdxT n_groups = (IdxT)(((uint64_t)len + 15) >> 4);
@@ -151,8 +167,13 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
         const uint32_t b = level0_byte(w, e);
         const IdxT g1 = i >> 1;
         u32x4 w1;
-        if constexpr (SMALL) w1 = philox4x32_10_uniform_hi((uint32_t)g1, kDomainLevel1, s0, s1, W.k0, W.k1);
-        else w1 = philox4x32_10((uint32_t)g1, (uint32_t)((uint64_t)g1 >> 32) | kDomainLevel1, s0, s1, W.k0, W.k1);
+        if constexpr ((V & 2) != 0) {  // variant: no level-1 Philox (cost probe)
+            w1 = u32x4{(uint32_t)g1 * 0x9E3779B9u, (uint32_t)g1 ^ s0, w.x, w.y};
+        } else if constexpr (SMALL) {
+            w1 = philox4x32_10_uniform_hi((uint32_t)g1, kDomainLevel1, s0, s1, W.k0, W.k1);
+        } else {
+            w1 = philox4x32_10((uint32_t)g1, (uint32_t)((uint64_t)g1 >> 32) | kDomainLevel1, s0, s1, W.k0, W.k1);
+        }
         // all four words, then one select per half (else the compiler selects the last round's
         // operands instead: 7 v_cndmask for the one saved product)
         asm volatile("" : "+v"(w1.x), "+v"(w1.y), "+v"(w1.z), "+v"(w1.w));
@@ -169,11 +190,12 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
     // The head is cut to whole 64-pair rounds (k = 64: [64, 192) instead of [64, 256): its 96 pairs
     // took two rounds, the second half empty; the 64 indices moved to the FIFO add ~20 candidates
     // to rounds it runs anyway): C3 1.75-1.76 -> 1.67-1.69 ms (tools/micro_k2 r, warm clock).
-    constexpr uint32_t HM = 4;
+    constexpr uint32_t HM = (V & 32) ? 2u : (V & 64) ? 1u : (V & 16384) ? 6u : (V & 32768) ? 8u : 4u;
     uint64_t hx = (uint64_t)HM * k;
     // (only where the head holds at least one whole round: below k = 43 the cut would remove it and
-    // send the 25-100 % dense region through the FIFO)
-    if (hx - k >= 128) hx = k + ((hx - k) & ~(uint64_t)127);
+    // send the 25-100 % dense region through the FIFO; V & 512: the r02 head everywhere)
+    if constexpr ((V & 512) == 0)
+        if (hx - k >= 128) hx = k + ((hx - k) & ~(uint64_t)127);
     const IdxT hend = (IdxT)std::min<uint64_t>((uint64_t)len, hx);
     const IdxT flo = std::max<IdxT>((IdxT)k, hend);
     for (; gb < n_groups; gb += 64, ring = (ring + 1) & (RG - 1)) {
@@ -191,13 +213,14 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
         // T falls with the block index, so lane 0's (block gb) bounds the iteration's: past the first
         // blocks of a stream every lane has T <= 16 (C3: iterations 1..3) and takes the short compare
         const uint32_t Tmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)T);
-        uint32_t mask = valid ? (Tmax <= 16u ? mask_for_small(w, T) : mask_for(w, T)) : 0u;
+        uint32_t mask = valid ? ((Tmax <= 16u && (V & 8192) == 0) ? mask_for_small(w, T) : mask_for(w, T)) : 0u;
+        if constexpr ((V & 4096) != 0) mask = (mask == 0x12345u) ? 1u : 0u;  // variant: no candidates (cost probe)
         bool clip;  // wave-uniform; 32-bit compares for SMALL (scalar: no 64-bit s_cmp_lt)
         if constexpr (SMALL) clip = ((uint32_t)gb << 4) < (uint32_t)flo || (((uint32_t)gb + 64) << 4) > (uint32_t)len;
         else clip = ((uint64_t)gb << 4) < (uint64_t)flo || (((uint64_t)gb + 64) << 4) > (uint64_t)len;
         if (clip) mask &= clip16(i0, (uint64_t)flo, (uint64_t)len);
         W.stash[ring * 64 + lane] = w;
-        if (((uint64_t)gb << 4) < (uint64_t)hend) {  // this iteration holds head indices (uniform)
+        if ((V & 1024) == 0 && ((uint64_t)gb << 4) < (uint64_t)hend) {  // this iteration holds head indices (uniform)
             __builtin_amdgcn_wave_barrier();
             const IdxT ia = std::max<IdxT>((IdxT)k & ~(IdxT)1, gb << 4);
             const IdxT ib = std::min<IdxT>(hend, (gb + 64) << 4);
@@ -223,7 +246,9 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
         const uint32_t incl = wave_incl_scan(cnt);
         const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint32_t tag = (ring << 10) | (lane << 4);  // = (g mod 256) << 4
-        if (tail - head + tot <= W.fifo_cap) {  // uniform: the whole iteration fits
+        if constexpr ((V & 2048) != 0) {  // variant: no FIFO append (cost probe)
+            if (tot == 0x7FFFFFFFu) W.q[0] = (uint16_t)mask;
+        } else if (tail - head + tot <= W.fifo_cap) {  // uniform: the whole iteration fits
             uint32_t pos = tail + incl - cnt;
             while (mask) {
                 const uint32_t e = __builtin_ctz(mask);
@@ -250,6 +275,7 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
                 if (tail - head >= 64) resolve_round(64u, gb);
             }
         }
+        if constexpr ((V & 8) != 0) head = tail;  // variant: candidates dropped (cost probe)
         while (tail - head >= 64) resolve_round(64u, gb);
     }
     while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head), gb - 64);
@@ -263,20 +289,29 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
         __builtin_amdgcn_wave_barrier();
         return at;
     }
+    if constexpr (GT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (uint32_t j = lane; j < k; j += 64) {
-        const IdxT wi = tab[j];
-        o[j] = wi ? keys[off + (int64_t)wi] : ((int64_t)j < len ? keys[off + j] : (KeyT)0);
+        IdxT wi;
+        if constexpr (GT) wi = __hip_atomic_exchange(&tab[j], (IdxT)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else wi = tab[j];
+        if constexpr ((V & 1) != 0)  // variant: no winner-key gather (cost probe)
+            o[j] = (KeyT)wi;
+        else
+            o[j] = wi ? keys[off + (int64_t)wi] : ((int64_t)j < len ? keys[off + j] : (KeyT)0);
     }
     __builtin_amdgcn_wave_barrier();
     return -1;
 }
 
-template <typename KeyT>
+// V: development variants for tools/micro_k2.hip (0 = the product kernel).  GT: winner tables in
+// global scratch `gtab` (k * 8 bytes per wave of the grid, all zero at launch; see k2_stream)
+template <typename KeyT, int V = 0, bool GT = false>
 __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restrict__ keys,
                                                             const int64_t* __restrict__ offsets, int64_t S,
                                                             uint32_t k, uint32_t k0, uint32_t k1, uint64_t stream_base,
                                                             KeyT* __restrict__ out, int64_t* __restrict__ counts,
-                                                            uint32_t fifo_cap = kQCap) {
+                                                            uint32_t fifo_cap = qcap_of(V),
+                                                            unsigned long long* __restrict__ gtab = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     uint16_t* lut = (uint16_t*)lds;
     const uint64_t dense_lim = 256ull * k;
@@ -295,12 +330,13 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
     // (scalar loads, counted by lgkmcnt -- never waited for together with the deferred key gather)
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     // per wave: stash [kRing][64] x 16 B | FIFO kQCap x u16 | last-writer table k x (u32 | u64)
-    constexpr size_t qbytes = kQueueBytes, sbytes = kStashBytes;
-    const size_t tbytes = (size_t)k * 8;
+    constexpr size_t qbytes = qcap_of(V) * 2, sbytes = ring_of(V) * 64 * 16;
+    const size_t tbytes = GT ? 0 : (size_t)k * 8;
     unsigned char* base = lds + kLutBytes + (size_t)wave * (sbytes + qbytes + tbytes);
     void* tab = base + sbytes + qbytes;
+    if constexpr (GT) tab = gtab + ((size_t)blockIdx.x * kWaves + wave) * k;
     const Wave W{(u32x4*)base, (uint16_t*)(base + sbytes), tab, lut, lane, k,
-                 k0, k1, dense_lim, std::min<uint32_t>(std::max<uint32_t>(fifo_cap, 128u), kQCap)};
+                 k0, k1, dense_lim, std::min<uint32_t>(std::max<uint32_t>(fifo_cap, 128u), qcap_of(V))};
     const int64_t wave_stride = (int64_t)gridDim.x * kWaves;
     int64_t s = (int64_t)blockIdx.x * kWaves + wave;
     int64_t off = 0, end = 0;
@@ -308,7 +344,7 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
         off = offsets[s];
         end = offsets[s + 1];
     }
-    const bool defer = k <= 64;
+    const bool defer = !GT && k <= 64 && (V & 16) == 0 && (V & 1) == 0;
     KeyT* pend_o = nullptr;
     KeyT pend_v = 0;
     bool pend_ok = false;
@@ -326,9 +362,9 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
         const int64_t off_next = offsets[s_pf], end_next = offsets[s_pf + 1];
         const uint64_t stream = stream_base + (uint64_t)s;
         KeyT* o = out + s * (int64_t)k;
-        if (defer) {  // k <= 64: this stream's key is stored after the next stream's draws
-            const int64_t at = len < kSmallLen ? k2_stream<KeyT, true, true>(W, keys, off, len, stream, o)
-                                               : k2_stream<KeyT, false, true>(W, keys, off, len, stream, o);
+        if (!GT && defer) {  // k <= 64: this stream's key is stored after the next stream's draws
+            const int64_t at = len < kSmallLen ? k2_stream<KeyT, V, true, !GT>(W, keys, off, len, stream, o)
+                                               : k2_stream<KeyT, V, false, !GT>(W, keys, off, len, stream, o);
             // the previous stream's key (loaded a whole stream ago) leaves its register before this
             // stream's load lands in it: no copy of a load in flight, so no s_waitcnt at the stream end
             if (pend_o && lane < k) pend_o[lane] = pend_ok ? pend_v : (KeyT)0;
@@ -336,9 +372,9 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
             pend_ok = at >= 0;  // else an empty slot: the load below reads a valid dummy word
             pend_v = *(pend_ok ? keys + off + at : (const KeyT*)offsets);
         } else if (len < kSmallLen) {
-            k2_stream<KeyT, true, false>(W, keys, off, len, stream, o);
+            k2_stream<KeyT, V, true, false, GT>(W, keys, off, len, stream, o);
         } else {
-            k2_stream<KeyT, false, false>(W, keys, off, len, stream, o);
+            k2_stream<KeyT, V, false, false, GT>(W, keys, off, len, stream, o);
         }
         if (lane == 0) counts[s] = len < (int64_t)k ? len : (int64_t)k;
         off = off_next;
@@ -347,187 +383,5 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
     if (pend_o && lane < k) pend_o[lane] = pend_ok ? pend_v : (KeyT)0;
 }
 
-// ---- large k: one WORKGROUP per stream ------------------------------------------------------------
-// Per wave, k2_segmented keeps a k-slot table in LDS: above k ~ 512 the tables cap a CU at one or two
-// workgroups (k = 4096: 150 KB, one wave per SIMD) and above k = 4416 they no longer fit at all --
-// round 4's global per-wave tables then paid global atomics and a 1 GiB zero fill per call (3.7 ms
-// for 4096 x 2^17 at k = 8192).  Here the NW waves of a workgroup share ONE stream and ONE table:
-// wave w takes the stream's 64-block iterations w, w + NW, w + 2 NW, ... (interleaved, so the
-// candidate-rich dense head is spread over the waves), each with its own stash ring and FIFO, and all
-// resolve into the workgroup's table -- in LDS while k * sizeof(TabT) fits beside the waves' rings,
-// else the workgroup's slice of a global scratch table that stays zero between streams (the gather
-// takes every entry back with an atomic exchange).  TabT = u32 when every stream index fits 32 bits.
-constexpr int kWavesWG = 8;
-constexpr uint32_t kWGMinK = 512;  // smaller k keep one wave per stream (C3: k = 64)
-
-__host__ __device__ inline size_t lds_bytes_wg(uint32_t k, size_t tab_entry, bool GT) {
-    return kLutBytes + (size_t)kWavesWG * (kStashBytes + kQueueBytes) + (GT ? 0 : (size_t)k * tab_entry);
-}
-
-template <typename TabT, bool SMALL, bool GT>
-__device__ __forceinline__ void k2_part(const Wave& W, TabT* tab, int64_t len, uint64_t stream, uint32_t wave) {
-    using IdxT = typename std::conditional<SMALL, uint32_t, uint64_t>::type;
-    constexpr uint32_t QC = kQCap, RG = kRing;
-    constexpr uint32_t STEP = 64u * kWavesWG;  // blocks between this wave's iterations
-    const uint32_t lane = W.lane, k = W.k;
-    const uint32_t s0 = (uint32_t)stream, s1 = (uint32_t)(stream >> 32);
-    const DrawKey dk{W.k0, W.k1, s0, s1};
-    const IdxT n_groups = (IdxT)(((uint64_t)len + 15) >> 4);
-    uint32_t head = 0, tail = 0;
-    IdxT gb = (IdxT)(((k >> 4) & ~63u) + 64u * wave);
-    uint32_t ring = 0;
-    IdxT slot_gb[RG] = {};  // first block of the iteration each ring slot holds (wave-uniform)
-
-    auto resolve_round = [&](uint32_t nvalid) {
-        __builtin_amdgcn_wave_barrier();
-        const bool valid = lane < nvalid;
-        const uint32_t ent = valid ? W.q[(head + lane) & (QC - 1)] : 0u;
-        const uint32_t e = ent & 15u, r = ent >> 10;
-        const u32x4 w = W.stash[ent >> 4];
-        IdxT g0 = slot_gb[0];
-#pragma unroll
-        for (uint32_t q = 1; q < RG; ++q) g0 = r == q ? slot_gb[q] : g0;
-        const IdxT i = ((g0 + (IdxT)((ent >> 4) & 63u)) << 4) + (IdxT)e;
-        const uint32_t b = level0_byte(w, e);
-        const IdxT g1 = i >> 1;
-        u32x4 w1;
-        if constexpr (SMALL) w1 = philox4x32_10_uniform_hi((uint32_t)g1, kDomainLevel1, s0, s1, W.k0, W.k1);
-        else w1 = philox4x32_10((uint32_t)g1, (uint32_t)((uint64_t)g1 >> 32) | kDomainLevel1, s0, s1, W.k0, W.k1);
-        asm volatile("" : "+v"(w1.x), "+v"(w1.y), "+v"(w1.z), "+v"(w1.w));
-        const bool odd = (i & 1) != 0;
-        const uint64_t j = draw_j(b, odd ? w1.z : w1.x, odd ? w1.w : w1.y, (uint64_t)i + 1, SMALL);
-        if (valid && j < k) atomicMax(&tab[(uint32_t)j], (TabT)i);
-        head += nvalid;
-        __builtin_amdgcn_wave_barrier();
-    };
-
-    // the dense head [k, hend) by index pairs, as k2_stream (each wave takes its iterations' share)
-    uint64_t hx = 4ull * k;
-    if (hx - k >= 128) hx = k + ((hx - k) & ~(uint64_t)127);
-    const IdxT hend = (IdxT)std::min<uint64_t>((uint64_t)len, hx);
-    const IdxT flo = std::max<IdxT>((IdxT)k, hend);
-    for (; gb < n_groups; gb += STEP, ring = (ring + 1) & (RG - 1)) {
-        if (tail != head && ((uint32_t)__builtin_amdgcn_readfirstlane((int)W.q[head & (QC - 1)]) >> 10) == ring) {
-            while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head));
-        }
-        slot_gb[0] = ring == 0 ? gb : slot_gb[0];
-#pragma unroll
-        for (uint32_t q = 1; q < RG; ++q) slot_gb[q] = ring == q ? gb : slot_gb[q];
-        const IdxT g = gb + lane;
-        const bool valid = g < n_groups;
-        u32x4 w;
-        if constexpr (SMALL) w = philox4x32_10_uniform_hi((uint32_t)g, 0u, s0, s1, W.k0, W.k1);
-        else w = level0(dk, (uint64_t)g);
-        const uint64_t i0 = (uint64_t)g << 4;
-        const uint32_t T = g < kLut ? (uint32_t)W.lut[(uint32_t)g] : block_threshold(i0, W.dense_lim);
-        const uint32_t Tmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)T);
-        uint32_t mask = valid ? (Tmax <= 16u ? mask_for_small(w, T) : mask_for(w, T)) : 0u;
-        const bool clip = ((uint64_t)gb << 4) < (uint64_t)flo || (((uint64_t)gb + 64) << 4) > (uint64_t)len;
-        if (clip) mask &= clip16(i0, (uint64_t)flo, (uint64_t)len);
-        W.stash[ring * 64 + lane] = w;
-        if (((uint64_t)gb << 4) < (uint64_t)hend) {  // this iteration holds head indices (uniform)
-            __builtin_amdgcn_wave_barrier();
-            const IdxT ia = std::max<IdxT>((IdxT)k & ~(IdxT)1, gb << 4);
-            const IdxT ib = std::min<IdxT>(hend, (gb + 64) << 4);
-            for (IdxT p0 = ia; p0 < ib; p0 += 128) {
-                const IdxT i = p0 + 2 * lane;  // even
-                const u32x4 wl = W.stash[ring * 64 + (uint32_t)((i >> 4) - gb)];
-                uint32_t b0, b1;
-                level0_byte_pair(wl, (uint32_t)i & 15u, b0, b1);
-                const IdxT g1 = i >> 1;
-                u32x4 w1;
-                if constexpr (SMALL) w1 = philox4x32_10_uniform_hi((uint32_t)g1, kDomainLevel1, s0, s1, W.k0, W.k1);
-                else w1 = philox4x32_10((uint32_t)g1, (uint32_t)((uint64_t)g1 >> 32) | kDomainLevel1, s0, s1, W.k0, W.k1);
-                asm volatile("" : "+v"(w1.x), "+v"(w1.y), "+v"(w1.z), "+v"(w1.w));
-                const uint64_t j0 = draw_j(b0, w1.x, w1.y, (uint64_t)i + 1, SMALL);
-                const uint64_t j1 = draw_j(b1, w1.z, w1.w, (uint64_t)i + 2, SMALL);
-                if (i < ib && i >= (IdxT)k && j0 < k) atomicMax(&tab[(uint32_t)j0], (TabT)i);
-                if (i + 1 < ib && i + 1 >= (IdxT)k && j1 < k) atomicMax(&tab[(uint32_t)j1], (TabT)(i + 1));
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        const uint32_t cnt = (uint32_t)__popc(mask);
-        const uint32_t incl = wave_incl_scan(cnt);
-        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        const uint32_t tag = (ring << 10) | (lane << 4);
-        if (tail - head + tot <= W.fifo_cap) {
-            uint32_t pos = tail + incl - cnt;
-            while (mask) {
-                const uint32_t e = __builtin_ctz(mask);
-                mask &= mask - 1;
-                W.q[pos & (QC - 1)] = (uint16_t)(tag | e);
-                ++pos;
-            }
-            tail += tot;
-        } else {  // denser than the FIFO: one candidate per lane per round, resolved 64 at a time
-            for (;;) {
-                const bool has = mask != 0;
-                const unsigned long long bal = __builtin_amdgcn_ballot_w64(has);
-                if (!bal) break;
-                if (has) {
-                    const uint32_t e = __builtin_ctz(mask);
-                    mask &= mask - 1;
-                    const uint32_t pos = tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    W.q[pos & (QC - 1)] = (uint16_t)(tag | e);
-                }
-                tail += (uint32_t)__popcll(bal);
-                if (tail - head >= 64) resolve_round(64u);
-            }
-        }
-        while (tail - head >= 64) resolve_round(64u);
-    }
-    while (tail != head) resolve_round(std::min<uint32_t>(64u, tail - head));
-    __builtin_amdgcn_wave_barrier();
-}
-
-template <typename KeyT, typename TabT, bool GT>
-__global__ __launch_bounds__(64 * kWavesWG) void k2_segmented_wg(const KeyT* __restrict__ keys,
-                                                                 const int64_t* __restrict__ offsets, int64_t S,
-                                                                 uint32_t k, uint32_t k0, uint32_t k1,
-                                                                 uint64_t stream_base, KeyT* __restrict__ out,
-                                                                 int64_t* __restrict__ counts, uint32_t fifo_cap,
-                                                                 TabT* __restrict__ gtab) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    uint16_t* lut = (uint16_t*)lds;
-    const uint64_t dense_lim = 256ull * k;
-    for (uint32_t g = threadIdx.x; g < kLut; g += blockDim.x) {
-        const uint64_t i0 = (uint64_t)g << 4;
-        uint32_t T;
-        if (i0 + 1 >= dense_lim) T = 0;
-        else if (dense_lim + i0 <= 0xFFFFFFFFull) T = std::min<uint32_t>(256u, (uint32_t)(dense_lim + i0) / (uint32_t)(i0 + 1));
-        else T = block_threshold(i0, dense_lim);
-        lut[g] = (uint16_t)T;
-    }
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-    unsigned char* base = lds + kLutBytes + (size_t)wave * (kStashBytes + kQueueBytes);
-    TabT* tab = GT ? gtab + (size_t)blockIdx.x * k
-                   : (TabT*)(lds + kLutBytes + (size_t)kWavesWG * (kStashBytes + kQueueBytes));
-    const Wave W{(u32x4*)base, (uint16_t*)(base + kStashBytes), nullptr, lut, lane, k,
-                 k0, k1, dense_lim, std::min<uint32_t>(std::max<uint32_t>(fifo_cap, 128u), kQCap)};
-    const uint32_t nthr = 64u * kWavesWG;
-    for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
-        const int64_t off = offsets[s], len = offsets[s + 1] - off;
-        if constexpr (!GT)
-            for (uint32_t j = threadIdx.x; j < k; j += nthr) tab[j] = 0;
-        __syncthreads();  // the table is zero (GT: the previous stream's gather left it so)
-        const uint64_t stream = stream_base + (uint64_t)s;
-        if (len < kSmallLen) k2_part<TabT, true, GT>(W, tab, len, stream, wave);
-        else k2_part<TabT, false, GT>(W, tab, len, stream, wave);
-        if constexpr (GT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's table atomics
-        __syncthreads();
-        if constexpr (GT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every wave's, before the gather
-        KeyT* o = out + s * (int64_t)k;
-        for (uint32_t j = threadIdx.x; j < k; j += nthr) {
-            TabT wi;
-            if constexpr (GT) wi = __hip_atomic_exchange(&tab[j], (TabT)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else wi = tab[j];
-            o[j] = wi ? keys[off + (int64_t)wi] : ((int64_t)j < len ? keys[off + j] : (KeyT)0);
-        }
-        if (threadIdx.x == 0) counts[s] = len < (int64_t)k ? len : (int64_t)k;
-        __syncthreads();  // the gather has read the table before the next stream zeroes it
-    }
-}
-
-}  // namespace k2
+}  // namespace k2dev
 }  // namespace rsv

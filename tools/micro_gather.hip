@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <vector>
@@ -52,6 +53,33 @@ __global__ __launch_bounds__(256) void gather(const int64_t* __restrict__ keys, 
     }
 }
 
+// The byte basis of a random 8-B gather (does a lone 8-B load move a 64-B half-line or
+// the whole 128-B line?).  Every wave loads 64 words of its stream at KNOWN line positions:
+//   LINE 0: 64 distinct 128-B lines, word 0 of each                    -> 64 lines, 64 half-lines
+//   LINE 1: 32 distinct lines, words 0 and 8 (both 64-B halves)         -> 32 lines, 64 half-lines
+//   LINE 2: 32 distinct lines, words 0 and 1 (the same 64-B half twice) -> 32 lines, 32 half-lines
+// 128-B fetches: LINE 1 costs what LINE 2 costs (and half of LINE 0); 64-B fetches: LINE 1 costs
+// what LINE 0 costs.  Read with rocprofv3 --pmc TCC_EA0_RDREQ_sum (requests) and kernel time.
+template <int LINE>
+__global__ __launch_bounds__(256) void line_probe(const int64_t* __restrict__ keys, int64_t S, int L,
+                                                  int64_t* __restrict__ out, uint64_t salt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wstride = (int64_t)gridDim.x * 4;
+    const uint32_t lines = (uint32_t)L / 16;  // 128-B lines per stream (256 at L = 4096)
+    for (int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); s < S; s += wstride) {
+        const uint32_t base = (uint32_t)(mix((uint64_t)s ^ salt) % lines);
+        uint32_t line, word;
+        if (LINE == 0) {
+            line = (base + 4u * lane) % lines;  // 64 distinct lines (step 4 of 256)
+            word = 0;
+        } else {
+            line = (base + 8u * (lane >> 1)) % lines;  // 32 distinct lines, two loads each
+            word = LINE == 1 ? 8u * (lane & 1) : (lane & 1);
+        }
+        out[s * 64 + lane] = keys[s * L + line * 16 + word];
+    }
+}
+
 int main() {
     const int64_t S = 1 << 20, L = 4096, n = S * L;
     int64_t *keys, *out;
@@ -81,10 +109,17 @@ int main() {
                name, grid, ms, ts[0], ms * 1e-3 * 6.3e12 / (double)(S * 64));
         return 0;
     };
-    for (unsigned grid : {4096u, 16384u, 262144u}) {
-        if (run(gather<0>, "gather", grid)) return 1;
-        if (run(gather<2>, "gather sorted", grid)) return 1;
-        if (run(gather<1>, "store only", grid)) return 1;
+    const char* only = getenv("MICRO_GATHER_ONLY");  // "lines": the byte-basis probes alone (PMC runs)
+    if (!(only && only[0] == 'l'))
+        for (unsigned grid : {4096u, 16384u, 262144u}) {
+            if (run(gather<0>, "gather", grid)) return 1;
+            if (run(gather<2>, "gather sorted", grid)) return 1;
+            if (run(gather<1>, "store only", grid)) return 1;
+        }
+    for (int rep = 0; rep < 2; ++rep) {
+        if (run(line_probe<0>, "lines: 64 distinct 128-B lines, word 0", 16384u)) return 1;
+        if (run(line_probe<1>, "lines: 32 lines x both 64-B halves", 16384u)) return 1;
+        if (run(line_probe<2>, "lines: 32 lines x one 64-B half twice", 16384u)) return 1;
     }
     return 0;
 }

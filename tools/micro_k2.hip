@@ -13,7 +13,8 @@
 #include <algorithm>
 #include <vector>
 
-#include "../reservoir_amd/csrc/rsv_k2.h"
+#include "k2_dev_variants.h"  // the round-4 kernel + cost-probe variants
+namespace k2 = rsv::k2dev;
 
 using namespace rsv;
 
