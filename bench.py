@@ -4,7 +4,9 @@ A step is one full pass of the hot path over the batch: a fresh Sampler (Sampler
 and closed inside the step) samples the device-resident keys (K1 last-writer kernel + resolve),
 then result() brings the k-slot reservoir to the host.  Two steps are in flight (step t+1's
 sampling is queued on the stream before step t's result is read, so the host turnaround overlaps
-the GPU); the one-at-a-time figure is reported beside it ("serial"; --serial times that instead).  With N GPUs the stream is N x 1e9 elements
+the GPU), and each step's one-workgroup slot resolve + publication runs on a second stream after
+its K1 (rsv_set_resolve_stream), so step t+1's K1 does not queue behind it; the one-at-a-time figure
+is reported beside it ("serial"; --serial times that instead).  With N GPUs the stream is N x 1e9 elements
 split by index range (each rank seeks to its offset, weak scaling) and the per-rank reservoirs are
 combined with one all_gather + merge kernel inside the step.
 
@@ -21,9 +23,10 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
   cpu_baseline  -- the oracle's C restatement of the reference (Algorithm L / RandomValues) on the
                    host cores, median of 5 runs per leg (C2 headline leg on one core; C1, C3 on
                    all cores, C4 prefix)
-  secondary     -- (N = 1) the other configs of BASELINE.json: C3 segmented (with K2's VALU
-                   roofline), C4 distinct (identity; Long.hashCode in set and ordered order; the
-                   ordered replay branch), C2 on engine java_l (tools/bench_paths.py), C5
+  secondary     -- (N = 1) the other configs of BASELINE.json: C3 segmented (roofline on its
+                   binding bound, the winners' 128-B HBM lines, beside K2's VALU model), C4
+                   distinct (identity; Long.hashCode in set and ordered order; the ordered replay
+                   branch; 16-byte UUID keys), C2 on engine java_l (tools/bench_paths.py), C5
                    sustained elem/s at k = 1 Mi (tools/bench_c5)
   c4            -- (N > 1) C4 at its own definition: N x 5e8 keys split by rank (4e9 at N = 8),
                    distinct sampling + distributed.combine inside the timed step, both hashes, the
@@ -402,6 +405,13 @@ def main() -> None:
     # tensors waits on the host for the stream it runs on, which then serialises the steps -- the
     # 2-rank rehearsal ran 0.54 -> 1.05 ms per step with it.)
     comm = torch.cuda.Stream(device=dev) if world > 1 and backend == "nccl" else None
+    # RSV_BENCH_RESOLVE_STREAM=1: each step's slot resolve + result publication (a one-workgroup
+    # dispatch, ~5 us) on a second stream after its K1 (rsv_set_resolve_stream), so the next step's
+    # K1 need not queue behind it.  Off by default: measured slower (r05j, same box, A/B/A/B: 0.0915
+    # and 0.0919 ms per step without, 0.0939 and 0.0963 with; K1 86.8 -> 89-90 us -- the dispatch
+    # running beside K1 costs K1 more than the queueing it saves)
+    rstream = (torch.cuda.Stream(device=dev).cuda_stream
+               if os.environ.get("RSV_BENCH_RESOLVE_STREAM", "0") == "1" else None)
 
     L = _native.load()
 
@@ -410,6 +420,8 @@ def main() -> None:
         # caller's stream sample_all and the combine are stream-ordered: nothing here waits
         s = Sampler(k, seed=args.seed, stream_id=args.stream_id, device=local)()
         s.set_stream(stream)
+        if rstream is not None:
+            s.set_resolve_stream(rstream)
         s.seek(offset)
         s.sample_all(keys)
         if comm is not None:
@@ -555,6 +567,7 @@ def main() -> None:
             "roofline": roof,
             "ranks_seen": dist.get_world_size() if world > 1 else 1,
             "steps_in_flight": depth,
+            "resolve_stream": rstream is not None,
             "serial": {"steps": serial_steps, "ms_per_step": round(elapsed_serial / serial_steps * 1e3, 4),
                        "value": round(n * world * serial_steps / elapsed_serial / 1e9, 3),
                        "what": "the same step run one at a time (result read and sampler closed before the "

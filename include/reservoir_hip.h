@@ -192,6 +192,14 @@ int64_t    rsv_count(const rsv_sampler* s);   /* elements sampled so far (S:203)
  * on the previous stream before the new stream's next work (an event wait, no host wait). */
 rsv_status rsv_set_stream(rsv_sampler* s, void* hip_stream);
 void*      rsv_get_stream(const rsv_sampler* s);
+/* Pipelining several samplers on one stream (ELEMENTS, batches whose K1 runs as its own dispatch:
+ * > 2^27 draws): each batch's slot resolve and result publication (a one-workgroup dispatch of a few
+ * microseconds) run on `hip_stream` instead, after the batch's K1 (an event), so the NEXT sampler's
+ * K1 on the handle's stream does not wait behind them.  The handle's own later work waits for them
+ * (an event), and rsv_result waits for the publication as always.  The keys of such a batch are read
+ * on `hip_stream`: the caller keeps them unchanged until rsv_result (or rsv_synchronize) returns.
+ * NULL = resolve on the handle's stream (the default). */
+rsv_status rsv_set_resolve_stream(rsv_sampler* s, void* hip_stream);
 rsv_status rsv_synchronize(rsv_sampler* s);
 
 /* Kernel timing: while enabled, HIP events bracket every launch of the handle's hot kernel (K1

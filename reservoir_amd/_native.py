@@ -26,7 +26,8 @@ EXPORTED_SYMBOLS = (
     "rsv_abi_version", "rsv_last_error", "rsv_status_string", "rsv_config_init", "rsv_create",
     "rsv_destroy", "rsv_sample", "rsv_sample_batch", "rsv_result", "rsv_result_device", "rsv_result_take",
     "rsv_host_release",
-    "rsv_is_open", "rsv_count", "rsv_set_stream", "rsv_get_stream", "rsv_synchronize", "rsv_seek",
+    "rsv_is_open", "rsv_count", "rsv_set_stream", "rsv_get_stream", "rsv_set_resolve_stream", "rsv_synchronize",
+    "rsv_seek",
     "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
     "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
     "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read", "rsv_stage_acquire",
@@ -119,6 +120,7 @@ def load():
     L.rsv_set_stream.argtypes = [vp, vp]
     L.rsv_get_stream.argtypes = [vp]
     L.rsv_get_stream.restype = vp
+    L.rsv_set_resolve_stream.argtypes = [vp, vp]
     L.rsv_synchronize.argtypes = [vp]
     L.rsv_seek.argtypes = [vp, i64]
     L.rsv_export_state.argtypes = [vp, vp, vp, vp, C.POINTER(i64)]
@@ -142,7 +144,8 @@ def load():
     L.rsv_abort_indexed.argtypes = [vp]
     L.rsv_retain_log.argtypes = [vp, i32]
     for name in ("rsv_config_init", "rsv_create", "rsv_sample", "rsv_sample_batch", "rsv_result",
-                 "rsv_result_device", "rsv_result_take", "rsv_set_stream", "rsv_synchronize", "rsv_seek",
+                 "rsv_result_device", "rsv_result_take", "rsv_set_stream", "rsv_set_resolve_stream",
+                 "rsv_synchronize", "rsv_seek",
                  "rsv_export_state", "rsv_merge_state", "rsv_sample_segmented", "rsv_replay_events",
                  "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
                  "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read", "rsv_stage_acquire",

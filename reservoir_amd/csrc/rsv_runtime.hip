@@ -164,6 +164,11 @@ struct rsv_sampler {
     bool pub_valid = false;
     KernelTimer timer;
     hipEvent_t handover = nullptr;  // rsv_set_stream's event (kept until destroy: see there)
+    // rsv_set_resolve_stream: each batch's resolve + publication on this caller stream, forked from
+    // `stream` after K1 (side_fork) and joined back (side_join) before the handle's next device work
+    hipStream_t rstream = nullptr;
+    hipEvent_t side_fork = nullptr, side_join = nullptr;
+    bool side_pending = false;
     // device work enqueued on `stream` by this handle, in groups, vs the groups known complete
     // (a stream synchronize, or the host flag of a publication that was the last group)
     uint64_t ops = 0, ops_done = 0, pub_ops = 0;
@@ -180,8 +185,18 @@ KernelTimer& global_timer() {
 }
 
 // a new group of device work on the handle's stream / everything enqueued so far is complete
-inline void touch(rsv_sampler* s) { ++s->ops; }
+// the forked resolve (rsv_set_resolve_stream) ordered before the handle's next work on its stream
+inline void join_side(rsv_sampler* s) {
+    if (!s->side_pending) return;
+    (void)hipStreamWaitEvent(s->stream, s->side_join, 0);
+    s->side_pending = false;
+}
+inline void touch(rsv_sampler* s) {
+    join_side(s);
+    ++s->ops;
+}
 inline hipError_t sync_stream(rsv_sampler* s) {
+    join_side(s);
     hipError_t e = hipStreamSynchronize(s->stream);
     if (e == hipSuccess) s->ops_done = s->ops;
     return e;
@@ -334,21 +349,23 @@ constexpr uint32_t kFusedPublishMaxK = 8192;  // resolve_publish: one workgroup,
 // The batch's resolve: fill phase + winners into the slots; for reservoirs of <= 8192 keys it
 // also writes the first min(count, k) keys into the coherent result buffer and publishes
 // generation ++result_gen there (one dispatch instead of resolve now + publish at result()).
-rsv_status resolve_batch(rsv_sampler* s, const void* keys, int64_t base, int64_t n, bool fresh) {
+rsv_status resolve_batch(rsv_sampler* s, const void* keys, int64_t base, int64_t n, bool fresh,
+                         hipStream_t rst = nullptr) {
+    if (!rst) rst = s->stream;
     if (s->k <= kFusedPublishMaxK) {
         if (rsv_status st = ensure_result_buffer(s)) return st;
         if (s->result_publish) {
             const uint32_t gen = ++s->result_gen;
             const int64_t m = std::min<int64_t>(base + n, (int64_t)s->k);
             RSV_HIP_TRY(launch_resolve_publish(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx,
-                                               fresh, m, s->result_dev, s->result_flag_dev, gen, s->stream));
+                                               fresh, m, s->result_dev, s->result_flag_dev, gen, rst));
             s->pub_ops = s->ops;  // the last work of this group
             s->pub_gen = gen;
             s->pub_valid = true;
             return RSV_OK;
         }
     }
-    RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, fresh, s->stream));
+    RSV_HIP_TRY(launch_resolve(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx, fresh, rst));
     s->pub_valid = false;
     return RSV_OK;
 }
@@ -434,7 +451,17 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
             const bool pm = prof_begin(s, s->stream);
             RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
             prof_end(s, s->stream, pm);
-            if (rsv_status st = resolve_batch(s, keys, base, n, fresh)) return st;
+            if (s->rstream) {  // the resolve + publication forked onto the resolve stream (see there)
+                if (!s->side_fork) RSV_HIP_TRY(pool_event(&s->side_fork, hipEventDisableTiming));
+                if (!s->side_join) RSV_HIP_TRY(pool_event(&s->side_join, hipEventDisableTiming));
+                RSV_HIP_TRY(hipEventRecord(s->side_fork, s->stream));
+                RSV_HIP_TRY(hipStreamWaitEvent(s->rstream, s->side_fork, 0));
+                if (rsv_status st = resolve_batch(s, keys, base, n, fresh, s->rstream)) return st;
+                RSV_HIP_TRY(hipEventRecord(s->side_join, s->rstream));
+                s->side_pending = true;
+            } else if (rsv_status st = resolve_batch(s, keys, base, n, fresh)) {
+                return st;
+            }
         }
     }
     if (s->cfg.kind == RSV_KIND_ELEMENTS) s->slots_init = s->win_zero = true;
@@ -498,6 +525,8 @@ void free_all(rsv_sampler* s) {
     // the handover record has completed: the stream waiting on it was synchronized, or its
     // publication seen, before this
     if (s->handover) pool_release_event(s->device, s->handover, hipEventDisableTiming);
+    if (s->side_fork) pool_release_event(s->device, s->side_fork, hipEventDisableTiming);
+    if (s->side_join) pool_release_event(s->device, s->side_join, hipEventDisableTiming);
     if (s->distinct) distinct_destroy(s->distinct);
     if (s->stream && s->own_stream) pool_release_stream(s->device, s->stream);
 }
@@ -640,7 +669,14 @@ void rsv_destroy(rsv_sampler* s) {
     // the buffers go back to the pool: nothing this handle enqueued may still touch them.  On a
     // caller stream whose last group of work was a publication the host has seen, that holds
     // already (the flag store is the last memory operation of that group).
-    if (s->stream && (s->own_stream || s->ops != s->ops_done)) (void)hipStreamSynchronize(s->stream);
+    if (s->stream && (s->own_stream || s->ops != s->ops_done)) {
+        join_side(s);
+        (void)hipStreamSynchronize(s->stream);
+    } else if (s->side_pending && s->rstream) {
+        // the publication was seen (its flag store is the resolve's last memory operation): only the
+        // events and buffers remain, and they outlive the queued work by the join below
+        (void)hipEventSynchronize(s->side_join);
+    }
     free_all(s);
     delete s;
 }
@@ -967,6 +1003,10 @@ int64_t rsv_count(const rsv_sampler* s) { return s ? s->count + s->stage_n : 0; 
 rsv_status rsv_set_stream(rsv_sampler* s, void* hip_stream) {
     if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
     DeviceGuard g(s->device);
+    if (s->side_pending) {  // the hand-over covers the forked resolve too
+        join_side(s);
+        ++s->ops;
+    }
     if (s->ops != s->ops_done && (hipStream_t)hip_stream != s->stream) {
         // stream-ordered hand-over, no host wait: the new stream waits for the work queued so far
         // (e.g. a combine moved to a communication stream while the next batch samples on the
@@ -983,6 +1023,18 @@ rsv_status rsv_set_stream(rsv_sampler* s, void* hip_stream) {
 }
 
 void* rsv_get_stream(const rsv_sampler* s) { return s ? (void*)s->stream : nullptr; }
+
+rsv_status rsv_set_resolve_stream(rsv_sampler* s, void* hip_stream) {
+    if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
+    if (s->cfg.kind != RSV_KIND_ELEMENTS) return fail(RSV_E_UNSUPPORTED, "rsv_set_resolve_stream: ELEMENTS samplers only");
+    DeviceGuard g(s->device);
+    if (s->side_pending) {
+        join_side(s);
+        ++s->ops;
+    }
+    s->rstream = (hipStream_t)hip_stream;
+    return RSV_OK;
+}
 
 rsv_status rsv_synchronize(rsv_sampler* s) {
     if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");

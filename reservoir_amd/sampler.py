@@ -231,6 +231,13 @@ class GpuSampler:
         N.check(self._L.rsv_set_stream(self._h, C.c_void_p(hip_stream)))
         self._stream = int(hip_stream)
 
+    def set_resolve_stream(self, hip_stream: int | None) -> None:
+        """Pipelining (element samplers, batches > 2^27 keys): the slot resolve + result publication
+        run on ``hip_stream`` after the batch's K1, so the next sampler's K1 on this stream does not
+        queue behind them (include/reservoir_hip.h rsv_set_resolve_stream).  The batch's keys must
+        stay unchanged until result() returns."""
+        N.check(self._L.rsv_set_resolve_stream(self._h, C.c_void_p(hip_stream or 0)))
+
     def synchronize(self) -> None:
         N.check(self._L.rsv_synchronize(self._h))
 

@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import ctypes as C
 import json
+import math
 import os
 import sys
 import time
@@ -83,16 +84,43 @@ def c3(dev):
     rows = keys.view(S, L)
     t_g = timed(lambda: torch.gather(rows, 1, idx), reps=5)
     del idx
+    # The binding bound: HBM lines.  A lone 8-B load moves its whole 128-B line (tools/micro_gather
+    # line probes, profiles/r05/gather_line_probe_time.jsonl: both 64-B halves of 32 lines cost what
+    # one half twice costs), so a stream's winners cost 128 B per DISTINCT line: 64 uniform positions
+    # without replacement in 256 lines touch 256 (1 - C(4080, 64) / C(4096, 64)) ~ 56.6 of them.
+    lines = 256.0 * (1.0 - math.exp(sum(math.log((L - 16 - q) / (L - q)) for q in range(k))))
+    line_bytes = S * lines * 128
+    traffic = _pmc_traffic("c3")
+    hbm = {"bound": "hbm", "achieved": round(line_bytes / t / 1e9, 1), "peak": HBM, "unit": "GB/s",
+           "frac": round(line_bytes / t / 1e9 / HBM, 4), "traffic": traffic,
+           "kernel": "k2_segmented",
+           "bytes_per_launch": round(line_bytes), "lines_per_stream": round(lines, 2),
+           "note": "algorithmic bytes = the winners' distinct 128-B lines (the fetch granule of a random 8-B "
+                   "load); traffic = HBM bytes per launch from PMC (profiles/r05)"}
     return {"config": "C3 segmented 2^20 x 4096, k=64", "elements": n, "seconds": t,
             "Gelem_s": n / t / 1e9,
-            "roofline": R.valu_roofline(l0, l1, t, "k2_segmented",
-                                        note="launch time = median of 5 (HIP events); VALU: the Philox draws "
-                                             "alone; the binding floor is the winner gather below"),
+            "roofline": hbm,
+            "roofline_valu": R.valu_roofline(l0, l1, t, "k2_segmented",
+                                             note="launch time = median of 5 (HIP events); VALU: the Philox draws "
+                                                  "alone (hidden under the line gather: see roofline)"),
             "gather_floor": {"seconds": t_g, "frac": t_g / t,
                              "what": "torch.gather of 64 random positions per 4096-key row (2^26 random "
                                      "8-B loads, ~57 distinct 128-B lines per row): the memory work K2 "
                                      "cannot avoid; frac = floor / K2 launch"},
             "winner_gather_bytes": S * k * 8}
+
+
+def _pmc_traffic(name):
+    """HBM bytes per launch of a kernel from the committed PMC summary (profiles/r05, else r04), or None."""
+    for r in ("r05", "r04"):
+        try:
+            d = json.load(open(os.path.join(ROOT, "profiles", r, "pmc_summary.json")))
+            v = d.get(name, {}).get("hbm_bytes_per_launch")
+            if v:
+                return v
+        except (OSError, ValueError):
+            pass
+    return None
 
 
 def c3_large_k(dev):

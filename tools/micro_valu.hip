@@ -3,7 +3,7 @@
 //
 // Every wave of a full chip (256 CUs x 32 waves, i.e. 8 waves on each SIMD) issues a long run of
 // independent instructions of one kind; s_memtime (shader-clock ticks, MI355X_MICROARCH.md) around
-// the run gives cycles per wave, and
+// the run gives cycles per wave (s_memrealtime, 100 MHz, beside it gives the clock the run had), and
 //     cycles per wave-instruction on one SIMD = median wave cycles / (instructions per wave x 8).
 // The result is clock-independent (DVFS moves wall time, not these cycles).  bench.py's VALU
 // roofline prices a Philox call with these costs (profiles/r02/valu_costs.json).
@@ -50,6 +50,11 @@ __device__ __forceinline__ void burst(uint32_t (&d)[8], uint64_t (&q)[8], uint32
         asm volatile("v_mul_lo_u32 %0, %1, %2" : "=v"(d[i]) : "v"(a), "s"(s));                              \
     } else if constexpr (OP == 5) {                                                                         \
         asm volatile("v_add_u32 %0, %1, %2" : "=v"(d[i]) : "s"(s), "v"(a));                                 \
+    } else if constexpr (OP == 6) {                                                                         \
+        asm volatile("v_fma_f32 %0, %1, %2, %3" : "=v"(d[i]) : "v"(a), "v"(b), "s"(s));                     \
+    } else if constexpr (OP == 7) {                                                                         \
+        const uint64_t ab = ((uint64_t)b << 32) | a;                                                        \
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(q[i]) : "v"(ab), "v"(ab), "v"(ab));               \
     }
     ONE(0) ONE(1) ONE(2) ONE(3) ONE(4) ONE(5) ONE(6) ONE(7)
 #undef ONE
@@ -61,18 +66,22 @@ __global__ __launch_bounds__(256) void op_rate(uint64_t* cyc, uint32_t* sink, ui
     uint64_t q[8];
     const uint32_t a = threadIdx.x * 0x9E3779B9u, b = a ^ s;
     __builtin_amdgcn_s_barrier();
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < kIters; ++it) {
         burst<OP>(d, q, a + it, b, s);
         burst<OP>(d, q, a + it, b, s);
         burst<OP>(d, q, a + it, b, s);
         burst<OP>(d, q, a + it, b, s);
     }
-    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     uint32_t r = 0;
     for (int i = 0; i < 8; ++i) r ^= d[i] ^ (uint32_t)q[i];
     if (r == 0x1234567u) sink[0] = r;
-    if ((threadIdx.x & 63) == 0) cyc[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        cyc[2 * w] = t1 - t0;
+        cyc[2 * w + 1] = r1 - r0;
+    }
 }
 
 // K1's level-0 call (counter words 1..3 wave-uniform), two chains per lane as in K1
@@ -81,30 +90,38 @@ __global__ __launch_bounds__(256) void philox_rate(uint64_t* cyc, uint32_t* sink
     uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x, acc = 0;
     const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
     __builtin_amdgcn_s_barrier();
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < kIters; ++it, gl += 1u << 21) {
         const u32x4 w0 = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1);
         const u32x4 w1 = philox4x32_10_uniform_hi(gl + 64, ghi, dk.s0, dk.s1, dk.k0, dk.k1);
         acc ^= w0.x ^ w0.y ^ w0.z ^ w0.w ^ w1.x ^ w1.y ^ w1.z ^ w1.w;
     }
-    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if (acc == 0x1234567u) sink[0] = acc;
-    if ((threadIdx.x & 63) == 0) cyc[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        cyc[2 * w] = t1 - t0;
+        cyc[2 * w + 1] = r1 - r0;
+    }
 }
 
 // the full (non-uniform) Philox4x32-10 of the level-1 draws
 __global__ __launch_bounds__(256) void philox_full_rate(uint64_t* cyc, uint32_t* sink, uint32_t s) {
     uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x, acc = 0;
     __builtin_amdgcn_s_barrier();
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < kIters; ++it, gl += 1u << 21) {
         const u32x4 w0 = philox4x32_10(gl, gl ^ 0x80000000u, s, gl >> 7, 0xC0FFEEu, s);
         const u32x4 w1 = philox4x32_10(gl + 64, gl ^ 0x80000001u, s, gl >> 7, 0xC0FFEEu, s);
         acc ^= w0.x ^ w0.y ^ w0.z ^ w0.w ^ w1.x ^ w1.y ^ w1.z ^ w1.w;
     }
-    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if (acc == 0x1234567u) sink[0] = acc;
-    if ((threadIdx.x & 63) == 0) cyc[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        cyc[2 * w] = t1 - t0;
+        cyc[2 * w + 1] = r1 - r0;
+    }
 }
 
 int main() {
@@ -113,12 +130,12 @@ int main() {
     const int grid = cus * kBlocksPerCu, waves = grid * 4;
     uint64_t* cyc;
     uint32_t* sink;
-    CK(hipMalloc(&cyc, (size_t)waves * 8));
+    CK(hipMalloc(&cyc, (size_t)waves * 16));
     CK(hipMalloc(&sink, 64));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    std::vector<uint64_t> h(waves);
+    std::vector<uint64_t> h(2 * (size_t)waves);
     auto run = [&](auto kern, const char* name, double per_wave) -> int {
         for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, cyc, sink, 7u);
         CK(hipEventRecord(e0));
@@ -127,23 +144,33 @@ int main() {
         CK(hipEventSynchronize(e1));
         float ms = 0;
         CK(hipEventElapsedTime(&ms, e0, e1));
-        CK(hipMemcpy(h.data(), cyc, (size_t)waves * 8, hipMemcpyDeviceToHost));
-        std::vector<uint64_t> s = h;
+        CK(hipMemcpy(h.data(), cyc, (size_t)waves * 16, hipMemcpyDeviceToHost));
+        std::vector<uint64_t> s(waves), r(waves);
+        for (int w = 0; w < waves; ++w) s[w] = h[2 * w], r[w] = h[2 * w + 1];
         std::sort(s.begin(), s.end());
-        const double med = (double)s[s.size() / 2];
+        std::sort(r.begin(), r.end());
+        const double med = (double)s[s.size() / 2], rmed = (double)r[r.size() / 2];
+        const double ghz = med / rmed * 0.1;  // shader clock during the run (guide: memtime / memrealtime x 100 MHz)
         const double cpi = med / (per_wave * kWavesPerSimd);
         printf("{\"op\": \"%s\", \"cycles_per_wave_instr_per_simd\": %.3f, \"full_rate_slots\": %.3f, "
-               "\"median_wave_cycles\": %.0f, \"wall_ms\": %.4f, \"effective_GHz\": %.3f}\n",
-               name, cpi, cpi / 2.0, med, ms, med / (ms * 1e6));
+               "\"median_wave_cycles\": %.0f, \"wall_ms\": %.4f, \"clock_GHz\": %.3f, \"ns_per_wave_instr_per_simd\": %.3f}\n",
+               name, cpi, cpi / 2.0, med, ms, ghz, cpi / ghz);
         return 0;
     };
     const double burst_instr = 4.0 * 8 * kIters;
+    // the clock ramps under sustained load: ~1 s of back-to-back launches before the first row
+    for (int rep = 0; rep < 2000; ++rep) hipLaunchKernelGGL(op_rate<2>, dim3(grid), dim3(256), 0, 0, cyc, sink, 7u);
+    CK(hipDeviceSynchronize());
     if (run(op_rate<0>, "v_mad_u64_u32", burst_instr)) return 1;
     if (run(op_rate<1>, "v_bitop3_b32", burst_instr)) return 1;
     if (run(op_rate<2>, "v_xor_b32", burst_instr)) return 1;
     if (run(op_rate<3>, "v_mul_hi_u32", burst_instr)) return 1;
     if (run(op_rate<4>, "v_mul_lo_u32", burst_instr)) return 1;
     if (run(op_rate<5>, "v_add_u32", burst_instr)) return 1;
+    // the guide's fp32 FMA figure (2 cycles per wave64 instruction on a SIMD) against the 32-bit
+    // integer ops above: reconciles the 4-cycle issue model bench.py's VALU roofline prices with
+    if (run(op_rate<6>, "v_fma_f32", burst_instr)) return 1;
+    if (run(op_rate<7>, "v_pk_fma_f32", burst_instr)) return 1;
     if (run(philox_rate, "philox4x32_10_uniform_hi (per call)", 2.0 * kIters)) return 1;
     if (run(philox_full_rate, "philox4x32_10 (per call)", 2.0 * kIters)) return 1;
     return 0;
