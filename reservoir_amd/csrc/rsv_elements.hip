@@ -20,10 +20,10 @@ namespace {
 
 constexpr int kBlock = 256;
 
-// K1: grid-stride over level-0 blocks (16 indices each), two per lane per iteration; one bit per
-// such pair marks a zero byte, and every 12 iterations the marked pairs go through the wave's LDS
-// queue -- with their 32-bit zero-byte fold, so a sparse-region resolve needs no level-0 recompute
-// -- and the level-1 draws run with all 64 lanes busy (rsv_scan.h k1_body_p).  Hits (k ln(n/k) of
+// K1: grid-stride over level-0 blocks (16 indices each), two per lane per iteration; a pair with a
+// zero byte is appended at once to the wave's LDS queue -- with its 32-bit zero-byte fold, so a
+// sparse-region resolve needs no level-0 recompute -- and after every half window of 6 iterations
+// the level-1 draws run 64 at a time, all lanes busy (rsv_scan.h k1_body_q).  Hits (k ln(n/k) of
 // them) go straight to global atomicMax on the k-slot winner table: 14k atomics per 1e9 indices at k = 1024.
 constexpr int kK1Unroll = 2;  // level-0 blocks per lane per iteration (two Philox chains in flight)
 
@@ -32,16 +32,20 @@ constexpr int kK1Unroll = 2;  // level-0 blocks per lane per iteration (two Phil
 // 87.5-89 us at 3072, 3390 (3 windows), 4096, 6144, 7629 and 10172 (1 window)
 constexpr unsigned kK1Grid = 256 * 20;
 
-// per-wave LDS of k1_body_p: pair queue (< 64 waiting + one round of 64), the window's pair folds,
-// the per-candidate queue.  12 iterations per window: tools/micro_k1o (r03p) 87.5-88.3 us per 1e9
-// indices vs 87.6-89.5 for 10 and 16, and 88.8-89.3 for the per-block entries of k1_body_z.
+// per-wave LDS of k1_body_q: pair queue (< 64 waiting + half a window of appends), the per-
+// candidate queue.  12 iterations per window: tools/micro_k1o (r05k, 1e9 indices, grid 5086)
+// 83.1-83.6 us vs 83.4-83.8 for 8 and 84.7-84.8 for 16, and 84.9-85.8 for the round-4 body
+// (k1_body_p: window bits pushed in ballot rounds, tools/k1_dev_bodies.h), winners identical.
 constexpr int kK1Win = 12;
 struct K1Lds {
-    uint64_t q[kBlock / 64][128];
-    uint32_t wz[kBlock / 64][kK1Win * 64];
-    uint32_t tab[kBlock / 64][kK1Win];
+    uint64_t q[kBlock / 64][k1q_cap<kK1Win>()];
     uint64_t cq[kBlock / 64][kQueue];
 };
+
+// the launch-uniform conditions of k1_body_q's FAST resolve
+__device__ __forceinline__ bool k1_fast(uint64_t lo, uint64_t hi) {
+    return (lo >> 33) == ((hi - 1) >> 33) && hi <= (1ull << 40);
+}
 
 __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k, uint64_t lo,
                                                          uint64_t hi, uint64_t g_begin,
@@ -49,7 +53,8 @@ __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k,
                                                          unsigned long long* __restrict__ win) {
     __shared__ K1Lds L;
     const int w = threadIdx.x >> 6;
-    k1_body_p<kK1Win>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wz[w], L.tab[w], L.cq[w]);
+    if (k1_fast(lo, hi)) k1_body_q<kK1Win, true>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w]);
+    else k1_body_q<kK1Win, false>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w]);
 }
 
 // K1 + resolve_publish in one dispatch (single-launch batches, k <= kK1FusedMaxK): every
@@ -70,7 +75,8 @@ __global__ __launch_bounds__(kBlock) void k1_resolve_publish(DrawKey dk, uint32_
     __shared__ K1Lds L;
     __shared__ uint32_t last;
     const int w = threadIdx.x >> 6;
-    k1_body_p<kK1Win>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wz[w], L.tab[w], L.cq[w]);
+    if (k1_fast(lo, hi)) k1_body_q<kK1Win, true>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w]);
+    else k1_body_q<kK1Win, false>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w]);
     // This wave's winner atomics are performed once vmcnt drains: on gfx942/gfx950 a global atomic
     // without return still counts in vmcnt until the memory system acknowledges it (there is no
     // separate vscnt), and an agent-scope atomic is performed at the agent's coherence point (the

@@ -114,10 +114,6 @@ __device__ __forceinline__ void resolve_block(const DrawKey& dk, bool valid, uin
     enqueue_block(dk, w, i0, mask, cq, cqn, lane, k, hit);
 }
 
-#ifndef RSV_K1P_COUNT
-#define RSV_K1P_COUNT(i, v)  // development counters (tools/micro_k1o.hip)
-#endif
-
 // the 16-bit OR of a block's plane halves: bit e clear <=> b_e == 0 (one SDWA op for the fold; the
 // wait state after it keeps a reader right behind from the gfx950 SDWA hazard, see fold_pair)
 __device__ __forceinline__ uint32_t fold16(const u32x4& w) {
@@ -139,16 +135,6 @@ __device__ __forceinline__ u32x4 level1_b0_words(const DrawKey& dk, uint64_t i, 
     return philox4x32_10((uint32_t)g1, (uint32_t)(g1 >> 32) | kDomainLevel1, dk.s0, dk.s1, dk.k0, dk.k1);
 }
 
-// ---- K1 with pair entries (k1_body_p) ----------------------------------------------------------
-// As k1_body_z (round 3; now tools/k1_dev_bodies.h), but a lane's two blocks of an iteration (offsets o and o + 64) share one window bit
-// and one queue entry: the 32-bit fold z holds block o's 16-bit fold in its low half and block
-// o + 64's in its high half (bit e clear <=> byte e & 15 of block o + 64 (e >> 4) is zero), built
-// by two SDWA ops straight into the halves, and one compare marks the pair -- 4 VALU ops per block
-// beside the Philox instead of 5, and half the window stores.  An entry's zero bytes are resolved
-// one at a time as before.  A pair with a dense-region (or out-of-range-partner) half -- z half 0,
-// impossible for a real sparse block (2^-128) -- takes the recomputing resolve for both blocks.
-constexpr uint32_t kK1PWin = 10;  // iterations (pairs per lane) per window
-
 // z = fold16(a) | fold16(b) << 16.  The wait states are part of the block: on gfx950 a VALU op
 // reading a register right after an SDWA op wrote part of it reads the OLD value (tools/micro_k1o
 // fold_check: 21 % wrong without them, none with one s_nop 0 each).
@@ -164,11 +150,27 @@ __device__ __forceinline__ uint32_t fold_pair(const u32x4& a, const u32x4& b) {
     return z;
 }
 
-template <int W = kK1PWin>
-__device__ __forceinline__ void k1_body_p(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+// ---- K1 with direct appends (k1_body_q, round 5) -----------------------------------------------
+// k1_body_p marks a window's pairs in a per-lane bit mask and pushes them afterwards in ballot
+// rounds (one entry per lane per round: ~5 rounds of ~14 VALU per 12-iteration window, the max
+// over 64 lanes of a Binomial(12, 0.118)).  Here every iteration appends its marked pairs at once:
+// the compare's lane mask IS the ballot, so an append is two mbcnt + one address op under that
+// mask, and the window keeps no fold rows or offset table.  The entry carries the pair's Philox
+// counter word gt (the launch never crosses a 2^32-block boundary, so the block is ghi:gt) and its
+// fold.  The queue holds < 64 waiting entries + half a window of appends (k1q_cap): the rounds run
+// after each half window.  The steady append takes no branch (the store runs under exec = the mark
+// inside one asm block), so the unrolled window stays one basic block for the scheduler.
+template <int W>
+constexpr uint32_t k1q_cap() { return 64u * (1u + W / 2); }
+
+// FAST (launch-uniform, the kernel picks): the level-1 counter's high word is uniform over the
+// launch and every index is below 2^40 -- the resolve then forms the counter's low word with
+// 32-bit ops from the entry's counter word instead of the general 64-bit index arithmetic.
+template <int W = 12, bool FAST = false>
+__device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
                                           uint64_t n_groups, unsigned long long* __restrict__ win, uint64_t* q,
-                                          uint32_t* wz, uint32_t* tab, uint64_t* cq) {
-    static_assert(W <= 32, "the window's bits fit one 32-bit mask");
+                                          uint64_t* cq) {
+    static_assert(W % 2 == 0, "half windows");
     constexpr int U = 2;
     const uint32_t lane = threadIdx.x & 63;
     uint32_t qn = 0, cqn = 0;
@@ -182,24 +184,20 @@ __device__ __forceinline__ void k1_body_p(const DrawKey& dk, uint32_t k, uint64_
     const bool hi_uniform = (lo >> 33) == ((hi - 1) >> 33);
     const bool pre_ok = hi <= (1ull << 40);
     const uint64_t k_hi = (uint64_t)k << 32;
+    const uint32_t g0 = (uint32_t)g_begin;
     uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
     const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g_begin >> 32));
-    uint32_t gl = (uint32_t)g_begin + base + lane;
-    uint32_t* wzl = wz + lane;
-    // window row b holds iteration W-1-b: pair base0 + (W-1-b) stride + lane (and + 64)
-    if (lane < W) tab[lane] = (W - 1 - lane) * stride;
-    __builtin_amdgcn_wave_barrier();
+    uint32_t gl = g0 + base + lane;
     const uint32_t off_steady =
         __builtin_amdgcn_readfirstlane((int)std::max<uint32_t>(off_sparse, (lo & 15) ? 1u : 0u));
     const uint32_t ng_steady = __builtin_amdgcn_readfirstlane((int)(ng - ((hi & 15) ? 1u : 0u)));
 
+    // one queue entry per lane (valid lanes): its pair's first zero byte by level 1; the pair's other
+    // zero bytes go back to the queue; a dense / clipped pair (a z half 0) recomputes both blocks
     auto resolve = [&](bool valid, uint64_t ent) {
-        const uint32_t off = (uint32_t)ent, z = (uint32_t)(ent >> 32);
+        const uint32_t gt = (uint32_t)ent, off = gt - g0, z = (uint32_t)(ent >> 32);
         const bool dense = valid && ((z & 0xFFFFu) == 0 || (z >> 16) == 0);
-        RSV_K1P_COUNT(0, 1);
-        RSV_K1P_COUNT(1, __popcll(__builtin_amdgcn_ballot_w64(valid)));
         if (__builtin_amdgcn_ballot_w64(dense)) {
-            RSV_K1P_COUNT(2, 1);
             resolve_block(dk, dense, g_begin + off, lo, hi, dense_lim, k, cq, cqn, lane, hit);
             resolve_block(dk, dense && off + 64 < ng, g_begin + off + 64, lo, hi, dense_lim, k, cq, cqn, lane, hit);
         }
@@ -208,55 +206,109 @@ __device__ __forceinline__ void k1_body_p(const DrawKey& dk, uint32_t k, uint64_
         if (zm) {
             const uint32_t e = __builtin_ctz(zm);
             rest = zm & (zm - 1);
-            const uint64_t i = ((g_begin + off + ((e >> 4) << 6)) << 4) + (e & 15u);
-            const u32x4 w = level1_b0_words(dk, i, hi_uniform, c1u);
-            const uint32_t Lh = (i & 1) ? w.z : w.x;
-            const bool maybe = !pre_ok || (uint64_t)(Lh >> 8) * (i + 1) < k_hi;
-            if (maybe) {
-                const uint64_t L = ((uint64_t)Lh << 32) | ((i & 1) ? w.w : w.y);
-                const uint64_t j = __umul64hi(L >> 8, i + 1);
-                if (j < k) hit((uint32_t)j, i);
+            if constexpr (FAST) {
+                // the zero byte's block ghi:bl (bl = gt or gt + 64: never crosses the launch's
+                // 2^32-block span); level-1 counter i >> 1 = ghi:bl:(e & 15) >> 1, low word below
+                const uint32_t bl = gt + ((e & 16u) << 2);
+                const uint32_t g1lo = (bl << 3) | ((e & 15u) >> 1);
+                const u32x4 w = philox4x32_10_uniform_hi(g1lo, c1u, dk.s0, dk.s1, dk.k0, dk.k1);
+                const uint64_t i = ((((uint64_t)ghi << 32) | bl) << 4) | (e & 15u);
+                const bool odd = e & 1u;
+                const uint32_t Lh = odd ? w.z : w.x;
+                if ((uint64_t)(Lh >> 8) * (i + 1) < k_hi) {
+                    const uint64_t L = ((uint64_t)Lh << 32) | (odd ? w.w : w.y);
+                    const uint64_t j = __umul64hi(L >> 8, i + 1);
+                    if (j < k) hit((uint32_t)j, i);
+                }
+            } else {
+                const uint64_t i = ((g_begin + off + ((e >> 4) << 6)) << 4) + (e & 15u);
+                const u32x4 w = level1_b0_words(dk, i, hi_uniform, c1u);
+                const uint32_t Lh = (i & 1) ? w.z : w.x;
+                const bool maybe = !pre_ok || (uint64_t)(Lh >> 8) * (i + 1) < k_hi;
+                if (maybe) {
+                    const uint64_t L = ((uint64_t)Lh << 32) | ((i & 1) ? w.w : w.y);
+                    const uint64_t j = __umul64hi(L >> 8, i + 1);
+                    if (j < k) hit((uint32_t)j, i);
+                }
             }
         }
         const unsigned long long bal = __builtin_amdgcn_ballot_w64(rest != 0);
         if (bal) {
             if (rest) {
                 const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                q[qn + pos] = (uint64_t)off | ((uint64_t)~rest << 32);
+                q[qn + pos] = (uint64_t)(uint32_t)ent | ((uint64_t)~rest << 32);
             }
             qn += (uint32_t)__popcll(bal);
         }
     };
+    auto rounds = [&]() {
+        while (qn >= 64) {  // a resolve may append (pairs with more zero bytes)
+            qn -= 64;
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t ent = q[qn + lane];
+            __builtin_amdgcn_wave_barrier();
+            resolve(true, ent);
+            __builtin_amdgcn_wave_barrier();
+        }
+    };
+    // append this lane's pair (counter word gt, fold z) when has; wave-uniform call
+    auto append = [&](bool has, uint32_t gt, uint32_t z) {
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(has);
+        if (has) {
+            const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            q[qn + pos] = (uint64_t)gt | ((uint64_t)z << 32);
+        }
+        qn += (uint32_t)__popcll(bal);
+    };
 
+    // the wave's queue base as a scalar (LDS addresses are 32-bit), so an append's address is one
+    // v_lshl_add of the lane's slot onto base + 8 qn
+    const uint32_t q_s = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)q);
     while (base < ng) {  // wave-uniform
-        const uint32_t base0 = base;
-        uint32_t bits = 0, nb = 0;
-        if (base0 >= off_steady && (uint64_t)base0 + (uint64_t)(W - 1) * stride + U * 64 <= ng_steady) {
+        if (base >= off_steady && (uint64_t)base + (uint64_t)(W - 1) * stride + U * 64 <= ng_steady) {
 #pragma unroll
-            for (int t = 0; t < W; ++t) {
-                const uint32_t gt = gl + t * stride;
-                u32x4 w0, w1;
-                philox4x32_10_uniform_hi_x2(gt, ghi, dk.s0, dk.s1, dk.k0, dk.k1, w0, w1);
-                // fold_pair and the mark in ONE asm block (the hazard recognizer pads an s_nop
-                // between adjacent inline-asm blocks; the two below are the SDWA wait states)
-                const uint32_t xa = w0.x | w0.y | w0.z | w0.w, xb = w1.x | w1.y | w1.z | w1.w;
-                uint32_t z;
-                asm("v_or_b32_sdwa %0, %2, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
-                    "s_nop 0\n\t"
-                    "v_or_b32_sdwa %0, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t"
-                    "s_nop 0\n\t"
-                    "v_cmp_ne_u32_e32 vcc, -1, %0\n\t"
-                    "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
-                    : "=&v"(z), "+v"(bits)
-                    : "v"(xa), "v"(xb)
-                    : "vcc");
-                wzl[(W - 1 - t) * 64] = z;
+            for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                for (int t = 0; t < W / 2; ++t) {
+                    const uint32_t gt = gl + t * stride;
+                    u32x4 w0, w1;
+                    philox4x32_10_uniform_hi_x2(gt, ghi, dk.s0, dk.s1, dk.k0, dk.k1, w0, w1);
+                    // the pair fold (with the gfx950 SDWA wait states, fold_pair) and its mark as a
+                    // lane mask in one asm block
+                    const uint32_t xa = w0.x | w0.y | w0.z | w0.w, xb = w1.x | w1.y | w1.z | w1.w;
+                    uint32_t z;
+                    unsigned long long m;
+                    asm("v_or_b32_sdwa %0, %2, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                        "s_nop 0\n\t"
+                        "v_or_b32_sdwa %0, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                        "s_nop 0\n\t"
+                        "v_cmp_ne_u32_e64 %1, -1, %0"
+                        : "=&v"(z), "=s"(m)
+                        : "v"(xa), "v"(xb));
+                    const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    // the marked lanes store (exec = m inside the asm, restored before it ends; one
+                    // wave's LDS operations complete in order, so the rounds' reads see the entries)
+                    const uint32_t sb = q_s + 8u * qn;
+                    const uint64_t ent = (uint64_t)gt | ((uint64_t)z << 32);
+                    unsigned long long sv;
+                    uint32_t addr;
+                    asm volatile("v_lshl_add_u32 %1, %2, 3, %3\n\t"
+                                 "s_mov_b64 %0, exec\n\t"
+                                 "s_mov_b64 exec, %4\n\t"
+                                 "ds_write_b64 %1, %5\n\t"
+                                 "s_mov_b64 exec, %0"
+                                 : "=&s"(sv), "=&v"(addr)
+                                 : "v"(pos), "s"(sb), "s"(m), "v"(ent)
+                                 : "memory");
+                    qn += (uint32_t)__popcll(m);
+                }
+                gl += (W / 2) * stride;
+                __builtin_amdgcn_wave_barrier();
+                rounds();
             }
             base += W * stride;
-            gl += W * stride;
-            nb = W;
         } else {  // a partial window (first, last, or where the dense / clipped blocks lie)
-            for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride, ++nb) {
+            for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride) {
                 u32x4 w[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u)
@@ -268,7 +320,7 @@ __device__ __forceinline__ void k1_body_p(const DrawKey& dk, uint32_t k, uint64_
                     has = z != 0xFFFFFFFFu;
                 } else {
                     uint32_t y[U];
-                    bool h[U];
+                    bool hb[U];
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const uint32_t off = base + u * 64 + lane;
@@ -278,43 +330,14 @@ __device__ __forceinline__ void k1_body_p(const DrawKey& dk, uint32_t k, uint64_
                         // block past the launch is no candidate and not dense
                         y[u] = off >= ng ? 0xFFFFu
                                          : dense ? 0u : (fold16(w[u]) | (~clip_mask16(i0, lo, hi) & 0xFFFFu));
-                        h[u] = (off < ng) & (dense | ((uint16_t)y[u] != 0xFFFFu));
+                        hb[u] = (off < ng) & (dense | ((uint16_t)y[u] != 0xFFFFu));
                     }
                     z = (y[0] & 0xFFFFu) | (y[1] << 16);
-                    has = h[0] | h[1];
+                    has = hb[0] | hb[1];
                 }
-                bits = bits + bits + (uint32_t)has;
-                wzl[(W - 1 - t) * 64] = z;
-            }
-        }
-        // push the window's marked pairs: each round every lane with bits left pushes its lowest.
-        // Left-aligned, bit b is row b: its fold is wz row b, its offset lbase + tab[b].
-        bits <<= W - nb;
-        const uint32_t lbase = base0 + lane;
-        __builtin_amdgcn_wave_barrier();
-        RSV_K1P_COUNT(3, 1);
-        for (;;) {
-            const bool has = bits != 0;
-            const unsigned long long bal = __builtin_amdgcn_ballot_w64(has);
-            if (!bal) break;
-            RSV_K1P_COUNT(4, 1);
-            RSV_K1P_COUNT(5, __popcll(bal));
-            const uint32_t b = __builtin_ctz(bits | (1u << (W - 1)));  // (any row for a lane with none)
-            bits &= bits - 1;
-            const uint32_t off = lbase + tab[b];
-            const uint32_t z = wzl[b * 64];
-            if (has) {
-                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                q[qn + pos] = (uint64_t)off | ((uint64_t)z << 32);
-            }
-            qn += (uint32_t)__popcll(bal);
-            while (qn >= 64) {  // a resolve may append (pairs with more zero bytes)
-                qn -= 64;
+                append(has, gl, z);
                 __builtin_amdgcn_wave_barrier();
-                const uint64_t ent = q[qn + lane];
-                __builtin_amdgcn_wave_barrier();
-                resolve(true, ent);
-                __builtin_amdgcn_wave_barrier();
+                rounds();
             }
         }
     }

@@ -1,11 +1,17 @@
 // k1_dev_bodies.h -- development K1 loop bodies kept for A/B timing in tools/micro_k1.hip and
-// tools/micro_k1o.hip (NOT product code: the product K1 is rsv_scan.h k1_body_p).  Moved out of the
-// product header in round 4.  Each was the product body in an earlier round (DESIGN.md 5 decision 1):
+// tools/micro_k1o.hip (NOT product code: the product K1 is rsv_scan.h k1_body_q).  Moved out of the
+// product header in rounds 4 and 5.  Each was the product body in an earlier round (DESIGN.md 5
+// decision 1):
 //   k1_body       per-iteration block pushes (round 1)
 //   k1_body_bits  deferred pushes, one bit per block (round 2)
 //   k1_body_z     the zero-byte fold carried in the queue (round 2-3)
+//   k1_body_p     pair entries, window bits pushed in ballot rounds (rounds 3-4)
 #pragma once
 #include "../reservoir_amd/csrc/rsv_scan.h"
+
+#ifndef RSV_K1P_COUNT
+#define RSV_K1P_COUNT(i, v)  // development counters (tools/micro_k1o.hip)
+#endif
 
 namespace rsv {
 // Push the U blocks of one iteration (has[u]: block g_begin + off[u] holds a candidate) with one
@@ -328,6 +334,183 @@ __device__ __forceinline__ void k1_body_z(const DrawKey& dk, uint32_t k, uint64_
             }
             qn += (uint32_t)__popcll(bal);
             while (qn >= 64) {  // a resolve may append (blocks with more zero bytes)
+                qn -= 64;
+                __builtin_amdgcn_wave_barrier();
+                const uint64_t ent = q[qn + lane];
+                __builtin_amdgcn_wave_barrier();
+                resolve(true, ent);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+    while (qn > 0) {  // the last partial rounds (appends shrink geometrically)
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t nv = std::min<uint32_t>(qn, 64u);
+        qn -= nv;
+        const bool valid = lane < nv;
+        const uint64_t ent = valid ? q[qn + lane] : 0ull;
+        __builtin_amdgcn_wave_barrier();
+        resolve(valid, ent);
+    }
+    __builtin_amdgcn_wave_barrier();
+    drain_queue(dk, cq, cqn, lane, k, hit);
+}
+
+// ---- K1 with pair entries (k1_body_p, rounds 3-4) ----------------------------------------------------------
+// As k1_body_z (round 3; now tools/k1_dev_bodies.h), but a lane's two blocks of an iteration (offsets o and o + 64) share one window bit
+// and one queue entry: the 32-bit fold z holds block o's 16-bit fold in its low half and block
+// o + 64's in its high half (bit e clear <=> byte e & 15 of block o + 64 (e >> 4) is zero), built
+// by two SDWA ops straight into the halves, and one compare marks the pair -- 4 VALU ops per block
+// beside the Philox instead of 5, and half the window stores.  An entry's zero bytes are resolved
+// one at a time as before.  A pair with a dense-region (or out-of-range-partner) half -- z half 0,
+// impossible for a real sparse block (2^-128) -- takes the recomputing resolve for both blocks.
+constexpr uint32_t kK1PWin = 10;  // iterations (pairs per lane) per window
+
+template <int W = kK1PWin>
+__device__ __forceinline__ void k1_body_p(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                          uint64_t n_groups, unsigned long long* __restrict__ win, uint64_t* q,
+                                          uint32_t* wz, uint32_t* tab, uint64_t* cq) {
+    static_assert(W <= 32, "the window's bits fit one 32-bit mask");
+    constexpr int U = 2;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t qn = 0, cqn = 0;
+    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
+    const uint64_t dense_lim = 256ull * k;
+    const uint32_t ng = (uint32_t)n_groups;  // < 2^31 per launch (host splits)
+    const uint64_t g_sparse = (dense_lim + 14) >> 4;
+    const uint32_t off_sparse = g_sparse <= g_begin ? 0u : (uint32_t)std::min<uint64_t>(g_sparse - g_begin, ng);
+    const uint32_t stride = gridDim.x * blockDim.x * U;
+    const uint32_t c1u = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(lo >> 33) | kDomainLevel1));
+    const bool hi_uniform = (lo >> 33) == ((hi - 1) >> 33);
+    const bool pre_ok = hi <= (1ull << 40);
+    const uint64_t k_hi = (uint64_t)k << 32;
+    uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
+    const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g_begin >> 32));
+    uint32_t gl = (uint32_t)g_begin + base + lane;
+    uint32_t* wzl = wz + lane;
+    // window row b holds iteration W-1-b: pair base0 + (W-1-b) stride + lane (and + 64)
+    if (lane < W) tab[lane] = (W - 1 - lane) * stride;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t off_steady =
+        __builtin_amdgcn_readfirstlane((int)std::max<uint32_t>(off_sparse, (lo & 15) ? 1u : 0u));
+    const uint32_t ng_steady = __builtin_amdgcn_readfirstlane((int)(ng - ((hi & 15) ? 1u : 0u)));
+
+    auto resolve = [&](bool valid, uint64_t ent) {
+        const uint32_t off = (uint32_t)ent, z = (uint32_t)(ent >> 32);
+        const bool dense = valid && ((z & 0xFFFFu) == 0 || (z >> 16) == 0);
+        RSV_K1P_COUNT(0, 1);
+        RSV_K1P_COUNT(1, __popcll(__builtin_amdgcn_ballot_w64(valid)));
+        if (__builtin_amdgcn_ballot_w64(dense)) {
+            RSV_K1P_COUNT(2, 1);
+            resolve_block(dk, dense, g_begin + off, lo, hi, dense_lim, k, cq, cqn, lane, hit);
+            resolve_block(dk, dense && off + 64 < ng, g_begin + off + 64, lo, hi, dense_lim, k, cq, cqn, lane, hit);
+        }
+        const uint32_t zm = (valid && !dense) ? ~z : 0u;
+        uint32_t rest = 0;
+        if (zm) {
+            const uint32_t e = __builtin_ctz(zm);
+            rest = zm & (zm - 1);
+            const uint64_t i = ((g_begin + off + ((e >> 4) << 6)) << 4) + (e & 15u);
+            const u32x4 w = level1_b0_words(dk, i, hi_uniform, c1u);
+            const uint32_t Lh = (i & 1) ? w.z : w.x;
+            const bool maybe = !pre_ok || (uint64_t)(Lh >> 8) * (i + 1) < k_hi;
+            if (maybe) {
+                const uint64_t L = ((uint64_t)Lh << 32) | ((i & 1) ? w.w : w.y);
+                const uint64_t j = __umul64hi(L >> 8, i + 1);
+                if (j < k) hit((uint32_t)j, i);
+            }
+        }
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(rest != 0);
+        if (bal) {
+            if (rest) {
+                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                q[qn + pos] = (uint64_t)off | ((uint64_t)~rest << 32);
+            }
+            qn += (uint32_t)__popcll(bal);
+        }
+    };
+
+    while (base < ng) {  // wave-uniform
+        const uint32_t base0 = base;
+        uint32_t bits = 0, nb = 0;
+        if (base0 >= off_steady && (uint64_t)base0 + (uint64_t)(W - 1) * stride + U * 64 <= ng_steady) {
+#pragma unroll
+            for (int t = 0; t < W; ++t) {
+                const uint32_t gt = gl + t * stride;
+                u32x4 w0, w1;
+                philox4x32_10_uniform_hi_x2(gt, ghi, dk.s0, dk.s1, dk.k0, dk.k1, w0, w1);
+                // fold_pair and the mark in ONE asm block (the hazard recognizer pads an s_nop
+                // between adjacent inline-asm blocks; the two below are the SDWA wait states)
+                const uint32_t xa = w0.x | w0.y | w0.z | w0.w, xb = w1.x | w1.y | w1.z | w1.w;
+                uint32_t z;
+                asm("v_or_b32_sdwa %0, %2, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                    "s_nop 0\n\t"
+                    "v_or_b32_sdwa %0, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                    "s_nop 0\n\t"
+                    "v_cmp_ne_u32_e32 vcc, -1, %0\n\t"
+                    "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
+                    : "=&v"(z), "+v"(bits)
+                    : "v"(xa), "v"(xb)
+                    : "vcc");
+                wzl[(W - 1 - t) * 64] = z;
+            }
+            base += W * stride;
+            gl += W * stride;
+            nb = W;
+        } else {  // a partial window (first, last, or where the dense / clipped blocks lie)
+            for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride, ++nb) {
+                u32x4 w[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    w[u] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
+                uint32_t z;
+                bool has;
+                if (base >= off_steady && base + U * 64 <= ng_steady) {
+                    z = fold_pair(w[0], w[1]);
+                    has = z != 0xFFFFFFFFu;
+                } else {
+                    uint32_t y[U];
+                    bool h[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t off = base + u * 64 + lane;
+                        const uint64_t i0 = (g_begin + off) << 4;
+                        const bool dense = i0 + 1 < dense_lim;
+                        // indices outside [lo, hi) count as nonzero bytes (never candidates); a
+                        // block past the launch is no candidate and not dense
+                        y[u] = off >= ng ? 0xFFFFu
+                                         : dense ? 0u : (fold16(w[u]) | (~clip_mask16(i0, lo, hi) & 0xFFFFu));
+                        h[u] = (off < ng) & (dense | ((uint16_t)y[u] != 0xFFFFu));
+                    }
+                    z = (y[0] & 0xFFFFu) | (y[1] << 16);
+                    has = h[0] | h[1];
+                }
+                bits = bits + bits + (uint32_t)has;
+                wzl[(W - 1 - t) * 64] = z;
+            }
+        }
+        // push the window's marked pairs: each round every lane with bits left pushes its lowest.
+        // Left-aligned, bit b is row b: its fold is wz row b, its offset lbase + tab[b].
+        bits <<= W - nb;
+        const uint32_t lbase = base0 + lane;
+        __builtin_amdgcn_wave_barrier();
+        RSV_K1P_COUNT(3, 1);
+        for (;;) {
+            const bool has = bits != 0;
+            const unsigned long long bal = __builtin_amdgcn_ballot_w64(has);
+            if (!bal) break;
+            RSV_K1P_COUNT(4, 1);
+            RSV_K1P_COUNT(5, __popcll(bal));
+            const uint32_t b = __builtin_ctz(bits | (1u << (W - 1)));  // (any row for a lane with none)
+            bits &= bits - 1;
+            const uint32_t off = lbase + tab[b];
+            const uint32_t z = wzl[b * 64];
+            if (has) {
+                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                q[qn + pos] = (uint64_t)off | ((uint64_t)z << 32);
+            }
+            qn += (uint32_t)__popcll(bal);
+            while (qn >= 64) {  // a resolve may append (pairs with more zero bytes)
                 qn -= 64;
                 __builtin_amdgcn_wave_barrier();
                 const uint64_t ent = q[qn + lane];

@@ -1,4 +1,4 @@
-// micro_k1o.hip -- K1 occupancy A/B (development tool, not product): the product body k1_body_z
+// micro_k1o.hip -- K1 A/B (development tool, not product): the round-3 body k1_body_z
 // compiled with the default register allocation (.sgpr_count 100 -> 6 workgroups of 256 per CU,
 // MI355X_MICROARCH.md "Residency") and with amdgpu_num_sgpr limits that admit 8, over a grid sweep.
 // Every variant's winner table is checked against the default's.
@@ -62,6 +62,20 @@ __global__ __launch_bounds__(256) void k1_pair(DrawKey dk, uint32_t k, uint64_t 
     __shared__ K1PLds<W> L;
     const int w = threadIdx.x >> 6;
     k1_body_p<W>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.wz[w], L.tab[w], L.cq[w]);
+}
+
+// direct appends (k1_body_q), W iterations per window
+template <int W>
+struct K1QLds {
+    uint64_t q[4][k1q_cap<W>()];
+    uint64_t cq[4][kQueue];
+};
+template <int W, bool FAST = false>
+__global__ __launch_bounds__(256) void k1_q(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                            uint64_t n_groups, unsigned long long* __restrict__ win) {
+    __shared__ K1QLds<W> L;
+    const int w = threadIdx.x >> 6;
+    k1_body_q<W, FAST>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w]);
 }
 
 template <bool NOP>
@@ -169,9 +183,9 @@ int main(int argc, char** argv) {
     for (int p = 0; p < passes; ++p)
         for (int g : grids) {
             if (time_v(k1_base, "base", g)) return 1;
-            if (time_v(k1_pair<10>, "pair10", g)) return 1;
             if (time_v(k1_pair<12>, "pair12", g)) return 1;
-            if (time_v(k1_pair<16>, "pair16", g)) return 1;
+            if (time_v(k1_q<12>, "q12", g)) return 1;
+            if (time_v(k1_q<12, true>, "q12fast", g)) return 1;
         }
     return 0;
 }

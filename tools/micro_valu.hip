@@ -31,7 +31,6 @@ using namespace rsv;
 
 constexpr int kWavesPerSimd = 8;
 constexpr int kBlocksPerCu = 8;  // 8 x 4 waves = 32 waves per CU
-constexpr int kIters = 1024;
 
 // 8 instructions of kind OP to 8 different destinations, inputs a, b (vector) and s (scalar)
 template <int OP>
@@ -61,13 +60,13 @@ __device__ __forceinline__ void burst(uint32_t (&d)[8], uint64_t (&q)[8], uint32
 }
 
 template <int OP>
-__global__ __launch_bounds__(256) void op_rate(uint64_t* cyc, uint32_t* sink, uint32_t s) {
+__global__ __launch_bounds__(256) void op_rate(uint64_t* cyc, uint32_t* sink, uint32_t s, int iters) {
     uint32_t d[8];
     uint64_t q[8];
     const uint32_t a = threadIdx.x * 0x9E3779B9u, b = a ^ s;
     __builtin_amdgcn_s_barrier();
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    for (int it = 0; it < kIters; ++it) {
+    for (int it = 0; it < iters; ++it) {
         burst<OP>(d, q, a + it, b, s);
         burst<OP>(d, q, a + it, b, s);
         burst<OP>(d, q, a + it, b, s);
@@ -85,13 +84,13 @@ __global__ __launch_bounds__(256) void op_rate(uint64_t* cyc, uint32_t* sink, ui
 }
 
 // K1's level-0 call (counter words 1..3 wave-uniform), two chains per lane as in K1
-__global__ __launch_bounds__(256) void philox_rate(uint64_t* cyc, uint32_t* sink, uint32_t s) {
+__global__ __launch_bounds__(256) void philox_rate(uint64_t* cyc, uint32_t* sink, uint32_t s, int iters) {
     const DrawKey dk{0xC0FFEEu, s, 0x5A5Au, 0};
     uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x, acc = 0;
     const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
     __builtin_amdgcn_s_barrier();
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    for (int it = 0; it < kIters; ++it, gl += 1u << 21) {
+    for (int it = 0; it < iters; ++it, gl += 1u << 21) {
         const u32x4 w0 = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1);
         const u32x4 w1 = philox4x32_10_uniform_hi(gl + 64, ghi, dk.s0, dk.s1, dk.k0, dk.k1);
         acc ^= w0.x ^ w0.y ^ w0.z ^ w0.w ^ w1.x ^ w1.y ^ w1.z ^ w1.w;
@@ -106,11 +105,11 @@ __global__ __launch_bounds__(256) void philox_rate(uint64_t* cyc, uint32_t* sink
 }
 
 // the full (non-uniform) Philox4x32-10 of the level-1 draws
-__global__ __launch_bounds__(256) void philox_full_rate(uint64_t* cyc, uint32_t* sink, uint32_t s) {
+__global__ __launch_bounds__(256) void philox_full_rate(uint64_t* cyc, uint32_t* sink, uint32_t s, int iters) {
     uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x, acc = 0;
     __builtin_amdgcn_s_barrier();
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    for (int it = 0; it < kIters; ++it, gl += 1u << 21) {
+    for (int it = 0; it < iters; ++it, gl += 1u << 21) {
         const u32x4 w0 = philox4x32_10(gl, gl ^ 0x80000000u, s, gl >> 7, 0xC0FFEEu, s);
         const u32x4 w1 = philox4x32_10(gl + 64, gl ^ 0x80000001u, s, gl >> 7, 0xC0FFEEu, s);
         acc ^= w0.x ^ w0.y ^ w0.z ^ w0.w ^ w1.x ^ w1.y ^ w1.z ^ w1.w;
@@ -136,10 +135,14 @@ int main() {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     std::vector<uint64_t> h(2 * (size_t)waves);
-    auto run = [&](auto kern, const char* name, double per_wave) -> int {
-        for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, cyc, sink, 7u);
+    // per row: cycles per wave-instruction per SIMD two ways -- from each wave's own s_memtime span
+    // (a LOWER bound: the 8 waves of a SIMD do not all overlap for the whole span, dispatch staggers
+    // their starts) and from the launch's wall time at the in-kernel clock (an UPPER bound: includes
+    // the dispatch ramp); a long run (16x the iterations) brings the two together
+    auto run = [&](auto kern, const char* name, double per_iter, int iters) -> int {
+        for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, cyc, sink, 7u, iters);
         CK(hipEventRecord(e0));
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, cyc, sink, 7u);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, cyc, sink, 7u, iters);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms = 0;
@@ -151,27 +154,29 @@ int main() {
         std::sort(r.begin(), r.end());
         const double med = (double)s[s.size() / 2], rmed = (double)r[r.size() / 2];
         const double ghz = med / rmed * 0.1;  // shader clock during the run (guide: memtime / memrealtime x 100 MHz)
-        const double cpi = med / (per_wave * kWavesPerSimd);
-        printf("{\"op\": \"%s\", \"cycles_per_wave_instr_per_simd\": %.3f, \"full_rate_slots\": %.3f, "
-               "\"median_wave_cycles\": %.0f, \"wall_ms\": %.4f, \"clock_GHz\": %.3f, \"ns_per_wave_instr_per_simd\": %.3f}\n",
-               name, cpi, cpi / 2.0, med, ms, ghz, cpi / ghz);
+        const double per_simd = per_iter * iters * kWavesPerSimd;
+        const double cpi = med / per_simd, wall_cpi = ms * 1e6 * ghz / per_simd;
+        printf("{\"op\": \"%s\", \"iters\": %d, \"cycles_per_wave_instr_per_simd_wave_span\": %.3f, "
+               "\"cycles_per_wave_instr_per_simd_wall\": %.3f, \"median_wave_cycles\": %.0f, \"wall_ms\": %.4f, "
+               "\"clock_GHz\": %.3f, \"wall_ns_per_wave_instr_per_simd\": %.3f}\n",
+               name, iters, cpi, wall_cpi, med, ms, ghz, ms * 1e6 / per_simd);
         return 0;
     };
-    const double burst_instr = 4.0 * 8 * kIters;
+    const double burst_instr = 4.0 * 8;
     // the clock ramps under sustained load: ~1 s of back-to-back launches before the first row
-    for (int rep = 0; rep < 2000; ++rep) hipLaunchKernelGGL(op_rate<2>, dim3(grid), dim3(256), 0, 0, cyc, sink, 7u);
+    for (int rep = 0; rep < 2000; ++rep) hipLaunchKernelGGL(op_rate<2>, dim3(grid), dim3(256), 0, 0, cyc, sink, 7u, 1024);
     CK(hipDeviceSynchronize());
-    if (run(op_rate<0>, "v_mad_u64_u32", burst_instr)) return 1;
-    if (run(op_rate<1>, "v_bitop3_b32", burst_instr)) return 1;
-    if (run(op_rate<2>, "v_xor_b32", burst_instr)) return 1;
-    if (run(op_rate<3>, "v_mul_hi_u32", burst_instr)) return 1;
-    if (run(op_rate<4>, "v_mul_lo_u32", burst_instr)) return 1;
-    if (run(op_rate<5>, "v_add_u32", burst_instr)) return 1;
+    for (int it : {1024, 16384}) if (run(op_rate<0>, "v_mad_u64_u32", burst_instr, it)) return 1;
+    for (int it : {1024, 16384}) if (run(op_rate<1>, "v_bitop3_b32", burst_instr, it)) return 1;
+    for (int it : {1024, 16384}) if (run(op_rate<2>, "v_xor_b32", burst_instr, it)) return 1;
+    for (int it : {1024, 16384}) if (run(op_rate<3>, "v_mul_hi_u32", burst_instr, it)) return 1;
+    for (int it : {1024, 16384}) if (run(op_rate<4>, "v_mul_lo_u32", burst_instr, it)) return 1;
+    for (int it : {1024, 16384}) if (run(op_rate<5>, "v_add_u32", burst_instr, it)) return 1;
     // the guide's fp32 FMA figure (2 cycles per wave64 instruction on a SIMD) against the 32-bit
     // integer ops above: reconciles the 4-cycle issue model bench.py's VALU roofline prices with
-    if (run(op_rate<6>, "v_fma_f32", burst_instr)) return 1;
-    if (run(op_rate<7>, "v_pk_fma_f32", burst_instr)) return 1;
-    if (run(philox_rate, "philox4x32_10_uniform_hi (per call)", 2.0 * kIters)) return 1;
-    if (run(philox_full_rate, "philox4x32_10 (per call)", 2.0 * kIters)) return 1;
+    for (int it : {1024, 16384}) if (run(op_rate<6>, "v_fma_f32", burst_instr, it)) return 1;
+    for (int it : {1024, 16384}) if (run(op_rate<7>, "v_pk_fma_f32", burst_instr, it)) return 1;
+    for (int it : {1024, 16384}) if (run(philox_rate, "philox4x32_10_uniform_hi (per call)", 2.0, it)) return 1;
+    for (int it : {1024, 16384}) if (run(philox_full_rate, "philox4x32_10 (per call)", 2.0, it)) return 1;
     return 0;
 }
