@@ -56,7 +56,10 @@ def pmc(dirpath: str, kernel: str) -> dict:
 
 def main(src: str, dst: str) -> None:
     os.makedirs(dst, exist_ok=True)
-    summary = {"source_run": os.path.basename(src.rstrip("/"))}
+    # merged into an existing summary (other runs' kernels, e.g. the C3 line-request pass, stay)
+    out_path = os.path.join(dst, "pmc_summary.json")
+    summary = json.load(open(out_path)) if os.path.exists(out_path) else {}
+    summary["source_run"] = os.path.basename(src.rstrip("/"))
     for tag, kern in KERNELS.items():
         stats = os.path.join(src, tag, f"{tag}_kernel_stats.csv")
         if os.path.exists(stats):
@@ -64,7 +67,10 @@ def main(src: str, dst: str) -> None:
         sq = pmc(os.path.join(src, f"{tag}_sq"), kern)
         fe = pmc(os.path.join(src, f"{tag}_fetch"), kern)
         wr = pmc(os.path.join(src, f"{tag}_write"), kern)
-        d = {"kernel": kern, "sq_pass": sq, "fetch_pass": fe, "write_pass": wr}
+        if not (sq or fe or wr):
+            continue
+        d = {"kernel": kern, "sq_pass": sq, "fetch_pass": fe, "write_pass": wr,
+             "pmc_source_run": summary["source_run"]}
         if "SQ_INSTS_VALU" in sq and "GRBM_GUI_ACTIVE" in sq:
             cyc = sq["GRBM_GUI_ACTIVE"] / 8
             d["valu_instrs_per_launch"] = sq["SQ_INSTS_VALU"]
@@ -72,10 +78,14 @@ def main(src: str, dst: str) -> None:
             d["cycles_per_valu_instr_per_simd"] = round(cyc * 1024 / sq["SQ_INSTS_VALU"], 3)
             if "dur_us_median" in sq:
                 d["clock_GHz"] = round(cyc / (sq["dur_us_median"] * 1e-6) / 1e9, 3)
+                # the same normalised by the launch's duration at the 2.4 GHz peak shader clock (the
+                # VALU model's clock): cycles per wave-instruction per SIMD if the clock ran at peak
+                d["cycles_per_valu_instr_per_simd_at_2.4GHz"] = round(
+                    sq["dur_us_median"] * 1e-6 * 2.4e9 * 1024 / sq["SQ_INSTS_VALU"], 3)
         if "FETCH_SIZE" in fe and "WRITE_SIZE" in wr:
             d["hbm_bytes_per_launch"] = int((2 * fe["FETCH_SIZE"] + wr["WRITE_SIZE"]) * 1024)
             d["hbm_bytes_rule"] = "(2 x FETCH_SIZE + WRITE_SIZE) KiB (gfx950 FETCH_SIZE correction)"
-        summary[tag] = d
+        summary[tag] = {**summary.get(tag, {}), **d}
     bench = os.path.join(src, "bench.log")
     if os.path.exists(bench):
         for line in open(bench):
@@ -89,7 +99,7 @@ def main(src: str, dst: str) -> None:
         with open(os.path.join(dst, "pmc_k1.json"), "w") as f:
             json.dump({"n": n, "hbm_bytes_per_launch": k1["hbm_bytes_per_launch"], "kernel": k1["kernel"],
                        "source_run": summary["source_run"]}, f, indent=1)
-    with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+    with open(out_path, "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps({t: {k: v for k, v in d.items() if not k.endswith("_pass")} for t, d in summary.items()
                       if isinstance(d, dict) and t != "bench_line"}, indent=1))

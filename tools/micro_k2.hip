@@ -14,7 +14,8 @@
 #include <vector>
 
 #include "k2_dev_variants.h"  // the round-4 kernel + cost-probe variants
-namespace k2 = rsv::k2dev;
+#include "../reservoir_amd/csrc/rsv_k2.h"  // the product kernel (mode n: the product against variant 0)
+namespace kd = rsv::k2dev;
 
 using namespace rsv;
 
@@ -48,8 +49,8 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&cnt, S * 8));
     hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, keys, n, offs, S, L);
     CK(hipDeviceSynchronize());
-    const size_t lds = k2::lds_bytes(k);
-    unsigned grid = (unsigned)std::min<int64_t>(S / k2::kWaves, 256 * 128);  // the product's cap (rsv_segmented.hip)
+    const size_t lds = kd::lds_bytes(k);
+    unsigned grid = (unsigned)std::min<int64_t>(S / kd::kWaves, 256 * 128);  // the product's cap (rsv_segmented.hip)
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -60,7 +61,7 @@ int main(int argc, char** argv) {
         // the first ~20 launches run on a still-ramping clock (bench.py's ramp note): timed after them
         for (int rep = 0; rep < 45; ++rep) {
             CK(hipEventRecord(e0));
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * k2::kWaves), lds_run, 0, (const int64_t*)keys,
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kd::kWaves), lds_run, 0, (const int64_t*)keys,
                                (const int64_t*)offs, S, k, 1u, 0u, 0ull, out, cnt, 0xFFFFFFFFu,
                                (unsigned long long*)nullptr);
             CK(hipEventRecord(e1));
@@ -77,44 +78,73 @@ int main(int argc, char** argv) {
         }
         return 0;
     };
-    if (run(k2::k2_segmented<int64_t, 0>, "0 wave-per-stream", false)) return 1;
+    // the product kernel (rsv_k2.h) through its own launch shape, timed like run()
+    auto run_product = [&](const char* name) -> int {
+        std::vector<float> ts;
+        const size_t plds = rsv::k2::lds_bytes(k);
+        const unsigned pgrid = (unsigned)std::min<int64_t>((S + rsv::k2::kWaves - 1) / rsv::k2::kWaves, 256 * 128);
+        for (int rep = 0; rep < 45; ++rep) {
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL(rsv::k2::k2_segmented<int64_t>, dim3(pgrid), dim3(64 * rsv::k2::kWaves), plds, 0,
+                               (const int64_t*)keys, (const int64_t*)offs, S, k, 1u, 0u, 0ull, out, cnt,
+                               rsv::k2::kQCap);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (rep >= 25) ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        printf("{\"variant\": \"%s\", \"median_ms\": %.4f, \"min_ms\": %.4f}\n", name, ts[ts.size() / 2], ts[0]);
+        CK(hipMemcpy(got.data(), out, S * k * 8, hipMemcpyDeviceToHost));
+        printf("  identical to variant 0: %s\n", got == ref ? "yes" : "NO");
+        return 0;
+    };
+    if (run(kd::k2_segmented<int64_t, 0>, "0 wave-per-stream", false)) return 1;
     CK(hipMemcpy(ref.data(), out, S * k * 8, hipMemcpyDeviceToHost));
+    if (argc > 1 && argv[1][0] == 'n') {  // the product kernel against the round-4 form (A/B/A/B)
+        for (int rep = 0; rep < 2; ++rep) {
+            if (run_product("product rsv_k2.h")) return 1;
+            if (run(kd::k2_segmented<int64_t, 0>, "0 round-4 copy (k2_dev_variants.h)", true)) return 1;
+        }
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 'o') {  // occupancy sensitivity: the product with its LDS padded
-        CK(hipFuncSetAttribute((const void*)k2::k2_segmented<int64_t, 0>,
+        CK(hipFuncSetAttribute((const void*)kd::k2_segmented<int64_t, 0>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         for (size_t pad : {lds, (size_t)(160 * 1024 / 3), (size_t)(160 * 1024 / 2)}) {
             lds_run = pad;
             char name[64];
             snprintf(name, sizeof name, "0 product, %zu B LDS per workgroup", pad);
-            if (run(k2::k2_segmented<int64_t, 0>, name, true)) return 1;
+            if (run(kd::k2_segmented<int64_t, 0>, name, true)) return 1;
         }
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'l') return 0;  // the two product forms only
     if (argc > 1 && argv[1][0] == 'p') return 0;  // one variant only (rocprofv3 --pmc passes)
     if (argc > 1 && argv[1][0] == 'q') {  // occupancy: the 2048-entry FIFO (4 workgroups per CU)
-        lds_run = k2::lds_bytes(k, 128);
-        if (run(k2::k2_segmented<int64_t, 128>, "128 FIFO 2048 entries", true)) return 1;
-        lds_run = k2::lds_bytes(k, 256);
-        if (run(k2::k2_segmented<int64_t, 256>, "256 stash ring of 2 iterations", true)) return 1;
+        lds_run = kd::lds_bytes(k, 128);
+        if (run(kd::k2_segmented<int64_t, 128>, "128 FIFO 2048 entries", true)) return 1;
+        lds_run = kd::lds_bytes(k, 256);
+        if (run(kd::k2_segmented<int64_t, 256>, "256 stash ring of 2 iterations", true)) return 1;
         lds_run = lds;
-        if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+        if (run(kd::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'g') {  // A/B/A against the previous masks and the gather-free forms
-        if (run(k2::k2_segmented<int64_t, 8192>, "8192 8-plane masks everywhere (r02 up to here)", true)) return 1;
-        if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
-        if (run(k2::k2_segmented<int64_t, 8193>, "8193 8-plane masks, no gather", false)) return 1;
-        if (run(k2::k2_segmented<int64_t, 1>, "1 no gather", false)) return 1;
-        if (run(k2::k2_segmented<int64_t, 8192>, "8192 (again)", true)) return 1;
+        if (run(kd::k2_segmented<int64_t, 8192>, "8192 8-plane masks everywhere (r02 up to here)", true)) return 1;
+        if (run(kd::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+        if (run(kd::k2_segmented<int64_t, 8193>, "8193 8-plane masks, no gather", false)) return 1;
+        if (run(kd::k2_segmented<int64_t, 1>, "1 no gather", false)) return 1;
+        if (run(kd::k2_segmented<int64_t, 8192>, "8192 (again)", true)) return 1;
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'c') {  // cost split of the level-0 side (no gather, no resolve)
-        if (run(k2::k2_segmented<int64_t, 9>, "9 dropped + no gather", false)) return 1;
-        if (run(k2::k2_segmented<int64_t, 9 | 1024>, "9 + no head", false)) return 1;
-        if (run(k2::k2_segmented<int64_t, 9 | 1024 | 2048>, "9 + no head + no append", false)) return 1;
-        if (run(k2::k2_segmented<int64_t, 9 | 1024 | 2048 | 4096>, "9 + no head + no append + no candidates", false)) return 1;
-        if (run(k2::k2_segmented<int64_t, 1 | 1024>, "1 + no head (resolve kept)", false)) return 1;
+        if (run(kd::k2_segmented<int64_t, 9>, "9 dropped + no gather", false)) return 1;
+        if (run(kd::k2_segmented<int64_t, 9 | 1024>, "9 + no head", false)) return 1;
+        if (run(kd::k2_segmented<int64_t, 9 | 1024 | 2048>, "9 + no head + no append", false)) return 1;
+        if (run(kd::k2_segmented<int64_t, 9 | 1024 | 2048 | 4096>, "9 + no head + no append + no candidates", false)) return 1;
+        if (run(kd::k2_segmented<int64_t, 1 | 1024>, "1 + no head (resolve kept)", false)) return 1;
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'G') {  // grid sweep of the product (argv[2..]: grids)
@@ -123,36 +153,36 @@ int main(int argc, char** argv) {
                 grid = (unsigned)atoi(argv[a]);
                 char name[64];
                 snprintf(name, sizeof name, "0 product, grid %u", grid);
-                if (run(k2::k2_segmented<int64_t, 0>, name, true)) return 1;
+                if (run(kd::k2_segmented<int64_t, 0>, name, true)) return 1;
             }
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'r') {  // dense head cut to whole 64-pair rounds vs uncut (A/B/A/B)
         for (int rep = 0; rep < 2; ++rep) {
-            if (run(k2::k2_segmented<int64_t, 512>, "512 head [k, 4k) uncut (r02)", true)) return 1;
-            if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+            if (run(kd::k2_segmented<int64_t, 512>, "512 head [k, 4k) uncut (r02)", true)) return 1;
+            if (run(kd::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
         }
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'm') {  // head multiplier 4 (product) vs 6, 8 (whole rounds)
         for (int rep = 0; rep < 2; ++rep) {
-            if (run(k2::k2_segmented<int64_t, 16384>, "16384 head [k, 6k) in whole rounds", true)) return 1;
-            if (run(k2::k2_segmented<int64_t, 32768>, "32768 head [k, 8k) in whole rounds", true)) return 1;
-            if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+            if (run(kd::k2_segmented<int64_t, 16384>, "16384 head [k, 6k) in whole rounds", true)) return 1;
+            if (run(kd::k2_segmented<int64_t, 32768>, "32768 head [k, 8k) in whole rounds", true)) return 1;
+            if (run(kd::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
         }
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'h') {  // dense-head multiplier: 4 (product), 2, none
-        if (run(k2::k2_segmented<int64_t, 32>, "32 head [k, 2k)", true)) return 1;
-        if (run(k2::k2_segmented<int64_t, 64>, "64 no head (all through the FIFO)", true)) return 1;
-        if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+        if (run(kd::k2_segmented<int64_t, 32>, "32 head [k, 2k)", true)) return 1;
+        if (run(kd::k2_segmented<int64_t, 64>, "64 no head (all through the FIFO)", true)) return 1;
+        if (run(kd::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
         return 0;
     }
-    if (run(k2::k2_segmented<int64_t, 1>, "1 no gather", false)) return 1;
-    if (run(k2::k2_segmented<int64_t, 2>, "2 no level-1 philox", false)) return 1;
-    if (run(k2::k2_segmented<int64_t, 16>, "16 gather stored at once (no deferral)", true)) return 1;
-    if (run(k2::k2_segmented<int64_t, 8>, "8 candidates dropped", false)) return 1;
-    if (run(k2::k2_segmented<int64_t, 9>, "9 dropped + no gather", false)) return 1;
-    if (run(k2::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
+    if (run(kd::k2_segmented<int64_t, 1>, "1 no gather", false)) return 1;
+    if (run(kd::k2_segmented<int64_t, 2>, "2 no level-1 philox", false)) return 1;
+    if (run(kd::k2_segmented<int64_t, 16>, "16 gather stored at once (no deferral)", true)) return 1;
+    if (run(kd::k2_segmented<int64_t, 8>, "8 candidates dropped", false)) return 1;
+    if (run(kd::k2_segmented<int64_t, 9>, "9 dropped + no gather", false)) return 1;
+    if (run(kd::k2_segmented<int64_t, 0>, "0 product (again)", true)) return 1;
     return 0;
 }
