@@ -24,6 +24,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -47,6 +48,41 @@ typedef long long w2i64 __attribute__((ext_vector_type(2)));
 inline unsigned wgrid(int64_t n, int64_t cap = 65535) {
     return (unsigned)std::min<int64_t>(std::max<int64_t>((n + kWBlock - 1) / kWBlock, 1), cap);
 }
+
+// The ordered mode's scheduled pass (see wide_sample_device): ranges [s_r, s_r+1) of the rest with
+// falling bounds B_r; device table = starts [R + 1] then bounds [R].
+constexpr int kWMaxR = 64;
+
+// the proof needs >= k distinct hashes under each predicted bound, ~Poisson(beta k) of them: below
+// k = 64 it fails too often to pay (k = 1: ~1 in 4 passes proves), so small k keep the chunk loop
+constexpr int32_t kSchedMinK = 64;
+constexpr int kSchedCounts = 192;                       // counts' offset in the table buffer
+constexpr int kSchedWords = kSchedCounts + kWMaxR + 1;  // table [2 kWMaxR + 1] + counts [kWMaxR + 1]
+static_assert(2 * kWMaxR + 1 <= kSchedCounts, "range table overlaps the counts");
+
+// the filter's per-element bound: the iteration covers ranges [rl, rh] (wave-uniform), element i
+// takes the bound of the range that holds it
+struct WRanges {
+    int64_t* rs;  // LDS starts [R + 1]
+    int64_t* rb;  // LDS bounds [R]
+    int32_t R;
+    __device__ __forceinline__ void load(const int64_t* __restrict__ tab) {
+        for (int t = threadIdx.x; t <= R; t += blockDim.x) rs[t] = tab[t];
+        for (int t = threadIdx.x; t < R; t += blockDim.x) rb[t] = tab[R + 1 + t];
+        __syncthreads();
+    }
+    // advance rl to the range holding lo, and rh to the one holding hi - 1 (uniform arguments)
+    __device__ __forceinline__ void span(int64_t lo, int64_t hi, int32_t& rl, int32_t& rh) const {
+        while (rl + 1 < R && rs[rl + 1] <= lo) ++rl;
+        rh = rl;
+        while (rh + 1 < R && rs[rh + 1] < hi) ++rh;
+    }
+    __device__ __forceinline__ int64_t at(int64_t i, int32_t rl, int32_t rh) const {
+        int64_t b = rb[rl];
+        for (int32_t r = rl + 1; r <= rh; ++r) b = i >= rs[r] ? rb[r] : b;
+        return b;
+    }
+};
 
 __device__ __forceinline__ unsigned long long lanemask_lt_w() {
     const uint32_t lane = threadIdx.x & 63;
@@ -123,15 +159,21 @@ struct WideOut {
 // The filter over precomputed hashes: 16-B non-temporal loads (two hashes each), kWideU in flight per
 // lane; the <= 1 head element before the first 16-B boundary and the odd tail go through the scalar
 // loops.  Loop bounds are wave-uniform (tile starts), so the ballots see every lane.
+// With R > 0 ranges (rtab), element i's bound is its range's (the ordered mode's scheduled pass).
 __global__ __launch_bounds__(kWBlock) void wide_filter_hashes(const int64_t* __restrict__ hashes, int64_t n, int64_t r0,
                                                               int64_t r1, int64_t bound, int64_t* __restrict__ cand_h,
                                                               int64_t* __restrict__ cand_i,
-                                                              unsigned long long* __restrict__ counter, int64_t cap) {
+                                                              unsigned long long* __restrict__ counter, int64_t cap,
+                                                              const int64_t* __restrict__ rtab, int32_t R) {
     __shared__ int64_t sh_h[kWBlock / 64][WideOut::Q];
     __shared__ int64_t sh_i[kWBlock / 64][WideOut::Q];
     __shared__ uint32_t s_q[kWBlock / 64];
     __shared__ unsigned long long s_base;
+    __shared__ int64_t s_rs[kWMaxR + 1], s_rb[kWMaxR];
     WideOut out{sh_h[threadIdx.x >> 6], sh_i[threadIdx.x >> 6], 0u, cand_h, cand_i, counter, cap};
+    WRanges rg{s_rs, s_rb, R};
+    if (R) rg.load(rtab);
+    int32_t rl = 0, rh = 0;
     const int64_t T = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t head = std::min<int64_t>(n, (int64_t)(((16u - ((uintptr_t)hashes & 15u)) & 15u) / 8u));
@@ -144,6 +186,7 @@ __global__ __launch_bounds__(kWBlock) void wide_filter_hashes(const int64_t* __r
             const int64_t v = t0 + u * T + tid;
             x[u] = __builtin_nontemporal_load(hv + (v < n_vec ? v : n_vec - 1));
         }
+        if (R) rg.span(head + 2 * t0, head + 2 * (t0 + T * kWideU), rl, rh);
         int64_t h[kWideU][2];
         bool c[kWideU][2];
         bool any = false;
@@ -152,8 +195,9 @@ __global__ __launch_bounds__(kWBlock) void wide_filter_hashes(const int64_t* __r
             const bool ok = t0 + u * T + tid < n_vec;
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
+                const int64_t i = head + (t0 + u * T + tid) * 2 + e;
                 h[u][e] = scramble(r0, r1, x[u][e]);
-                c[u][e] = ok && h[u][e] <= bound;
+                c[u][e] = ok && h[u][e] <= (R ? rg.at(i, rl, rh) : bound);
                 any |= c[u][e];
             }
         }
@@ -167,12 +211,12 @@ __global__ __launch_bounds__(kWBlock) void wide_filter_hashes(const int64_t* __r
     for (int64_t i0 = 0; i0 < head; i0 += T) {
         const int64_t i = i0 + tid;
         const int64_t hh = i < head ? scramble(r0, r1, hashes[i]) : 0;
-        out.push(i < head && hh <= bound, hh, i);
+        out.push(i < head && hh <= (R ? rg.at(i, 0, R - 1) : bound), hh, i);
     }
     for (int64_t i0 = head + 2 * n_vec; i0 < n; i0 += T) {
         const int64_t i = i0 + tid;
         const int64_t hh = i < n ? scramble(r0, r1, hashes[i]) : 0;
-        out.push(i < n && hh <= bound, hh, i);
+        out.push(i < n && hh <= (R ? rg.at(i, 0, R - 1) : bound), hh, i);
     }
     out.flush_block(s_q, &s_base);
 }
@@ -182,12 +226,17 @@ __global__ __launch_bounds__(kWBlock) void wide_filter_hashes(const int64_t* __r
 __global__ __launch_bounds__(kWBlock) void wide_filter_uuid(const uint64_t* __restrict__ rows, int64_t n, int64_t r0,
                                                             int64_t r1, int64_t bound, int64_t* __restrict__ cand_h,
                                                             int64_t* __restrict__ cand_i,
-                                                            unsigned long long* __restrict__ counter, int64_t cap) {
+                                                            unsigned long long* __restrict__ counter, int64_t cap,
+                                                            const int64_t* __restrict__ rtab, int32_t R) {
     __shared__ int64_t sh_h[kWBlock / 64][WideOut::Q];
     __shared__ int64_t sh_i[kWBlock / 64][WideOut::Q];
     __shared__ uint32_t s_q[kWBlock / 64];
     __shared__ unsigned long long s_base;
+    __shared__ int64_t s_rs[kWMaxR + 1], s_rb[kWMaxR];
     WideOut out{sh_h[threadIdx.x >> 6], sh_i[threadIdx.x >> 6], 0u, cand_h, cand_i, counter, cap};
+    WRanges rg{s_rs, s_rb, R};
+    if (R) rg.load(rtab);
+    int32_t rl = 0, rh = 0;
     const int64_t T = (int64_t)gridDim.x * blockDim.x;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int64_t t0 = 0; t0 < n; t0 += T * kWideU) {
@@ -198,13 +247,15 @@ __global__ __launch_bounds__(kWBlock) void wide_filter_uuid(const uint64_t* __re
             a[u] = __builtin_nontemporal_load(rows + 2 * i);
             b[u] = __builtin_nontemporal_load(rows + 2 * i + 1);
         }
+        if (R) rg.span(t0, t0 + T * kWideU, rl, rh);
         int64_t h[kWideU];
         bool c[kWideU];
         bool any = false;
 #pragma unroll
         for (int u = 0; u < kWideU; ++u) {
+            const int64_t i = t0 + u * T + tid;
             h[u] = scramble(r0, r1, uuid_hash_code(a[u], b[u]));
-            c[u] = t0 + u * T + tid < n && h[u] <= bound;
+            c[u] = i < n && h[u] <= (R ? rg.at(i, rl, rh) : bound);
             any |= c[u];
         }
         if (__any(any)) {
@@ -363,6 +414,45 @@ __global__ __launch_bounds__(kWBlock) void wide_emit(const int64_t* __restrict__
     }
 }
 
+// The scheduled pass's proof (ordered mode): range r's bound B_r covered every element the
+// reference could admit in range r iff at least k distinct elements with h < B_r arrived before s_r
+// (the set's members count as arrived): the heap's maximum at s_r is then below B_r.  Over the merge
+// (set + the pass's candidates, in (h, key) order, `flags` = first of each run of one element), each
+// distinct element with first arrival a and hash h counts for the ranges r with range(a) < r and
+// B_r > h -- one difference-array interval per element, summed per workgroup in LDS.
+__global__ __launch_bounds__(kWBlock) void wide_verify(const int64_t* __restrict__ eh, const uint32_t* __restrict__ ev,
+                                                       const uint32_t* __restrict__ flags, int64_t N, int64_t m_old,
+                                                       const int64_t* __restrict__ cand_i,
+                                                       const int64_t* __restrict__ rtab, int32_t R,
+                                                       unsigned long long* __restrict__ diff) {
+    __shared__ int64_t s_rs[kWMaxR + 1], s_rb[kWMaxR];
+    __shared__ int s_d[kWMaxR + 1];
+    WRanges rg{s_rs, s_rb, R};
+    for (int t = threadIdx.x; t <= R; t += blockDim.x) s_d[t] = 0;
+    rg.load(rtab);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += stride) {
+        if (!flags[p]) continue;
+        int64_t a = INT64_MAX;  // the element's first arrival (-1: a set member)
+        for (int64_t q = p; q < N && (q == p || !flags[q]); ++q) {
+            const uint32_t e = ev[q];
+            a = std::min<int64_t>(a, (int64_t)e < m_old ? -1 : cand_i[(int64_t)e - m_old]);
+        }
+        const int64_t h = eh[p];
+        int32_t ra = -1;  // the range holding a
+        while (ra + 1 < R && s_rs[ra + 1] <= a) ++ra;
+        int32_t rh = -1;  // the last range whose bound exceeds h (bounds fall with r)
+        while (rh + 1 < R && s_rb[rh + 1] > h) ++rh;
+        if (ra + 1 <= rh) {
+            atomicAdd(&s_d[ra + 1], 1);
+            atomicAdd(&s_d[rh + 1], -1);
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t <= R; t += blockDim.x)
+        if (s_d[t]) atomicAdd(&diff[t], (unsigned long long)(int64_t)s_d[t]);
+}
+
 __global__ __launch_bounds__(kWBlock) void wide_iota(uint32_t* __restrict__ v, int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) v[i] = (uint32_t)i;
@@ -448,6 +538,15 @@ struct WideDistinct {
     bool arch_ok = true;
     std::vector<int64_t> arch_h;  // consumed candidates in arrival order
     std::vector<uint64_t> arch_k;
+    // ordered mode's scheduled pass: range table + verification counts (device [0, 2 kWMaxR + 1) the
+    // table, [kSchedCounts, + kWMaxR + 1) the counts; pinned staging alike), and the set before the pass
+    int64_t* sched = nullptr;
+    int64_t* hsched = nullptr;
+    int64_t* bk_h = nullptr;
+    uint64_t* bk_k = nullptr;
+    int64_t bk_cap = 0;
+    double sched_beta = 1.6;      // bound margin over the predicted k-th smallest hash
+    bool sched_on = true;
 };
 
 namespace {
@@ -684,7 +783,8 @@ hipError_t ensure_log(WideDistinct* d, int64_t need, hipStream_t st) {
 // one chunk [off, off + L) of the batch: filter (bound: the set's maximum, or `bound_in` when given),
 // rows, log, merge
 hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes, int64_t off, int64_t L,
-                        int64_t gbase, hipStream_t st, const int64_t* bound_in = nullptr) {
+                        int64_t gbase, hipStream_t st, const int64_t* bound_in = nullptr, int32_t R = 0,
+                        int64_t* c_out = nullptr) {
     const uint64_t* rows = (const uint64_t*)keys + (size_t)off * d->words;
     const int64_t* hv = hashes ? hashes + off : nullptr;
     hipError_t e;
@@ -713,10 +813,10 @@ hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes
             if (d->timer) d->timer->mark(st);
             if (d->src == kWideSrcHashes)
                 hipLaunchKernelGGL(wide_filter_hashes, dim3(g), dim3(kWBlock), 0, st, hv, L, d->r0, d->r1, bound,
-                                   d->cand_h, d->cand_i, (unsigned long long*)d->ctl, d->cand_cap);
+                                   d->cand_h, d->cand_i, (unsigned long long*)d->ctl, d->cand_cap, d->sched, R);
             else
                 hipLaunchKernelGGL(wide_filter_uuid, dim3(g), dim3(kWBlock), 0, st, rows, L, d->r0, d->r1, bound,
-                                   d->cand_h, d->cand_i, (unsigned long long*)d->ctl, d->cand_cap);
+                                   d->cand_h, d->cand_i, (unsigned long long*)d->ctl, d->cand_cap, d->sched, R);
             if (d->timer) d->timer->mark(st);
             if ((e = hipGetLastError())) return e;
             if ((e = read_ctl(d, st))) return e;
@@ -725,6 +825,7 @@ hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes
             if ((e = ensure_cand(d, c, st))) return e;  // more candidates than room: again, with room
         }
     }
+    if (c_out) *c_out = c;
     if (c == 0) return hipSuccess;
     hipLaunchKernelGGL(wide_gather_rows, dim3(wgrid(c * d->words, 8192)), dim3(kWBlock), 0, st, (const uint64_t*)keys +
                        (size_t)off * d->words, d->cand_i, c, d->words, d->cand_k);
@@ -740,6 +841,98 @@ hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes
     if ((e = merge_cands(d, c, st))) return e;
     if (d->ordered) d->exact = !d->tied;  // an uncut boundary bucket leaves one possible set
     return hipSuccess;
+}
+
+// Ordered mode over a long rest (the set full): ONE filter pass whose bound falls with the index,
+// like rsv_distinct.hip's scheduled pass.  Range 0 = [0, seen) of the rest takes the set's maximum
+// (exact: the heap's maximum never rises); range r >= 1 = [(2^r - 1) seen, (2^(r+1) - 1) seen)
+// takes B_r = MIN + (top - MIN) beta / 2^r -- the scrambled hash is uniform, so the k-th smallest of
+// the 2^r seen lengths before the range sits near (top - MIN) / 2^r.  Every candidate is logged and
+// merged as in a chunk; wide_verify then proves each range's bound (>= k distinct elements under
+// B_r arrived before it, so the log holds every element the reference can admit there).  A failed
+// proof restores the set and the log, and the chunk loop takes the rest (*ok = false).
+hipError_t sample_sched(WideDistinct* d, const void* keys, const int64_t* hashes, int64_t off, int64_t rest,
+                        int64_t gbase, hipStream_t st, bool* ok) {
+    *ok = false;
+    hipError_t e;
+    if (!d->sched) {
+        if ((e = walloc((void**)&d->sched, kSchedWords * 8))) return e;
+        if ((e = pool_host_alloc((void**)&d->hsched, kSchedWords * 8, hipHostMallocDefault))) return e;
+    }
+    if (d->bk_cap < d->k) {
+        if ((e = wgrow((void**)&d->bk_h, 0, (size_t)d->k * 8, false, st))) return e;
+        if ((e = wgrow((void**)&d->bk_k, 0, (size_t)d->k * d->words * 8, false, st))) return e;
+        d->bk_cap = d->k;
+    }
+    // a bounded log is replayed first (as sample_chunk would), so the state saved below is the one
+    // the pass starts from
+    if (d->log_n > 0 && d->log_n + std::min<int64_t>(rest, 8 * (int64_t)d->k + 4096) > d->log_limit)
+        if ((e = replay_log(d, st))) return e;
+    // the ranges (host; the pinned table's previous contents were consumed by a synchronized pass)
+    const int64_t seen = std::max<int64_t>(d->seen, 1);
+    const uint64_t span = (uint64_t)d->top - (uint64_t)INT64_MIN;
+    int64_t* rs = d->hsched;
+    int32_t R = 1;  // ranges [0, R): s_r = 2 s_(r-1) + seen = (2^r - 1) seen
+    rs[0] = 0;
+    while (R < kWMaxR && rs[R - 1] < (rest - seen) / 2) {
+        rs[R] = 2 * rs[R - 1] + seen;
+        ++R;
+    }
+    rs[R] = rest;
+    int64_t* rb = rs + R + 1;
+    rb[0] = d->top;
+    for (int32_t r = 1; r < R; ++r) {
+        const double frac = d->sched_beta / (double)((int64_t)1 << r);
+        rb[r] = frac >= 1.0 ? d->top : (int64_t)((uint64_t)INT64_MIN + (uint64_t)((double)span * frac));
+    }
+    // room for the expected candidates (each range's length x the share of hashes under its bound,
+    // +25 %): an overflow would run the whole filter again
+    double expect = 0;
+    for (int32_t r = 0; r < R; ++r)
+        expect += (double)(rs[r + 1] - rs[r]) * ((double)((uint64_t)rb[r] - (uint64_t)INT64_MIN) / 18446744073709551616.0);
+    if ((e = ensure_cand(d, (int64_t)(1.25 * expect) + 65536, st))) return e;
+    if ((e = hipMemcpyAsync(d->sched, rs, (size_t)(2 * R + 1) * 8, hipMemcpyHostToDevice, st))) return e;
+    if ((e = hipMemsetAsync(d->sched + kSchedCounts, 0, (kWMaxR + 1) * 8, st))) return e;
+    // the set and the scalars before the pass
+    const int64_t m0 = d->m, top0 = d->top, log0 = d->log_n;
+    const bool tied0 = d->tied, exact0 = d->exact;
+    if ((e = hipMemcpyAsync(d->bk_h, d->set_h, (size_t)m0 * 8, hipMemcpyDeviceToDevice, st))) return e;
+    if ((e = hipMemcpyAsync(d->bk_k, d->set_k, (size_t)m0 * d->words * 8, hipMemcpyDeviceToDevice, st))) return e;
+    int64_t c = 0;
+    if ((e = sample_chunk(d, keys, hashes, off, rest, gbase, st, nullptr, R, &c))) return e;
+    bool good = false;
+    if (c > 0 && d->m == d->k) {  // the merge's sorted entries are still in eh1 / ev1 / flags
+        const int64_t N = m0 + c;
+        hipLaunchKernelGGL(wide_verify, dim3(wgrid(N, 4096)), dim3(kWBlock), 0, st, d->eh1, d->ev1, d->flags, N, m0,
+                           d->cand_i, d->sched, R, (unsigned long long*)(d->sched + kSchedCounts));
+        if ((e = hipGetLastError())) return e;
+        if ((e = hipMemcpyAsync(d->hsched + kSchedCounts, d->sched + kSchedCounts, (size_t)(R + 1) * 8, hipMemcpyDeviceToHost, st)))
+            return e;
+        if ((e = hipStreamSynchronize(st))) return e;
+        good = true;
+        int64_t cnt = 0;
+        for (int32_t r = 0; r < R; ++r) {
+            cnt += d->hsched[kSchedCounts + r];
+            if (r >= 1 && cnt < d->k) good = false;
+        }
+    }
+    const bool debug = std::getenv("RSV_WIDE_SCHED_DEBUG") != nullptr;  // (read per pass: tests toggle it)
+    if (debug)
+        std::fprintf(stderr, "[rsv wide sched] rest=%lld ranges=%d candidates=%lld proof=%s\n", (long long)rest, R,
+                     (long long)c, good ? "ok" : "failed");
+    if (good) {
+        *ok = true;
+        return hipSuccess;
+    }
+    // the proof failed: the set and the log as before the pass
+    if ((e = hipMemcpyAsync(d->set_h, d->bk_h, (size_t)m0 * 8, hipMemcpyDeviceToDevice, st))) return e;
+    if ((e = hipMemcpyAsync(d->set_k, d->bk_k, (size_t)m0 * d->words * 8, hipMemcpyDeviceToDevice, st))) return e;
+    d->m = m0;
+    d->top = top0;
+    d->tied = tied0;
+    d->exact = exact0;
+    d->log_n = log0;
+    return hipStreamSynchronize(st);
 }
 
 int fail_hip(hipError_t e, const char* what) {
@@ -809,6 +1002,9 @@ WideDistinct* wide_create(int32_t k, int key_width, int src, int64_t r0, int64_t
     if (const char* v = std::getenv("RSV_ORDERED_LOG_LIMIT"))  // test hook: force eager replays
         d->log_limit = std::max<int64_t>(1, std::atoll(v));
     if (ordered) d->rep.reset(k, d->words);
+    if (const char* v = std::getenv("RSV_WIDE_SCHED")) d->sched_on = std::atoi(v) != 0;  // test hook: the chunk loop only
+    if (const char* v = std::getenv("RSV_WIDE_SCHED_BETA"))  // test hook: tight bounds, failed proofs
+        d->sched_beta = std::atof(v);
     hipError_t e = walloc((void**)&d->ctl, 8 * 8);
     if (e == hipSuccess) e = pool_host_alloc((void**)&d->hctl, 8 * 8, hipHostMallocDefault);
     if (e != hipSuccess) {
@@ -825,6 +1021,10 @@ void wide_destroy(WideDistinct* d) {
     void* ps[] = {d->set_h, d->set_k, d->set_h2, d->set_k2, d->cand_h, d->cand_i, d->cand_k, d->eh0, d->eh1,
                   d->ev0, d->ev1, d->flags, d->pos, d->temp, d->ctl, d->log_h, d->log_g, d->log_k};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
+    pool_device_free(d->sched);
+    pool_device_free(d->bk_h);
+    pool_device_free(d->bk_k);
+    pool_host_free(d->hsched);
     pool_host_free(d->hctl);
     delete d;
 }
@@ -847,6 +1047,17 @@ int wide_sample_device(WideDistinct* d, const void* keys, const int64_t* hashes,
     bool predicted = false;
     for (int64_t off = 0; off < n;) {
         const int64_t rest = n - off;
+        if (d->ordered && d->sched_on && d->k >= kSchedMinK && d->m == d->k && !predicted && rest > 4 * d->seen) {
+            predicted = true;
+            bool ok = false;
+            if (hipError_t e = sample_sched(d, keys, hashes, off, rest, seen0, st, &ok))
+                return fail_hip(e, "distinct sample");
+            if (ok) {
+                d->seen += rest;
+                break;
+            }
+            continue;  // a range's bound was short: the chunk loop below covers the same rest
+        }
         if (!d->ordered && d->m == d->k && !predicted && rest > 4 * d->seen) {
             // Set mode, a long rest: ONE pass with the bound the rest's bottom-k is predicted under.
             // The scrambled hash is uniform, so the k-th smallest of D distinct values sits near

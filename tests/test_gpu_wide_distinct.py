@@ -137,6 +137,53 @@ def test_wide_distinct_uuid_default_hash(cuda, k):
     assert _sorted_rows(got) == want
 
 
+@pytest.mark.parametrize("k", [1, 100, 5000])
+@pytest.mark.parametrize("hkind", ["random", "collide", "uuid"])
+def test_wide_sched_pass(cuda, capfd, monkeypatch, k, hkind):
+    """Ordered mode over one long batch takes the scheduled pass (falling per-range bounds, proved
+    by wide_verify): equal to the oracle, to the chunk loop (RSV_WIDE_SCHED=0), and -- with bounds
+    made too tight (RSV_WIDE_SCHED_BETA) -- the failed proof restores the set and the log and the
+    chunk loop gives the same set."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    monkeypatch.setenv("RSV_WIDE_SCHED_DEBUG", "1")
+    n = 400_000
+    ids = _stream(n, 7 * k + len(hkind))
+    rows = _rows(ids, 16)
+    uuid = hkind == "uuid"
+    hs = None if uuid else _hashes(ids, hkind)
+    want, _ = _expect(k, 5, 16, rows, hs, uuid=uuid)
+    rd = torch.from_numpy(rows).to(cuda)
+    hd = None if uuid else torch.from_numpy(hs).to(cuda)
+
+    def run(**env):
+        for key, v in env.items():
+            monkeypatch.setenv(key, v)
+        d = Sampler.distinct(k, key_type="bytes16", seed=5)() if uuid else \
+            Sampler.distinct(k, key_type="bytes16", seed=5)(hash=lambda b: 0)
+        assert d.is_ordered
+        d.sample_all(rd, hashes=hd)
+        got = _sorted_rows(d.result())
+        for key in env:
+            monkeypatch.delenv(key)
+        return got, capfd.readouterr().err
+
+    got, err = run()
+    assert got == want
+    sched = k >= 64  # (smaller k keep the chunk loop: rsv_wide.hip kSchedMinK)
+    assert ("[rsv wide sched]" in err) == sched, err
+    if sched and hkind != "collide":  # (97 hash values: no k-th smallest falls below a predicted bound)
+        assert "proof=ok" in err, err
+    got0, err0 = run(RSV_WIDE_SCHED="0")
+    assert got0 == want and "[rsv wide sched]" not in err0
+    got1, err1 = run(RSV_WIDE_SCHED_BETA="0.02")
+    assert got1 == want
+    if sched:
+        assert "proof=failed" in err1, err1
+
+
 def test_wide_distinct_eager_replays(cuda, monkeypatch):
     """A small log limit forces the ordered log to be replayed mid-batch (several times)."""
     import torch
