@@ -354,6 +354,35 @@ struct HostValuesWide {
             max_hash = hh[1];
         }
     }
+    // RandomValues.sample for an element known to be the FIRST occurrence of its key since the
+    // replica's state (flagged on the device): no member carries its key, so `contains` is false and
+    // the element set is not consulted; a later repeat of it could never be admitted (the heap's
+    // maximum never rises), so repeats are simply skipped.  The table is stale until table_rebuild().
+    void sample_first(int64_t h, const uint64_t* r) {
+        if (n < k) {
+            pq_add(alloc(h, r), h);
+            if (h > max_hash) max_hash = h;
+        } else if (h < max_hash) {
+            free_slots.push_back(pq_dequeue());
+            pq_add(alloc(h, r), h);
+            max_hash = hh[1];
+        }
+    }
+    void table_rebuild() {
+        uint64_t cap = 16;
+        while (cap < (uint64_t)(n + 1) * 2 + 2) cap *= 2;
+        rehash(cap);
+    }
+    // the members as (hash, row) in heap order (no sort: for the device, which orders them itself)
+    void members_heap(std::vector<int64_t>& out_h, std::vector<uint64_t>& out_rows) const {
+        out_h.resize((size_t)n);
+        out_rows.resize((size_t)(n * words));
+        for (int64_t i = 0; i < n; ++i) {
+            const int32_t s = hs[(size_t)i + 1];
+            out_h[(size_t)i] = hh[(size_t)i + 1];
+            std::copy(row(s), row(s) + words, out_rows.begin() + (std::ptrdiff_t)(i * words));
+        }
+    }
     // the members as (hash, row) ascending by (hash, row words) -- the device set's order
     void members(std::vector<int64_t>& out_h, std::vector<uint64_t>& out_rows) const {
         std::vector<int32_t> ord(hs.begin() + 1, hs.begin() + 1 + n);

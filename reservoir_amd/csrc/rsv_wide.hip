@@ -24,6 +24,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -472,6 +473,21 @@ __global__ __launch_bounds__(kWBlock) void wide_log_permute(const uint32_t* __re
     }
 }
 
+// first-occurrence flags of the log for the host replay: the entries [members | the log in arrival
+// order] sorted stably by h and, within a run of equal h, stably by the key words, so each key's
+// entries sit together in entry order; a log entry is flagged when it heads its key's group (no
+// member and no earlier log entry carries the key).  flag[t] for log position t (arrival order).
+__global__ __launch_bounds__(kWBlock) void wide_mark_first(const int64_t* __restrict__ eh, const uint32_t* __restrict__ ev,
+                                                           int64_t N, WRows R, uint32_t* __restrict__ flag) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += stride) {
+        const uint32_t e = ev[p];
+        if ((int64_t)e < R.m) continue;
+        const bool head = p == 0 || eh[p] != eh[p - 1] || row_cmp(R(ev[p - 1]), R(e), R.words) != 0;
+        flag[(int64_t)e - R.m] = head ? 1u : 0u;
+    }
+}
+
 // packed row: [key words (k x words) | hashes (k) | n, count, tied, max_hash, log_retained, ordered]
 __global__ __launch_bounds__(kWBlock) void wide_export_row(const int64_t* __restrict__ set_h,
                                                            const uint64_t* __restrict__ set_k, int64_t m, int64_t k,
@@ -546,6 +562,7 @@ struct WideDistinct {
     uint64_t* bk_k = nullptr;
     int64_t bk_cap = 0;
     double sched_beta = 1.6;      // bound margin over the predicted k-th smallest hash
+    int64_t first_min = 4096;     // logs at least this long replay through first-occurrence flags
     bool sched_on = true;
 };
 
@@ -690,20 +707,24 @@ hipError_t merge_cands(WideDistinct* d, int64_t c, hipStream_t st) {
     return hipSuccess;
 }
 
-// the device set := the replica's members (ascending (h, key words))
+// the device set := the replica's members, put in ascending (h, key words) order on the device (the
+// merge of an empty set with them as candidates; a host sort of 65536 rows took ~10 ms)
 hipError_t upload_replica(WideDistinct* d, hipStream_t st) {
     std::vector<int64_t> hs;
     std::vector<uint64_t> rows;
-    d->rep.members(hs, rows);
+    d->rep.members_heap(hs, rows);
+    const int64_t nm = (int64_t)hs.size();
     hipError_t e;
-    if ((e = ensure_set(d, (int64_t)hs.size(), st))) return e;
-    d->m = (int64_t)hs.size();
-    if (d->m) {
-        if ((e = hipMemcpyAsync(d->set_h, hs.data(), hs.size() * 8, hipMemcpyHostToDevice, st))) return e;
-        if ((e = hipMemcpyAsync(d->set_k, rows.data(), rows.size() * 8, hipMemcpyHostToDevice, st))) return e;
-        d->top = hs.back();
-    }
-    return hipStreamSynchronize(st);  // the host vectors are the copies' sources
+    if ((e = ensure_set(d, nm, st))) return e;
+    d->m = 0;
+    if (!nm) return hipSuccess;
+    if ((e = ensure_cand(d, nm, st))) return e;
+    if ((e = hipMemcpyAsync(d->cand_h, hs.data(), (size_t)nm * 8, hipMemcpyHostToDevice, st))) return e;
+    if ((e = hipMemcpyAsync(d->cand_k, rows.data(), (size_t)nm * d->words * 8, hipMemcpyHostToDevice, st))) return e;
+    const bool tied = d->tied;
+    if ((e = merge_cands(d, nm, st))) return e;  // synchronizes (its control words): hs / rows may go
+    d->tied = tied;
+    return hipSuccess;
 }
 
 // the replica from the device set (after a merge replaced it): its members inserted in (h, key) order
@@ -743,15 +764,72 @@ hipError_t log_to_host(WideDistinct* d, std::vector<int64_t>& oh, std::vector<ui
     return hipStreamSynchronize(st);
 }
 
+// First-occurrence flags of the log (already in arrival order in cand_h / cand_k, log_to_host):
+// entries [the replica's members | the log] through the merge's sort (stable radix by h, runs of
+// equal h stably by the key words, or the comparison sort for runs > kRunMax), then wide_mark_first.
+hipError_t first_flags(WideDistinct* d, std::vector<uint32_t>& flags, hipStream_t st) {
+    const int64_t n = d->log_n;
+    std::vector<int64_t> mh;
+    std::vector<uint64_t> mk;
+    d->rep.members_heap(mh, mk);  // (any order: the sort below groups the keys)
+    const int64_t nm = (int64_t)mh.size(), N = nm + n;
+    hipError_t e;
+    if ((e = ensure_set(d, nm, st))) return e;
+    if ((e = ensure_merge(d, N, st))) return e;
+    if (nm) {
+        if ((e = hipMemcpyAsync(d->set_h2, mh.data(), (size_t)nm * 8, hipMemcpyHostToDevice, st))) return e;
+        if ((e = hipMemcpyAsync(d->set_k2, mk.data(), (size_t)nm * d->words * 8, hipMemcpyHostToDevice, st))) return e;
+    }
+    const WRows R{d->set_k2, d->cand_k, nm, d->words};
+    const unsigned g = wgrid(N, 4096);
+    hipLaunchKernelGGL(wide_merge_init, dim3(g), dim3(kWBlock), 0, st, d->set_h2, d->cand_h, nm, N, d->eh0, d->ev0);
+    size_t tb = d->temp_bytes;
+    if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->eh0, d->eh1, d->ev0, d->ev1, (size_t)N, 0, 64, st))) return e;
+    if ((e = hipMemsetAsync(d->ctl, 0, 8 * 8, st))) return e;
+    hipLaunchKernelGGL(wide_run_fix, dim3(g), dim3(kWBlock), 0, st, d->eh1, d->ev1, N, R, d->ctl);
+    if ((e = read_ctl(d, st))) return e;
+    if (d->hctl[1]) {  // a run longer than kRunMax: the (stable) comparison sort over (h, key words)
+        size_t mb = 0;
+        const WLess less{d->eh0, R};
+        if ((e = rocprim::merge_sort(nullptr, mb, d->ev1, d->ev1, (size_t)N, less, st))) return e;
+        if ((e = ensure_temp(d, mb, st))) return e;
+        hipLaunchKernelGGL(wide_iota, dim3(g), dim3(kWBlock), 0, st, d->ev0, N);
+        mb = d->temp_bytes;
+        if ((e = rocprim::merge_sort(d->temp, mb, d->ev0, d->ev1, (size_t)N, less, st))) return e;
+        hipLaunchKernelGGL(wide_gather_h, dim3(g), dim3(kWBlock), 0, st, d->eh0, d->ev1, N, d->eh1);
+    }
+    hipLaunchKernelGGL(wide_mark_first, dim3(g), dim3(kWBlock), 0, st, d->eh1, d->ev1, N, R, d->pos);
+    if ((e = hipGetLastError())) return e;
+    flags.resize((size_t)n);
+    if ((e = hipMemcpyAsync(flags.data(), d->pos, (size_t)n * 4, hipMemcpyDeviceToHost, st))) return e;
+    return hipStreamSynchronize(st);
+}
+
 // Consume the log: replay it in arrival order through the replica (the reference's sequential
-// RandomValues), archive it if retained, and make the device set the replica's (exact) set.
+// RandomValues), archive it if retained, and make the device set the replica's (exact) set.  Long
+// logs replay first occurrences only, through the heap alone (sample_first: no element set).
 hipError_t replay_log(WideDistinct* d, hipStream_t st) {
     hipError_t e;
     if (d->rep_stale && (e = rebuild_replica(d, st))) return e;
     std::vector<int64_t> oh;
     std::vector<uint64_t> ok;
+    const bool first = d->log_n > 0 && d->log_n >= d->first_min;
+    const int64_t n_log = d->log_n;
+    const auto t0 = std::chrono::steady_clock::now();
     if ((e = log_to_host(d, oh, ok, st))) return e;
-    for (size_t t = 0; t < oh.size(); ++t) d->rep.sample(oh[t], ok.data() + t * d->words);
+    const auto t1 = std::chrono::steady_clock::now();
+    auto t2 = t1;
+    if (first) {
+        std::vector<uint32_t> fl;
+        if ((e = first_flags(d, fl, st))) return e;
+        t2 = std::chrono::steady_clock::now();
+        for (size_t t = 0; t < oh.size(); ++t)
+            if (fl[t]) d->rep.sample_first(oh[t], ok.data() + t * d->words);
+        d->rep.table_rebuild();
+    } else {
+        for (size_t t = 0; t < oh.size(); ++t) d->rep.sample(oh[t], ok.data() + t * d->words);
+    }
+    const auto t3 = std::chrono::steady_clock::now();
     if (d->retain && d->arch_ok) {
         if ((int64_t)(d->arch_h.size() + oh.size()) > ((int64_t)1 << 27)) {
             d->arch_ok = false;
@@ -765,6 +843,12 @@ hipError_t replay_log(WideDistinct* d, hipStream_t st) {
     d->log_n = 0;
     if ((e = upload_replica(d, st))) return e;
     d->exact = true;
+    if (std::getenv("RSV_REPLAY_DEBUG")) {
+        const auto t4 = std::chrono::steady_clock::now();
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        std::fprintf(stderr, "[rsv wide replay] log=%lld first=%d to_host_us=%.1f flags_us=%.1f run_us=%.1f upload_us=%.1f\n",
+                     (long long)n_log, (int)first, us(t0, t1), us(t1, t2), us(t2, t3), us(t3, t4));
+    }
     return hipSuccess;
 }
 
@@ -1005,6 +1089,8 @@ WideDistinct* wide_create(int32_t k, int key_width, int src, int64_t r0, int64_t
     if (const char* v = std::getenv("RSV_WIDE_SCHED")) d->sched_on = std::atoi(v) != 0;  // test hook: the chunk loop only
     if (const char* v = std::getenv("RSV_WIDE_SCHED_BETA"))  // test hook: tight bounds, failed proofs
         d->sched_beta = std::atof(v);
+    if (const char* v = std::getenv("RSV_FIRST_MIN"))  // test hook: which replay form serves a log
+        d->first_min = std::max<int64_t>(0, std::atoll(v));
     hipError_t e = walloc((void**)&d->ctl, 8 * 8);
     if (e == hipSuccess) e = pool_host_alloc((void**)&d->hctl, 8 * 8, hipHostMallocDefault);
     if (e != hipSuccess) {

@@ -6,7 +6,9 @@
 // (hash and element arrays, size, maxHash) must be identical.  Set-based calls after a heap-only
 // run (rebuild of the element set) are interleaved.  A third replica, HostValuesWide (the byte-key
 // form of rsv_wide.hip) fed each key as the two-word row [key, ~key], must hold the same heap entry
-// for entry (hash, and the row's first word = the key).  Exit 0 and "ok <cases>" on success.
+// for entry (hash, and the row's first word = the key); a fourth, HostValuesWide fed only the flagged
+// first occurrences through sample_first (heap only, its element table rebuilt afterwards -- the
+// wide replay's first-occurrence form), too.  Exit 0 and "ok <cases>" on success.
 //   g++ -std=c++17 -O2 -I reservoir_amd/csrc tests/cpp/test_host_replay.cpp -o test_host_replay
 #include <cstdio>
 #include <cstring>
@@ -46,10 +48,11 @@ int main() {
                 std::mt19937_64 rng(seed * 7919 + (uint64_t)k * 31 + (uint64_t)buckets);
                 const int64_t universe = std::max<int64_t>(4, 6 * k);  // keys repeat across segments
                 rsv::HostValues a, b;
-                rsv::HostValuesWide cw;
+                rsv::HostValuesWide cw, cf;
                 a.reset(k);
                 b.reset(k);
                 cw.reset(k, 2);
+                cf.reset(k, 2);
                 for (int seg = 0; seg < 12; ++seg) {
                     const int64_t c = (int64_t)(rng() % (uint64_t)(3 * k + 50));
                     std::vector<int64_t> ek((size_t)c), eh((size_t)c);
@@ -68,6 +71,8 @@ int main() {
                         for (int64_t t = 0; t < c; ++t) {
                             a.sample(ek[(size_t)t], eh[(size_t)t]);
                             b.sample(ek[(size_t)t], eh[(size_t)t]);
+                            const uint64_t row[2] = {(uint64_t)ek[(size_t)t], ~(uint64_t)ek[(size_t)t]};
+                            cf.sample(eh[(size_t)t], row);
                         }
                     } else {
                         std::unordered_set<int64_t> seen;
@@ -77,8 +82,14 @@ int main() {
                         a.sample_run(c, [&](int64_t t) { return ek[(size_t)t]; }, [&](int64_t t) { return eh[(size_t)t]; });
                         b.sample_run_unique(c, first.data(), [&](int64_t t) { return ek[(size_t)t]; },
                                             [&](int64_t t) { return eh[(size_t)t]; });
+                        for (int64_t t = 0; t < c; ++t) {
+                            if (!first[(size_t)t]) continue;
+                            const uint64_t row[2] = {(uint64_t)ek[(size_t)t], ~(uint64_t)ek[(size_t)t]};
+                            cf.sample_first(eh[(size_t)t], row);
+                        }
+                        cf.table_rebuild();
                     }
-                    if (!same(a, b) || !same_wide(a, cw)) {
+                    if (!same(a, b) || !same_wide(a, cw) || !same_wide(a, cf)) {
                         std::printf("MISMATCH k=%lld buckets=%lld seed=%llu segment=%d\n", (long long)k,
                                     (long long)buckets, (unsigned long long)seed, seg);
                         return 1;

@@ -202,6 +202,31 @@ def test_wide_distinct_eager_replays(cuda, monkeypatch):
     assert _sorted_rows(d.result()) == want
 
 
+@pytest.mark.parametrize("first_min", ["0", "1000000000"])
+@pytest.mark.parametrize("log_limit", [None, "3000"])
+def test_wide_first_occurrence_replay(cuda, monkeypatch, first_min, log_limit):
+    """The ordered replay through first-occurrence flags (heap only, no element set: RSV_FIRST_MIN=0)
+    and through the replica's element set (RSV_FIRST_MIN huge) both equal the oracle -- colliding
+    hashes, keys repeating within and across batches and logs, eager replays mid-batch."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    monkeypatch.setenv("RSV_FIRST_MIN", first_min)
+    if log_limit:
+        monkeypatch.setenv("RSV_ORDERED_LOG_LIMIT", log_limit)
+    ids = _stream(150_000, 21)
+    ids = np.concatenate([ids, ids[:40_000]])  # whole-log repeats
+    rows = _rows(ids, 24)
+    hs = _hashes(ids, "collide")
+    want, _ = _expect(300, 4, 24, rows, hs)
+    d = Sampler.distinct(300, key_type="bytes24", seed=4)(hash=lambda b: 0)
+    rd, hd = torch.from_numpy(rows).to(cuda), torch.from_numpy(hs).to(cuda)
+    for a in range(0, rows.shape[0], 47_000):
+        d.sample_all(rd[a:a + 47_000], hashes=hd[a:a + 47_000])
+    assert _sorted_rows(d.result()) == want
+
+
 def test_wide_distinct_reusable_and_long_runs(cuda):
     """A reusable sampler (result() between batches), and one hash value for every key: runs of
     equal hash far above 64 entries take the comparison-sort merge."""
