@@ -876,7 +876,7 @@ hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes
     // bounded log: replay what it holds before this chunk's candidates take the scratch buffers
     if (d->ordered && d->log_n > 0 && d->log_n + std::min<int64_t>(L, 8 * (int64_t)d->k + 4096) > d->log_limit)
         if ((e = replay_log(d, st))) return e;
-    if (d->m < d->k) {  // still filling: every element is a candidate
+    if (d->m < d->k && !bound_in) {  // still filling, no predicted bound: every element is a candidate
         if ((e = ensure_cand(d, L, st))) return e;
         if (d->src == kWideSrcHashes)
             hipLaunchKernelGGL(wide_hash_all<kWideSrcHashes>, dim3(wgrid(L, 8192)), dim3(kWBlock), 0, st, hv, rows, L,
@@ -1143,6 +1143,23 @@ int wide_sample_device(WideDistinct* d, const void* keys, const int64_t* hashes,
                 break;
             }
             continue;  // a range's bound was short: the chunk loop below covers the same rest
+        }
+        if (!d->ordered && d->m == 0 && d->seen == 0 && !predicted && rest >= 64 * (int64_t)d->k) {
+            // Set mode, a fresh sampler and a long batch: no filling chunk -- ONE pass under the bound
+            // the batch's k-th smallest hash is predicted under if at least 1 / 2.5 of it is distinct
+            // (uniform scrambled hashes: k / D of the range).  Proved like the pass below: a full
+            // set whose maximum is <= B saw every element under it; else the chunk loop redoes the
+            // batch (what the pass merged is seen again: duplicates merge away).
+            predicted = true;
+            const double frac = 2.5 * (double)d->k / (double)rest;
+            const int64_t B = (int64_t)((uint64_t)INT64_MIN + (uint64_t)(18446744073709551616.0 * frac));
+            if (hipError_t e = sample_chunk(d, keys, hashes, off, rest, seen0, st, &B))
+                return fail_hip(e, "distinct sample");
+            if (d->m == d->k && d->top <= B) {
+                d->seen += rest;
+                break;
+            }
+            continue;
         }
         if (!d->ordered && d->m == d->k && !predicted && rest > 4 * d->seen) {
             // Set mode, a long rest: ONE pass with the bound the rest's bottom-k is predicted under.
