@@ -88,15 +88,18 @@ def c3(dev):
     # line probes, profiles/r05/gather_line_probe_time.jsonl: both 64-B halves of 32 lines cost what
     # one half twice costs), so a stream's winners cost 128 B per DISTINCT line: 64 uniform positions
     # without replacement in 256 lines touch 256 (1 - C(4080, 64) / C(4096, 64)) ~ 56.6 of them.
+    # Plus the output rows (k keys per stream) and the offsets, so the algorithmic bytes and the PMC
+    # traffic (reads + writes) count the same things.
     lines = 256.0 * (1.0 - math.exp(sum(math.log((L - 16 - q) / (L - q)) for q in range(k))))
-    line_bytes = S * lines * 128
+    line_bytes = S * lines * 128 + S * k * 8 + (S + 1) * 8
     traffic = _pmc_traffic("c3")
     hbm = {"bound": "hbm", "achieved": round(line_bytes / t / 1e9, 1), "peak": HBM, "unit": "GB/s",
            "frac": round(line_bytes / t / 1e9 / HBM, 4), "traffic": traffic,
            "kernel": "k2_segmented",
            "bytes_per_launch": round(line_bytes), "lines_per_stream": round(lines, 2),
            "note": "algorithmic bytes = the winners' distinct 128-B lines (the fetch granule of a random 8-B "
-                   "load); traffic = HBM bytes per launch from PMC (profiles/r05)"}
+                   "load) + the k-key output rows + offsets; traffic = HBM bytes per launch from PMC "
+                   "(profiles/r05: 128 B x TCC_EA0_RDREQ + WRITE_SIZE)"}
     return {"config": "C3 segmented 2^20 x 4096, k=64", "elements": n, "seconds": t,
             "Gelem_s": n / t / 1e9,
             "roofline": hbm,
