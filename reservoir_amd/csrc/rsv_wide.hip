@@ -974,6 +974,9 @@ hipError_t sample_sched(WideDistinct* d, const void* keys, const int64_t* hashes
     double expect = 0;
     for (int32_t r = 0; r < R; ++r)
         expect += (double)(rs[r + 1] - rs[r]) * ((double)((uint64_t)rb[r] - (uint64_t)INT64_MIN) / 18446744073709551616.0);
+    // a set whose maximum sits high in the hash range (few distinct keys beyond k) would make most of
+    // the rest candidates: the chunk loop bounds each chunk's instead
+    if (expect > 32.0 * (double)d->k + (double)(1 << 22)) return hipSuccess;
     if ((e = ensure_cand(d, (int64_t)(1.25 * expect) + 65536, st))) return e;
     if ((e = hipMemcpyAsync(d->sched, rs, (size_t)(2 * R + 1) * 8, hipMemcpyHostToDevice, st))) return e;
     if ((e = hipMemsetAsync(d->sched + kSchedCounts, 0, (kWMaxR + 1) * 8, st))) return e;
