@@ -35,6 +35,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
 from __future__ import annotations
 
 import argparse
+import collections
 import ctypes as C
 import json
 import mmap
@@ -358,6 +359,8 @@ def main() -> None:
                          "each timed launch carries ~10 us of marker packets and host calls")
     ap.add_argument("--serial", action="store_true",
                     help="one step at a time (no second sampler in flight) for the timed steps")
+    ap.add_argument("--depth", type=int, default=int(os.environ.get("RSV_BENCH_DEPTH", "2")),
+                    help="samplers in flight (each step still creates, samples, reads and closes its own)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the other hot-path configs (C3 segmented, C4 distinct, C2 on java_l, C5)")
@@ -441,21 +444,18 @@ def main() -> None:
         return finish(issue())
 
     def run_steps(count: int, depth: int):
-        """`count` steps; depth 2 keeps two samplers in flight: step t+1 is issued (its kernels queue
-        behind step t's on the stream) before step t's result() is read, so the host's result /
-        close / create turnaround overlaps the GPU's next step instead of idling it.  Every step
-        still creates its sampler, samples all keys, reads its result and closes."""
-        res, pending = None, None
+        """`count` steps with `depth` samplers in flight: step t + depth - 1 is issued (its kernels
+        queue behind the earlier steps' on the stream) before step t's result() is read, so the
+        host's result / close / create turnaround overlaps the GPU's next steps instead of idling
+        it.  Every step still creates its sampler, samples all keys, reads its result and closes."""
+        res = None
+        pending = collections.deque()
         for _ in range(count):
-            s = issue()
-            if depth == 1:
-                res = finish(s)
-                continue
-            if pending is not None:
-                res = finish(pending)
-            pending = s
-        if pending is not None:
-            res = finish(pending)
+            pending.append(issue())
+            if len(pending) >= depth:
+                res = finish(pending.popleft())
+        while pending:
+            res = finish(pending.popleft())
         return res
 
     def profile_read():
@@ -480,7 +480,7 @@ def main() -> None:
         t = torch.tensor([min(n_ramp, 10_000)], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         n_ramp = int(t.item())
-    depth = 1 if args.serial else 2
+    depth = 1 if args.serial else max(1, args.depth)
     run_steps(min(n_ramp, 10_000), depth)
     run_steps(args.warmup, depth)
     torch.cuda.synchronize()
