@@ -308,10 +308,61 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
         off = offsets[s];
         end = offsets[s + 1];
     }
-    const bool defer = k <= 64;
-    KeyT* pend_o = nullptr;
-    KeyT pend_v = 0;
-    bool pend_ok = false;
+    if (k <= 64) {
+        // Each stream's winner key is gathered at its end and stored TWO streams later, so every
+        // wave keeps two streams' gathers in flight (one was measured short of the memory
+        // concurrency the random-line rate needs: ~57 lines x 6k waves x 2 / 9 us of in-flight time).
+        // The stream loop is unrolled by two so stream t's key lives in register set t & 1 and no
+        // register copy of a load in flight exists (no s_waitcnt beyond the one for the store's data).
+        KeyT* po[2] = {nullptr, nullptr};
+        KeyT pv[2] = {0, 0};
+        bool pok[2] = {false, false};
+        const __attribute__((address_space(4))) int64_t* co =
+            (const __attribute__((address_space(4))) int64_t*)offsets;
+        auto one = [&](int u) {
+            off = ((int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)off)) |
+                  ((int64_t)__builtin_amdgcn_readfirstlane((int)(off >> 32)) << 32);
+            end = ((int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)end)) |
+                  ((int64_t)__builtin_amdgcn_readfirstlane((int)(end >> 32)) << 32);
+            const int64_t len = end - off;
+            const int64_t s_pf = std::min<int64_t>(s + wave_stride, S - 1);
+            // scalar loads (constant address space: offsets[] is read-only here), so that no
+            // vmcnt wait for them drains the gathers in flight
+            const int64_t off_next = co[s_pf], end_next = co[s_pf + 1];
+            const uint64_t stream = stream_base + (uint64_t)s;
+            KeyT* o = out + s * (int64_t)k;
+            const int64_t at = len < kSmallLen ? k2_stream<KeyT, true, true>(W, keys, off, len, stream, o)
+                                               : k2_stream<KeyT, false, true>(W, keys, off, len, stream, o);
+            // the gather of stream s - 2*wave_stride (slot u) has had two streams of work to land:
+            // after it this wave issued at least two vector-memory ops (the counts store and slot
+            // 1-u's gather; the po store too once both slots are live), so vmcnt(2) covers it
+            // without waiting for slot 1-u's gather. The loads are asm so that the compiler's own
+            // waits (which cannot count past a load it does not see) stay conservative.
+            asm volatile("s_waitcnt vmcnt(2)" : "+v"(pv[u]));
+            if (po[u] && lane < k) po[u][lane] = pok[u] ? pv[u] : (KeyT)0;
+            if (lane == 0) counts[s] = len < (int64_t)k ? len : (int64_t)k;
+            po[u] = o;
+            pok[u] = at >= 0;  // else an empty slot: the load below reads a valid dummy word
+            const KeyT* src = pok[u] ? keys + off + at : (const KeyT*)offsets;
+            if constexpr (sizeof(KeyT) == 8)
+                asm volatile("global_load_dwordx2 %0, %1, off" : "=&v"(pv[u]) : "v"(src));
+            else
+                asm volatile("global_load_dword %0, %1, off" : "=&v"(pv[u]) : "v"(src));
+            off = off_next;
+            end = end_next;
+            s += wave_stride;
+        };
+        for (; s + wave_stride < S;) {  // two streams a trip (wave-uniform), no exit between them
+            one(0);
+            one(1);
+        }
+        if (s < S) one(0);
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]));
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (po[u] && lane < k) po[u][lane] = pok[u] ? pv[u] : (KeyT)0;
+        return;
+    }
     for (; s < S; s += wave_stride) {
         // wave-uniform stream bounds (scalar registers: uniform control flow below)
         off = ((int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)off)) |
@@ -326,16 +377,7 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
         const int64_t off_next = offsets[s_pf], end_next = offsets[s_pf + 1];
         const uint64_t stream = stream_base + (uint64_t)s;
         KeyT* o = out + s * (int64_t)k;
-        if (defer) {  // k <= 64: this stream's key is stored after the next stream's draws
-            const int64_t at = len < kSmallLen ? k2_stream<KeyT, true, true>(W, keys, off, len, stream, o)
-                                               : k2_stream<KeyT, false, true>(W, keys, off, len, stream, o);
-            // the previous stream's key (loaded a whole stream ago) leaves its register before this
-            // stream's load lands in it: no copy of a load in flight, so no s_waitcnt at the stream end
-            if (pend_o && lane < k) pend_o[lane] = pend_ok ? pend_v : (KeyT)0;
-            pend_o = o;
-            pend_ok = at >= 0;  // else an empty slot: the load below reads a valid dummy word
-            pend_v = *(pend_ok ? keys + off + at : (const KeyT*)offsets);
-        } else if (len < kSmallLen) {
+        if (len < kSmallLen) {
             k2_stream<KeyT, true, false>(W, keys, off, len, stream, o);
         } else {
             k2_stream<KeyT, false, false>(W, keys, off, len, stream, o);
@@ -344,7 +386,6 @@ __global__ __launch_bounds__(64 * kWaves) void k2_segmented(const KeyT* __restri
         off = off_next;
         end = end_next;
     }
-    if (pend_o && lane < k) pend_o[lane] = pend_ok ? pend_v : (KeyT)0;
 }
 
 // ---- large k: one WORKGROUP per stream ------------------------------------------------------------
