@@ -47,14 +47,22 @@ __device__ __forceinline__ bool k1_fast(uint64_t lo, uint64_t hi) {
     return (lo >> 33) == ((hi - 1) >> 33) && hi <= (1ull << 40);
 }
 
+// the work layout of one K1 launch (k1_body_q): sch.A == 0 -- grid-stride windows; else the two-group
+// schedule of half windows
+struct K1Sched {
+    uint32_t W1, A, B;
+};
+
 __global__ __launch_bounds__(kBlock) void k1_last_writer(DrawKey dk, uint32_t k, uint64_t lo,
                                                          uint64_t hi, uint64_t g_begin,
                                                          uint64_t n_groups,
-                                                         unsigned long long* __restrict__ win) {
+                                                         unsigned long long* __restrict__ win, K1Sched sch) {
     __shared__ K1Lds L;
     const int w = threadIdx.x >> 6;
-    if (k1_fast(lo, hi)) k1_body_q<kK1Win, true>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w]);
-    else k1_body_q<kK1Win, false>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w]);
+    if (k1_fast(lo, hi))
+        k1_body_q<kK1Win, true>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], sch.W1, sch.A, sch.B);
+    else
+        k1_body_q<kK1Win, false>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], sch.W1, sch.A, sch.B);
 }
 
 // K1 + resolve_publish in one dispatch (single-launch batches, k <= kK1FusedMaxK): every
@@ -71,12 +79,14 @@ __global__ __launch_bounds__(kBlock) void k1_resolve_publish(DrawKey dk, uint32_
                                                              uint32_t* ticket, const KeyT* __restrict__ keys,
                                                              int64_t base, int64_t n, KeyT* __restrict__ slot_key,
                                                              int64_t* __restrict__ slot_idx, int fresh, int64_t m,
-                                                             KeyT* dst, uint32_t* flag, uint32_t gen) {
+                                                             KeyT* dst, uint32_t* flag, uint32_t gen, K1Sched sch) {
     __shared__ K1Lds L;
     __shared__ uint32_t last;
     const int w = threadIdx.x >> 6;
-    if (k1_fast(lo, hi)) k1_body_q<kK1Win, true>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w]);
-    else k1_body_q<kK1Win, false>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w]);
+    if (k1_fast(lo, hi))
+        k1_body_q<kK1Win, true>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], sch.W1, sch.A, sch.B);
+    else
+        k1_body_q<kK1Win, false>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], sch.W1, sch.A, sch.B);
     // This wave's winner atomics are performed once vmcnt drains: on gfx942/gfx950 a global atomic
     // without return still counts in vmcnt until the memory system acknowledges it (there is no
     // separate vscnt), and an agent-scope atomic is performed at the agent's coherence point (the
@@ -407,6 +417,26 @@ inline unsigned k1_grid(uint64_t n_groups) {
     return (unsigned)std::max<uint64_t>(1, n_groups / (per_window * m));
 }
 
+// The two-group schedule (k1_body_q), for launches of >= 4 half windows per first-group wave: the
+// first kK1W1 waves (one generation of resident waves: 6 four-wave workgroups per CU) take ~75 % of
+// the half windows, the rest go two per wave.  tools/micro_k1o s, 1e9 draws (81 k half windows):
+// (6144, 10, 2) 81.7-81.8 us, (5120, 12, 2) 81.7-82.5, (4096, 16, 1) 82.1-82.7, (6144, 8, 2)
+// 82.9-83.2, (6144, 13, 1) 89.3 (a long first group outlasts the rest) vs 83.0-83.2 us grid-stride.
+constexpr uint32_t kK1W1 = 256 * 6 * (kBlock / 64);
+inline unsigned k1_plan(uint64_t n_groups, K1Sched& sch) {
+    sch = K1Sched{0, 0, 0};
+    constexpr uint64_t UB = (uint64_t)kK1Unroll * 64 * (kK1Win / 2);  // blocks per half window
+    const uint64_t units = (n_groups + UB - 1) / UB;
+    const uint64_t A = (units * 755 / 1000 + kK1W1 / 2) / kK1W1;
+    if (n_groups < (uint64_t)kK1Unroll * kBlock * kK1Win * 768 || A < 4) return k1_grid(n_groups);
+    sch.W1 = kK1W1;
+    sch.A = (uint32_t)A;
+    sch.B = 2;
+    const uint64_t rest = units - (uint64_t)kK1W1 * A;  // > 0: A ~ 0.755 units / W1
+    const uint64_t waves = kK1W1 + (rest + sch.B - 1) / sch.B;
+    return (unsigned)((waves + kBlock / 64 - 1) / (kBlock / 64));
+}
+
 }  // namespace
 
 hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, uint64_t hi,
@@ -419,9 +449,10 @@ hipError_t launch_k1_last_writer(const DrawParams& dp, uint32_t k, uint64_t lo, 
         // and no launch crosses a multiple of 2^32 blocks: the counter's high word is a scalar
         const uint64_t g_wrap = ((g_begin >> 32) + 1) << 32;
         n_groups = std::min<uint64_t>(std::min<uint64_t>(g_end, g_wrap) - g_begin, kMaxGroups);
-        const unsigned grid = k1_grid(n_groups);
+        K1Sched sch;
+        const unsigned grid = k1_plan(n_groups, sch);
         hipLaunchKernelGGL(k1_last_writer, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
-                           g_begin, n_groups, batch_win);
+                           g_begin, n_groups, batch_win, sch);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -442,15 +473,16 @@ hipError_t launch_k1_resolve_publish(const DrawParams& dp, uint32_t k, uint64_t 
                                      hipStream_t st) {
     if (!k1_fused_ok(lo, hi, k, key_width)) return hipErrorInvalidValue;
     const uint64_t g_begin = lo >> 4, n_groups = ((hi + 15) >> 4) - g_begin;
-    const unsigned grid = k1_grid(n_groups);
+    K1Sched sch;
+    const unsigned grid = k1_plan(n_groups, sch);
     if (key_width == 8)
         hipLaunchKernelGGL(k1_resolve_publish<int64_t>, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
                            g_begin, n_groups, batch_win, ticket, (const int64_t*)keys, base, n, (int64_t*)slot_key,
-                           slot_idx, (int)fresh, m, (int64_t*)dst_host_dev, flag_dev, gen);
+                           slot_idx, (int)fresh, m, (int64_t*)dst_host_dev, flag_dev, gen, sch);
     else
         hipLaunchKernelGGL(k1_resolve_publish<int32_t>, dim3(grid), dim3(kBlock), 0, st, make_key(dp), k, lo, hi,
                            g_begin, n_groups, batch_win, ticket, (const int32_t*)keys, base, n, (int32_t*)slot_key,
-                           slot_idx, (int)fresh, m, (int32_t*)dst_host_dev, flag_dev, gen);
+                           slot_idx, (int)fresh, m, (int32_t*)dst_host_dev, flag_dev, gen, sch);
     return hipGetLastError();
 }
 

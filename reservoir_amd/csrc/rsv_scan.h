@@ -166,10 +166,20 @@ constexpr uint32_t k1q_cap() { return 64u * (1u + W / 2); }
 // FAST (launch-uniform, the kernel picks): the level-1 counter's high word is uniform over the
 // launch and every index is below 2^40 -- the resolve then forms the counter's low word with
 // 32-bit ops from the entry's counter word instead of the general 64-bit index arithmetic.
+//
+// Two work layouts (launch-uniform): A == 0 -- grid-stride over whole windows (every wave the same
+// number of iterations); A > 0 -- a static two-group schedule of half windows (units of W/2
+// iterations over 768 contiguous blocks): the first W1 waves take A units each, the rest B each,
+// strided within each group (unit j * group_waves + wave, so the launch's first units -- the dense
+// region, many times a sparse unit's work -- go one per wave to the first-dispatched waves).  The
+// first generation of resident workgroups then runs long (fewer waves: every wave ends on one or two
+// partial resolve rounds, 4.4 us of an 83 us launch at 20 k waves -- tools/micro_k1o t), the last
+// stays short (the launch's end waits on the last workgroups): tools/micro_k1o s, 1e9 draws:
+// 81.7-81.8 us at (6144, 10, 2) vs 83.0-83.2 for the grid-stride launch (profiles/r05/).
 template <int W = 12, bool FAST = false>
 __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
                                           uint64_t n_groups, unsigned long long* __restrict__ win, uint64_t* q,
-                                          uint64_t* cq) {
+                                          uint64_t* cq, uint32_t W1 = 0, uint32_t A = 0, uint32_t B = 0) {
     static_assert(W % 2 == 0, "half windows");
     constexpr int U = 2;
     const uint32_t lane = threadIdx.x & 63;
@@ -264,44 +274,101 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
     // the wave's queue base as a scalar (LDS addresses are 32-bit), so an append's address is one
     // v_lshl_add of the lane's slot onto base + 8 qn
     const uint32_t q_s = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)q);
+    // one steady iteration: the pair at counter word gt, its fold and mark appended (see below)
+    auto steady = [&](uint32_t gt) {
+        u32x4 w0, w1;
+        philox4x32_10_uniform_hi_x2(gt, ghi, dk.s0, dk.s1, dk.k0, dk.k1, w0, w1);
+        // the pair fold (with the gfx950 SDWA wait states, fold_pair) and its mark as a
+        // lane mask in one asm block
+        const uint32_t xa = w0.x | w0.y | w0.z | w0.w, xb = w1.x | w1.y | w1.z | w1.w;
+        uint32_t z;
+        unsigned long long m;
+        asm("v_or_b32_sdwa %0, %2, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+            "s_nop 0\n\t"
+            "v_or_b32_sdwa %0, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+            "s_nop 0\n\t"
+            "v_cmp_ne_u32_e64 %1, -1, %0"
+            : "=&v"(z), "=s"(m)
+            : "v"(xa), "v"(xb));
+        const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        // the marked lanes store (exec = m inside the asm, restored before it ends; one
+        // wave's LDS operations complete in order, so the rounds' reads see the entries)
+        const uint32_t sb = q_s + 8u * qn;
+        const uint64_t ent = (uint64_t)gt | ((uint64_t)z << 32);
+        unsigned long long sv;
+        uint32_t addr;
+        asm volatile("v_lshl_add_u32 %1, %2, 3, %3\n\t"
+                     "s_mov_b64 %0, exec\n\t"
+                     "s_mov_b64 exec, %4\n\t"
+                     "ds_write_b64 %1, %5\n\t"
+                     "s_mov_b64 exec, %0"
+                     : "=&s"(sv), "=&v"(addr)
+                     : "v"(pos), "s"(sb), "s"(m), "v"(ent)
+                     : "memory");
+        qn += (uint32_t)__popcll(m);
+    };
+    // one iteration of a partial window (the first, the last, or where dense / clipped blocks lie) at
+    // block offset b (wave-uniform) and counter word gl
+    auto partial = [&](uint32_t b) {
+        u32x4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            w[u] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
+        uint32_t z;
+        bool has;
+        if (b >= off_steady && b + U * 64 <= ng_steady) {
+            z = fold_pair(w[0], w[1]);
+            has = z != 0xFFFFFFFFu;
+        } else {
+            uint32_t y[U];
+            bool hb[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t off = b + u * 64 + lane;
+                const uint64_t i0 = (g_begin + off) << 4;
+                const bool dense = i0 + 1 < dense_lim;
+                // indices outside [lo, hi) count as nonzero bytes (never candidates); a
+                // block past the launch is no candidate and not dense
+                y[u] = off >= ng ? 0xFFFFu
+                                 : dense ? 0u : (fold16(w[u]) | (~clip_mask16(i0, lo, hi) & 0xFFFFu));
+                hb[u] = (off < ng) & (dense | ((uint16_t)y[u] != 0xFFFFu));
+            }
+            z = (y[0] & 0xFFFFu) | (y[1] << 16);
+            has = hb[0] | hb[1];
+        }
+        append(has, gl, z);
+        __builtin_amdgcn_wave_barrier();
+        rounds();
+    };
+    if (A > 0) {
+        constexpr uint32_t UB = (W / 2) * U * 64;
+        const uint32_t units = (ng + UB - 1) / UB;
+        const uint32_t wg = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+        const uint32_t nB = gridDim.x * (blockDim.x >> 6) - W1;
+        const bool ga = wg < W1;
+        const uint32_t cnt = ga ? A : B, u_step = ga ? W1 : nB, u_first = ga ? wg : W1 * A + (wg - W1);
+        for (uint32_t j = 0; j < cnt; ++j) {  // wave-uniform
+            const uint32_t u = u_first + j * u_step;
+            if (u >= units) break;
+            uint32_t ub = u * UB;
+            gl = g0 + ub + lane;
+            if (ub >= off_steady && ub + UB <= ng_steady) {
+#pragma unroll
+                for (int t = 0; t < W / 2; ++t) steady(gl + t * (U * 64));
+                __builtin_amdgcn_wave_barrier();
+                rounds();
+            } else {  // a unit holding dense / clipped blocks or the launch's end
+                for (int t = 0; t < W / 2 && ub < ng; ++t, ub += U * 64, gl += U * 64) partial(ub);
+            }
+        }
+        base = ng;  // the grid-stride loop below has nothing left
+    }
     while (base < ng) {  // wave-uniform
         if (base >= off_steady && (uint64_t)base + (uint64_t)(W - 1) * stride + U * 64 <= ng_steady) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
 #pragma unroll
-                for (int t = 0; t < W / 2; ++t) {
-                    const uint32_t gt = gl + t * stride;
-                    u32x4 w0, w1;
-                    philox4x32_10_uniform_hi_x2(gt, ghi, dk.s0, dk.s1, dk.k0, dk.k1, w0, w1);
-                    // the pair fold (with the gfx950 SDWA wait states, fold_pair) and its mark as a
-                    // lane mask in one asm block
-                    const uint32_t xa = w0.x | w0.y | w0.z | w0.w, xb = w1.x | w1.y | w1.z | w1.w;
-                    uint32_t z;
-                    unsigned long long m;
-                    asm("v_or_b32_sdwa %0, %2, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
-                        "s_nop 0\n\t"
-                        "v_or_b32_sdwa %0, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t"
-                        "s_nop 0\n\t"
-                        "v_cmp_ne_u32_e64 %1, -1, %0"
-                        : "=&v"(z), "=s"(m)
-                        : "v"(xa), "v"(xb));
-                    const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    // the marked lanes store (exec = m inside the asm, restored before it ends; one
-                    // wave's LDS operations complete in order, so the rounds' reads see the entries)
-                    const uint32_t sb = q_s + 8u * qn;
-                    const uint64_t ent = (uint64_t)gt | ((uint64_t)z << 32);
-                    unsigned long long sv;
-                    uint32_t addr;
-                    asm volatile("v_lshl_add_u32 %1, %2, 3, %3\n\t"
-                                 "s_mov_b64 %0, exec\n\t"
-                                 "s_mov_b64 exec, %4\n\t"
-                                 "ds_write_b64 %1, %5\n\t"
-                                 "s_mov_b64 exec, %0"
-                                 : "=&s"(sv), "=&v"(addr)
-                                 : "v"(pos), "s"(sb), "s"(m), "v"(ent)
-                                 : "memory");
-                    qn += (uint32_t)__popcll(m);
-                }
+                for (int t = 0; t < W / 2; ++t) steady(gl + t * stride);
                 gl += (W / 2) * stride;
                 __builtin_amdgcn_wave_barrier();
                 rounds();
@@ -309,35 +376,7 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
             base += W * stride;
         } else {  // a partial window (first, last, or where the dense / clipped blocks lie)
             for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride) {
-                u32x4 w[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    w[u] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
-                uint32_t z;
-                bool has;
-                if (base >= off_steady && base + U * 64 <= ng_steady) {
-                    z = fold_pair(w[0], w[1]);
-                    has = z != 0xFFFFFFFFu;
-                } else {
-                    uint32_t y[U];
-                    bool hb[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint32_t off = base + u * 64 + lane;
-                        const uint64_t i0 = (g_begin + off) << 4;
-                        const bool dense = i0 + 1 < dense_lim;
-                        // indices outside [lo, hi) count as nonzero bytes (never candidates); a
-                        // block past the launch is no candidate and not dense
-                        y[u] = off >= ng ? 0xFFFFu
-                                         : dense ? 0u : (fold16(w[u]) | (~clip_mask16(i0, lo, hi) & 0xFFFFu));
-                        hb[u] = (off < ng) & (dense | ((uint16_t)y[u] != 0xFFFFu));
-                    }
-                    z = (y[0] & 0xFFFFu) | (y[1] << 16);
-                    has = hb[0] | hb[1];
-                }
-                append(has, gl, z);
-                __builtin_amdgcn_wave_barrier();
-                rounds();
+                partial(base);
             }
         }
     }

@@ -533,4 +533,385 @@ __device__ __forceinline__ void k1_body_p(const DrawKey& dk, uint32_t k, uint64_
     drain_queue(dk, cq, cqn, lane, k, hit);
 }
 
+// ---- the round-5 k1_body_q (each wave resolves its own leftovers) with a cost probe: SKIP_TAIL
+// leaves out the final partial rounds (WRONG winners; tools/micro_k1o t) -----------------------------
+template <int W = 12, bool FAST = false, bool SKIP_TAIL = false>
+__device__ __forceinline__ void k1_body_q_dev(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                          uint64_t n_groups, unsigned long long* __restrict__ win, uint64_t* q,
+                                          uint64_t* cq) {
+    static_assert(W % 2 == 0, "half windows");
+    constexpr int U = 2;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t qn = 0, cqn = 0;
+    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
+    const uint64_t dense_lim = 256ull * k;
+    const uint32_t ng = (uint32_t)n_groups;  // < 2^31 per launch (host splits)
+    const uint64_t g_sparse = (dense_lim + 14) >> 4;
+    const uint32_t off_sparse = g_sparse <= g_begin ? 0u : (uint32_t)std::min<uint64_t>(g_sparse - g_begin, ng);
+    const uint32_t stride = gridDim.x * blockDim.x * U;
+    const uint32_t c1u = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(lo >> 33) | kDomainLevel1));
+    const bool hi_uniform = (lo >> 33) == ((hi - 1) >> 33);
+    const bool pre_ok = hi <= (1ull << 40);
+    const uint64_t k_hi = (uint64_t)k << 32;
+    const uint32_t g0 = (uint32_t)g_begin;
+    uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
+    const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g_begin >> 32));
+    uint32_t gl = g0 + base + lane;
+    const uint32_t off_steady =
+        __builtin_amdgcn_readfirstlane((int)std::max<uint32_t>(off_sparse, (lo & 15) ? 1u : 0u));
+    const uint32_t ng_steady = __builtin_amdgcn_readfirstlane((int)(ng - ((hi & 15) ? 1u : 0u)));
+
+    // one queue entry per lane (valid lanes): its pair's first zero byte by level 1; the pair's other
+    // zero bytes go back to the queue; a dense / clipped pair (a z half 0) recomputes both blocks
+    auto resolve = [&](bool valid, uint64_t ent) {
+        const uint32_t gt = (uint32_t)ent, off = gt - g0, z = (uint32_t)(ent >> 32);
+        const bool dense = valid && ((z & 0xFFFFu) == 0 || (z >> 16) == 0);
+        if (__builtin_amdgcn_ballot_w64(dense)) {
+            resolve_block(dk, dense, g_begin + off, lo, hi, dense_lim, k, cq, cqn, lane, hit);
+            resolve_block(dk, dense && off + 64 < ng, g_begin + off + 64, lo, hi, dense_lim, k, cq, cqn, lane, hit);
+        }
+        const uint32_t zm = (valid && !dense) ? ~z : 0u;
+        uint32_t rest = 0;
+        if (zm) {
+            const uint32_t e = __builtin_ctz(zm);
+            rest = zm & (zm - 1);
+            if constexpr (FAST) {
+                // the zero byte's block ghi:bl (bl = gt or gt + 64: never crosses the launch's
+                // 2^32-block span); level-1 counter i >> 1 = ghi:bl:(e & 15) >> 1, low word below
+                const uint32_t bl = gt + ((e & 16u) << 2);
+                const uint32_t g1lo = (bl << 3) | ((e & 15u) >> 1);
+                const u32x4 w = philox4x32_10_uniform_hi(g1lo, c1u, dk.s0, dk.s1, dk.k0, dk.k1);
+                const uint64_t i = ((((uint64_t)ghi << 32) | bl) << 4) | (e & 15u);
+                const bool odd = e & 1u;
+                const uint32_t Lh = odd ? w.z : w.x;
+                if ((uint64_t)(Lh >> 8) * (i + 1) < k_hi) {
+                    const uint64_t L = ((uint64_t)Lh << 32) | (odd ? w.w : w.y);
+                    const uint64_t j = __umul64hi(L >> 8, i + 1);
+                    if (j < k) hit((uint32_t)j, i);
+                }
+            } else {
+                const uint64_t i = ((g_begin + off + ((e >> 4) << 6)) << 4) + (e & 15u);
+                const u32x4 w = level1_b0_words(dk, i, hi_uniform, c1u);
+                const uint32_t Lh = (i & 1) ? w.z : w.x;
+                const bool maybe = !pre_ok || (uint64_t)(Lh >> 8) * (i + 1) < k_hi;
+                if (maybe) {
+                    const uint64_t L = ((uint64_t)Lh << 32) | ((i & 1) ? w.w : w.y);
+                    const uint64_t j = __umul64hi(L >> 8, i + 1);
+                    if (j < k) hit((uint32_t)j, i);
+                }
+            }
+        }
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(rest != 0);
+        if (bal) {
+            if (rest) {
+                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                q[qn + pos] = (uint64_t)(uint32_t)ent | ((uint64_t)~rest << 32);
+            }
+            qn += (uint32_t)__popcll(bal);
+        }
+    };
+    auto rounds = [&]() {
+        while (qn >= 64) {  // a resolve may append (pairs with more zero bytes)
+            qn -= 64;
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t ent = q[qn + lane];
+            __builtin_amdgcn_wave_barrier();
+            resolve(true, ent);
+            __builtin_amdgcn_wave_barrier();
+        }
+    };
+    // append this lane's pair (counter word gt, fold z) when has; wave-uniform call
+    auto append = [&](bool has, uint32_t gt, uint32_t z) {
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(has);
+        if (has) {
+            const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            q[qn + pos] = (uint64_t)gt | ((uint64_t)z << 32);
+        }
+        qn += (uint32_t)__popcll(bal);
+    };
+
+    // the wave's queue base as a scalar (LDS addresses are 32-bit), so an append's address is one
+    // v_lshl_add of the lane's slot onto base + 8 qn
+    const uint32_t q_s = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)q);
+    while (base < ng) {  // wave-uniform
+        if (base >= off_steady && (uint64_t)base + (uint64_t)(W - 1) * stride + U * 64 <= ng_steady) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                for (int t = 0; t < W / 2; ++t) {
+                    const uint32_t gt = gl + t * stride;
+                    u32x4 w0, w1;
+                    philox4x32_10_uniform_hi_x2(gt, ghi, dk.s0, dk.s1, dk.k0, dk.k1, w0, w1);
+                    // the pair fold (with the gfx950 SDWA wait states, fold_pair) and its mark as a
+                    // lane mask in one asm block
+                    const uint32_t xa = w0.x | w0.y | w0.z | w0.w, xb = w1.x | w1.y | w1.z | w1.w;
+                    uint32_t z;
+                    unsigned long long m;
+                    asm("v_or_b32_sdwa %0, %2, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                        "s_nop 0\n\t"
+                        "v_or_b32_sdwa %0, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                        "s_nop 0\n\t"
+                        "v_cmp_ne_u32_e64 %1, -1, %0"
+                        : "=&v"(z), "=s"(m)
+                        : "v"(xa), "v"(xb));
+                    const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    // the marked lanes store (exec = m inside the asm, restored before it ends; one
+                    // wave's LDS operations complete in order, so the rounds' reads see the entries)
+                    const uint32_t sb = q_s + 8u * qn;
+                    const uint64_t ent = (uint64_t)gt | ((uint64_t)z << 32);
+                    unsigned long long sv;
+                    uint32_t addr;
+                    asm volatile("v_lshl_add_u32 %1, %2, 3, %3\n\t"
+                                 "s_mov_b64 %0, exec\n\t"
+                                 "s_mov_b64 exec, %4\n\t"
+                                 "ds_write_b64 %1, %5\n\t"
+                                 "s_mov_b64 exec, %0"
+                                 : "=&s"(sv), "=&v"(addr)
+                                 : "v"(pos), "s"(sb), "s"(m), "v"(ent)
+                                 : "memory");
+                    qn += (uint32_t)__popcll(m);
+                }
+                gl += (W / 2) * stride;
+                __builtin_amdgcn_wave_barrier();
+                rounds();
+            }
+            base += W * stride;
+        } else {  // a partial window (first, last, or where the dense / clipped blocks lie)
+            for (int t = 0; t < W && base < ng; ++t, base += stride, gl += stride) {
+                u32x4 w[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    w[u] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * u));
+                uint32_t z;
+                bool has;
+                if (base >= off_steady && base + U * 64 <= ng_steady) {
+                    z = fold_pair(w[0], w[1]);
+                    has = z != 0xFFFFFFFFu;
+                } else {
+                    uint32_t y[U];
+                    bool hb[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t off = base + u * 64 + lane;
+                        const uint64_t i0 = (g_begin + off) << 4;
+                        const bool dense = i0 + 1 < dense_lim;
+                        // indices outside [lo, hi) count as nonzero bytes (never candidates); a
+                        // block past the launch is no candidate and not dense
+                        y[u] = off >= ng ? 0xFFFFu
+                                         : dense ? 0u : (fold16(w[u]) | (~clip_mask16(i0, lo, hi) & 0xFFFFu));
+                        hb[u] = (off < ng) & (dense | ((uint16_t)y[u] != 0xFFFFu));
+                    }
+                    z = (y[0] & 0xFFFFu) | (y[1] << 16);
+                    has = hb[0] | hb[1];
+                }
+                append(has, gl, z);
+                __builtin_amdgcn_wave_barrier();
+                rounds();
+            }
+        }
+    }
+    if (SKIP_TAIL) return;  // cost probe: WRONG winners
+    while (qn > 0) {  // the last partial rounds (appends shrink geometrically)
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t nv = std::min<uint32_t>(qn, 64u);
+        qn -= nv;
+        const bool valid = lane < nv;
+        const uint64_t ent = valid ? q[qn + lane] : 0ull;
+        __builtin_amdgcn_wave_barrier();
+        resolve(valid, ent);
+    }
+    __builtin_amdgcn_wave_barrier();
+    drain_queue(dk, cq, cqn, lane, k, hit);
+}
+
+// ---- k1_body_q over a static two-group schedule (round 5 probe; the product took it, rsv_scan.h).  The launch's half windows (units
+// of W/2 iterations, 768 contiguous blocks) go to waves in order: the first W1 waves take A units
+// each, the rest B each -- so the first generation of resident workgroups can run long (fewer
+// waves, fewer final partial rounds: 4.4 us of the 5086-workgroup launch) while the last
+// generation stays short (the launch's end waits for the last workgroups).  A first try claimed
+// units dynamically from one global counter: 1.05 ms per launch -- ~87 k same-address atomics
+// serialise at ~12 ns each (profiles/r05/micro_k1o_dyn_claims.jsonl). ---------------------------------
+template <int W = 12, bool FAST = false>
+__device__ __forceinline__ void k1_body_q_sched(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                              uint64_t n_groups, unsigned long long* __restrict__ win, uint64_t* q,
+                                              uint64_t* cq, uint32_t W1, uint32_t A, uint32_t B) {
+    static_assert(W % 2 == 0, "half windows");
+    constexpr int U = 2;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t qn = 0, cqn = 0;
+    auto hit = [&](uint32_t j, uint64_t i) { atomicMax(&win[j], (unsigned long long)i); };
+    const uint64_t dense_lim = 256ull * k;
+    const uint32_t ng = (uint32_t)n_groups;  // < 2^31 per launch (host splits)
+    const uint64_t g_sparse = (dense_lim + 14) >> 4;
+    const uint32_t off_sparse = g_sparse <= g_begin ? 0u : (uint32_t)std::min<uint64_t>(g_sparse - g_begin, ng);
+    const uint32_t stride = gridDim.x * blockDim.x * U;
+    const uint32_t c1u = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(lo >> 33) | kDomainLevel1));
+    const bool hi_uniform = (lo >> 33) == ((hi - 1) >> 33);
+    const bool pre_ok = hi <= (1ull << 40);
+    const uint64_t k_hi = (uint64_t)k << 32;
+    const uint32_t g0 = (uint32_t)g_begin;
+    uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
+    const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g_begin >> 32));
+    uint32_t gl = g0 + base + lane;
+    const uint32_t off_steady =
+        __builtin_amdgcn_readfirstlane((int)std::max<uint32_t>(off_sparse, (lo & 15) ? 1u : 0u));
+    const uint32_t ng_steady = __builtin_amdgcn_readfirstlane((int)(ng - ((hi & 15) ? 1u : 0u)));
+
+    // one queue entry per lane (valid lanes): its pair's first zero byte by level 1; the pair's other
+    // zero bytes go back to the queue; a dense / clipped pair (a z half 0) recomputes both blocks
+    auto resolve = [&](bool valid, uint64_t ent) {
+        const uint32_t gt = (uint32_t)ent, off = gt - g0, z = (uint32_t)(ent >> 32);
+        const bool dense = valid && ((z & 0xFFFFu) == 0 || (z >> 16) == 0);
+        if (__builtin_amdgcn_ballot_w64(dense)) {
+            resolve_block(dk, dense, g_begin + off, lo, hi, dense_lim, k, cq, cqn, lane, hit);
+            resolve_block(dk, dense && off + 64 < ng, g_begin + off + 64, lo, hi, dense_lim, k, cq, cqn, lane, hit);
+        }
+        const uint32_t zm = (valid && !dense) ? ~z : 0u;
+        uint32_t rest = 0;
+        if (zm) {
+            const uint32_t e = __builtin_ctz(zm);
+            rest = zm & (zm - 1);
+            if constexpr (FAST) {
+                // the zero byte's block ghi:bl (bl = gt or gt + 64: never crosses the launch's
+                // 2^32-block span); level-1 counter i >> 1 = ghi:bl:(e & 15) >> 1, low word below
+                const uint32_t bl = gt + ((e & 16u) << 2);
+                const uint32_t g1lo = (bl << 3) | ((e & 15u) >> 1);
+                const u32x4 w = philox4x32_10_uniform_hi(g1lo, c1u, dk.s0, dk.s1, dk.k0, dk.k1);
+                const uint64_t i = ((((uint64_t)ghi << 32) | bl) << 4) | (e & 15u);
+                const bool odd = e & 1u;
+                const uint32_t Lh = odd ? w.z : w.x;
+                if ((uint64_t)(Lh >> 8) * (i + 1) < k_hi) {
+                    const uint64_t L = ((uint64_t)Lh << 32) | (odd ? w.w : w.y);
+                    const uint64_t j = __umul64hi(L >> 8, i + 1);
+                    if (j < k) hit((uint32_t)j, i);
+                }
+            } else {
+                const uint64_t i = ((g_begin + off + ((e >> 4) << 6)) << 4) + (e & 15u);
+                const u32x4 w = level1_b0_words(dk, i, hi_uniform, c1u);
+                const uint32_t Lh = (i & 1) ? w.z : w.x;
+                const bool maybe = !pre_ok || (uint64_t)(Lh >> 8) * (i + 1) < k_hi;
+                if (maybe) {
+                    const uint64_t L = ((uint64_t)Lh << 32) | ((i & 1) ? w.w : w.y);
+                    const uint64_t j = __umul64hi(L >> 8, i + 1);
+                    if (j < k) hit((uint32_t)j, i);
+                }
+            }
+        }
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(rest != 0);
+        if (bal) {
+            if (rest) {
+                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                q[qn + pos] = (uint64_t)(uint32_t)ent | ((uint64_t)~rest << 32);
+            }
+            qn += (uint32_t)__popcll(bal);
+        }
+    };
+    auto rounds = [&]() {
+        while (qn >= 64) {  // a resolve may append (pairs with more zero bytes)
+            qn -= 64;
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t ent = q[qn + lane];
+            __builtin_amdgcn_wave_barrier();
+            resolve(true, ent);
+            __builtin_amdgcn_wave_barrier();
+        }
+    };
+    // append this lane's pair (counter word gt, fold z) when has; wave-uniform call
+    auto append = [&](bool has, uint32_t gt, uint32_t z) {
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(has);
+        if (has) {
+            const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            q[qn + pos] = (uint64_t)gt | ((uint64_t)z << 32);
+        }
+        qn += (uint32_t)__popcll(bal);
+    };
+
+    // the wave's queue base as a scalar (LDS addresses are 32-bit), so an append's address is one
+    // v_lshl_add of the lane's slot onto base + 8 qn
+    const uint32_t q_s = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)q);
+    constexpr uint32_t UB = (W / 2) * U * 64;
+    const uint32_t units = (ng + UB - 1) / UB;
+    (void)base;
+    (void)stride;
+    // strided within each group (unit j * group_waves + wave): the launch's first units -- the dense
+    // region, many times a sparse unit's work -- go one per wave to the first-dispatched waves
+    const uint32_t wg = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nB = gridDim.x * (blockDim.x >> 6) - W1;
+    const bool ga = wg < W1;
+    const uint32_t cnt = ga ? A : B, u_step = ga ? W1 : nB, u_first = ga ? wg : W1 * A + (wg - W1);
+    for (uint32_t j = 0; j < cnt; ++j) {  // wave-uniform
+        const uint32_t u = u_first + j * u_step;
+        if (u >= units) break;
+        uint32_t ub = u * UB;
+        gl = g0 + ub + lane;
+        if (ub >= off_steady && ub + UB <= ng_steady) {
+#pragma unroll
+            for (int t = 0; t < W / 2; ++t) {
+                const uint32_t gt = gl + t * (U * 64);
+                u32x4 w0, w1;
+                philox4x32_10_uniform_hi_x2(gt, ghi, dk.s0, dk.s1, dk.k0, dk.k1, w0, w1);
+                const uint32_t xa = w0.x | w0.y | w0.z | w0.w, xb = w1.x | w1.y | w1.z | w1.w;
+                uint32_t z;
+                unsigned long long m;
+                asm("v_or_b32_sdwa %0, %2, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                    "s_nop 0\n\t"
+                    "v_or_b32_sdwa %0, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                    "s_nop 0\n\t"
+                    "v_cmp_ne_u32_e64 %1, -1, %0"
+                    : "=&v"(z), "=s"(m)
+                    : "v"(xa), "v"(xb));
+                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                const uint32_t sb = q_s + 8u * qn;
+                const uint64_t ent = (uint64_t)gt | ((uint64_t)z << 32);
+                unsigned long long sv;
+                uint32_t addr;
+                asm volatile("v_lshl_add_u32 %1, %2, 3, %3\n\t"
+                             "s_mov_b64 %0, exec\n\t"
+                             "s_mov_b64 exec, %4\n\t"
+                             "ds_write_b64 %1, %5\n\t"
+                             "s_mov_b64 exec, %0"
+                             : "=&s"(sv), "=&v"(addr)
+                             : "v"(pos), "s"(sb), "s"(m), "v"(ent)
+                             : "memory");
+                qn += (uint32_t)__popcll(m);
+            }
+            __builtin_amdgcn_wave_barrier();
+            rounds();
+        } else {  // a unit holding the dense / clipped blocks or the launch's end
+            for (int t = 0; t < W / 2 && ub < ng; ++t, ub += U * 64, gl += U * 64) {
+                u32x4 w[U];
+#pragma unroll
+                for (int v = 0; v < U; ++v)
+                    w[v] = philox4x32_10_uniform_hi(gl, ghi, dk.s0, dk.s1, dk.k0, dk.k1, (uint64_t)kPhiloxM0 * (64u * v));
+                uint32_t y[U];
+                bool hb[U];
+#pragma unroll
+                for (int v = 0; v < U; ++v) {
+                    const uint32_t off = ub + v * 64 + lane;
+                    const uint64_t i0 = (g_begin + off) << 4;
+                    const bool dense = i0 + 1 < dense_lim;
+                    y[v] = off >= ng ? 0xFFFFu
+                                     : dense ? 0u : (fold16(w[v]) | (~clip_mask16(i0, lo, hi) & 0xFFFFu));
+                    hb[v] = (off < ng) & (dense | ((uint16_t)y[v] != 0xFFFFu));
+                }
+                const uint32_t z = (y[0] & 0xFFFFu) | (y[1] << 16);
+                append(hb[0] | hb[1], gl, z);
+                __builtin_amdgcn_wave_barrier();
+                rounds();
+            }
+        }
+    }
+    while (qn > 0) {  // the last partial rounds (appends shrink geometrically)
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t nv = std::min<uint32_t>(qn, 64u);
+        qn -= nv;
+        const bool valid = lane < nv;
+        const uint64_t ent = valid ? q[qn + lane] : 0ull;
+        __builtin_amdgcn_wave_barrier();
+        resolve(valid, ent);
+    }
+    __builtin_amdgcn_wave_barrier();
+    drain_queue(dk, cq, cqn, lane, k, hit);
+}
+
 }  // namespace rsv

@@ -78,6 +78,25 @@ __global__ __launch_bounds__(256) void k1_q(DrawKey dk, uint32_t k, uint64_t lo,
     k1_body_q<W, FAST>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w]);
 }
 
+// the product body (a copy) with the tail cost probe (tools/k1_dev_bodies.h)
+template <int W, bool FAST, bool SKIP>
+__global__ __launch_bounds__(256) void k1_qd(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                             uint64_t n_groups, unsigned long long* __restrict__ win) {
+    __shared__ K1QLds<W> L;
+    const int w = threadIdx.x >> 6;
+    k1_body_q_dev<W, FAST, SKIP>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w]);
+}
+
+// a static two-group schedule of half windows (tools/k1_dev_bodies.h k1_body_q_sched)
+template <int W, bool FAST>
+__global__ __launch_bounds__(256) void k1_qs(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                             uint64_t n_groups, unsigned long long* __restrict__ win, uint32_t W1,
+                                             uint32_t A, uint32_t B) {
+    __shared__ K1QLds<W> L;
+    const int w = threadIdx.x >> 6;
+    k1_body_q_sched<W, FAST>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], W1, A, B);
+}
+
 template <bool NOP>
 __global__ void fold_check(const uint32_t* in, uint32_t* out) {
     const uint32_t t = blockIdx.x * 64 + threadIdx.x;
@@ -174,6 +193,49 @@ int main(int argc, char** argv) {
         CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(g_dbg), sizeof z));
         printf("{\"resolves\": %llu, \"valid\": %llu, \"dense\": %llu, \"windows\": %llu, \"rounds\": %llu, "
                "\"pushed\": %llu, \"base_pushed\": %llu, \"match\": %s}\n", z[0], z[1], z[2], z[3], z[4], z[5], z[6], got == ref ? "true" : "false");
+        return 0;
+    }
+    if (argc > 1 && (argv[1][0] == 't' || argv[1][0] == 'p')) {
+        // t: the final partial rounds' cost (the body with / without them).  p (round 5, removed): the
+        // workgroup's leftovers handed to its last wave -- slower, the workgroup slot stays held while
+        // that wave resolves them alone (profiles/r05/micro_k1o_pool_ab.jsonl)
+        for (int p = 0; p < 3; ++p)
+            for (int g : {5086, 3072}) {
+                if (time_v(k1_qd<12, true, false>, "q12fast_perwave", g)) return 1;
+                if (time_v(k1_qd<12, true, true>, "q12fast_skiptail(wrong)", g)) return 1;
+            }
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 's') {  // static two-group schedules vs the product grid
+        // argv[2..]: "W1:A:B" triples (W1 waves of A half windows, the rest B each)
+        const uint32_t units = (uint32_t)((n_groups + 767) / 768);
+        for (int p = 0; p < 3; ++p) {
+            if (time_v(k1_q<12, true>, "q12fast", 5086)) return 1;
+            for (int a = 2; a < argc; ++a) {
+                unsigned W1, A, B;
+                if (sscanf(argv[a], "%u:%u:%u", &W1, &A, &B) != 3) return 2;
+                const uint64_t rest = (uint64_t)units > (uint64_t)W1 * A ? units - (uint64_t)W1 * A : 0;
+                const uint64_t waves = std::min<uint64_t>(W1, (units + A - 1) / A) + (rest + B - 1) / B;
+                const int grid = (int)((waves + 3) / 4);
+                auto launch = [&]() {
+                    hipLaunchKernelGGL((k1_qs<12, true>), dim3(grid), dim3(256), 0, 0, dk, k, lo, n, 0ull, n_groups, win,
+                                       W1, A, B);
+                };
+                for (int rep = 0; rep < 3; ++rep) launch();
+                const int reps = 20;
+                CK(hipEventRecord(e0));
+                for (int rep = 0; rep < reps; ++rep) launch();
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                CK(hipMemset(win, 0, k * 8));
+                launch();
+                CK(hipMemcpy(got.data(), win, k * 8, hipMemcpyDeviceToHost));
+                printf("{\"kernel\": \"q12fast_sched\", \"W1\": %u, \"A\": %u, \"B\": %u, \"grid\": %d, \"us\": %.2f, "
+                       "\"winners_match\": %s}\n", W1, A, B, grid, ms / reps * 1e3, got == ref ? "true" : "false");
+            }
+        }
         return 0;
     }
     const int passes = argc > 1 ? atoi(argv[1]) : 2;
