@@ -417,7 +417,7 @@ inline unsigned k1_grid(uint64_t n_groups) {
     return (unsigned)std::max<uint64_t>(1, n_groups / (per_window * m));
 }
 
-// The two-group schedule (k1_body_q), for launches of >= 4 half windows per first-group wave: the
+// The two-group schedule (k1_body_q), for launches of >= 10 half windows per first-group wave: the
 // first kK1W1 waves (one generation of resident waves: 6 four-wave workgroups per CU) take ~75 % of
 // the half windows, the rest go two per wave.  tools/micro_k1o s, 1e9 draws (81 k half windows):
 // (6144, 10, 2) 81.7-81.8 us, (5120, 12, 2) 81.7-82.5, (4096, 16, 1) 82.1-82.7, (6144, 8, 2)
@@ -428,7 +428,9 @@ inline unsigned k1_plan(uint64_t n_groups, K1Sched& sch) {
     constexpr uint64_t UB = (uint64_t)kK1Unroll * 64 * (kK1Win / 2);  // blocks per half window
     const uint64_t units = (n_groups + UB - 1) / UB;
     const uint64_t A = (units * 755 / 1000 + kK1W1 / 2) / kK1W1;
-    if (n_groups < (uint64_t)kK1Unroll * kBlock * kK1Win * 768 || A < 4) return k1_grid(n_groups);
+    // from ~1e9 draws (A >= 10); below, the plan lost to the grid-stride launch (micro_k1o n: 4.5e8
+    // 48.2 vs 44.7 us, 6e8 58.2 vs 55.7; 1e9 81.7 vs 82.8, 2e9 157.5 vs 158.8, 8e9 610.5 vs 616.9)
+    if (n_groups < (uint64_t)kK1Unroll * kBlock * kK1Win * 768 || A < 10) return k1_grid(n_groups);
     sch.W1 = kK1W1;
     sch.A = (uint32_t)A;
     sch.B = 2;

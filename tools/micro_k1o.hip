@@ -206,6 +206,54 @@ int main(int argc, char** argv) {
             }
         return 0;
     }
+    if (argc > 1 && argv[1][0] == 'n') {  // the product's grid-stride grid vs its two-group plan over sizes
+        // (replicas of rsv_elements.hip k1_grid / k1_plan); argv[2..]: draw counts
+        for (int a = 2; a < argc; ++a) {
+            const uint64_t nn = (uint64_t)atof(argv[a]), ng = (nn + 15) / 16 - lo / 16;
+            const uint64_t per_window = 2ull * 256 * 12;
+            uint64_t g;
+            if (ng < per_window * 768) g = std::min<uint64_t>((ng / 2 + 255) / 256, 256 * 20);
+            else {
+                const uint64_t mm = std::max<uint64_t>(1, (ng + per_window * 5120 / 2) / (per_window * 5120));
+                g = std::max<uint64_t>(1, ng / (per_window * mm));
+            }
+            const uint64_t units = (ng + 767) / 768, A = (units * 755 / 1000 + 3072) / 6144;
+            const bool plan = ng >= per_window * 768 && A >= 4;
+            const uint64_t waves = plan ? 6144 + (units - 6144 * A + 1) / 2 : 0;
+            const int pg = plan ? (int)((waves + 3) / 4) : 0;
+            std::vector<unsigned long long> r0(k), r1(k);
+            float best0 = 1e9f, best1 = 1e9f;
+            for (int p = 0; p < 3; ++p) {
+                for (int v = 0; v < 2; ++v) {
+                    if (v == 1 && !plan) continue;
+                    auto launch = [&]() {
+                        if (v == 0)
+                            hipLaunchKernelGGL((k1_q<12, true>), dim3((unsigned)g), dim3(256), 0, 0, dk, k, lo, nn, lo / 16, ng, win);
+                        else
+                            hipLaunchKernelGGL((k1_qs<12, true>), dim3(pg), dim3(256), 0, 0, dk, k, lo, nn, lo / 16, ng, win,
+                                               6144u, (uint32_t)A, 2u);
+                    };
+                    for (int rep = 0; rep < 3; ++rep) launch();
+                    const int reps = 10;
+                    CK(hipEventRecord(e0));
+                    for (int rep = 0; rep < reps; ++rep) launch();
+                    CK(hipEventRecord(e1));
+                    CK(hipEventSynchronize(e1));
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    CK(hipMemset(win, 0, k * 8));
+                    launch();
+                    CK(hipMemcpy((v ? r1 : r0).data(), win, k * 8, hipMemcpyDeviceToHost));
+                    float& b = v ? best1 : best0;
+                    b = std::min(b, ms / reps * 1000.0f);
+                }
+            }
+            printf("{\"n\": %.3g, \"grid_stride_us\": %.2f, \"grid\": %llu, \"plan_A\": %llu, \"plan_grid\": %d, \"plan_us\": %.2f, "
+                   "\"winners_match\": %s}\n", (double)nn, best0, (unsigned long long)g, plan ? (unsigned long long)A : 0ull,
+                   pg, plan ? best1 : 0.0f, plan ? (r0 == r1 ? "true" : "false") : "null");
+        }
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 's') {  // static two-group schedules vs the product grid
         // argv[2..]: "W1:A:B" triples (W1 waves of A half windows, the rest B each)
         const uint32_t units = (uint32_t)((n_groups + 767) / 768);
