@@ -450,6 +450,127 @@ struct Blocked : HeapOnly<2> {
     }
 };
 
+// heap-only with each node's (hash, element) side by side (one 16-B slot): a level's move reads the
+// element from the line its hash came in (one line per level instead of two)
+template <int PF>
+struct Aos {
+    struct Node {
+        int64_t h, e;
+    };
+    std::vector<Node> a;
+    int64_t k, n = 0, max_hash = INT64_MIN;
+    std::vector<int64_t> hh, he;  // copies for the check
+    explicit Aos(int64_t kk) : a((size_t)(8 * kk + 16), Node{INT64_MIN, 0}), k(kk) {}
+    void add(int64_t e, int64_t h) {
+        Node* A = a.data();
+        int64_t m = ++n;
+        while (m > 1 && A[m >> 1].h < h) {
+            A[m] = A[m >> 1];
+            m >>= 1;
+        }
+        A[m] = Node{h, e};
+    }
+    void dequeue() {
+        Node* A = a.data();
+        const Node x = A[n];
+        const int64_t nn = --n;
+        A[nn + 1].h = x.h;
+        int64_t kk = 1;
+        while (nn >= 2 * kk) {
+            int64_t j = 2 * kk;
+            if (PF >= 1) __builtin_prefetch(A + 4 * j);
+            if (PF >= 2) __builtin_prefetch(A + 4 * j + 4);
+            j += A[j].h < A[j + 1].h;
+            if (x.h >= A[j].h) break;
+            A[kk] = A[j];
+            kk = j;
+        }
+        A[kk] = x;
+    }
+    void run(int64_t c, const int64_t* ek, const int64_t* eh) {
+        int64_t t = 0;
+        for (; t < c && n < k; ++t) {
+            add(ek[t], eh[t]);
+            if (eh[t] > max_hash) max_hash = eh[t];
+        }
+        for (; t < c; ++t) {
+            const int64_t h = eh[t];
+            if (h < max_hash) {
+                dequeue();
+                add(ek[t], h);
+                max_hash = a[1].h;
+            }
+        }
+        hh.resize((size_t)k + 2);
+        he.resize((size_t)k + 2);
+        for (int64_t i = 1; i <= k; ++i) hh[i] = a[i].h, he[i] = a[i].e;
+    }
+};
+
+// heap-only with 4-byte element slots (the entry's log position; the key is read from the log at
+// the end): the element array is half the bytes, so the hashes + elements fit the core's L2 better
+template <int PF>
+struct Idx32 {
+    std::vector<int64_t> hh, he;
+    std::vector<uint32_t> ei;
+    int64_t k, n = 0, max_hash = INT64_MIN;
+    explicit Idx32(int64_t kk) : hh((size_t)kk + 2, INT64_MIN), ei((size_t)kk + 2, 0), k(kk) {}
+    void add(uint32_t e, int64_t h) {
+        int64_t* H = hh.data();
+        uint32_t* E = ei.data();
+        int64_t m = ++n;
+        while (m > 1 && H[m >> 1] < h) {
+            H[m] = H[m >> 1];
+            E[m] = E[m >> 1];
+            m >>= 1;
+        }
+        H[m] = h;
+        E[m] = e;
+    }
+    void dequeue() {
+        int64_t* H = hh.data();
+        uint32_t* E = ei.data();
+        const int64_t h = H[n];
+        const uint32_t e = E[n];
+        const int64_t nn = --n;
+        H[nn + 1] = h;
+        const int64_t last = (int64_t)hh.size() - 1;
+        int64_t kk = 1;
+        while (nn >= 2 * kk) {
+            int64_t j = 2 * kk;
+            if (PF >= 1) __builtin_prefetch(H + std::min(4 * j, last));
+            if (PF >= 2) {
+                __builtin_prefetch(H + std::min(8 * j, last));
+                __builtin_prefetch(H + std::min(8 * j + 8, last));
+            }
+            j += H[j] < H[j + 1];
+            if (h >= H[j]) break;
+            H[kk] = H[j];
+            E[kk] = E[j];
+            kk = j;
+        }
+        H[kk] = h;
+        E[kk] = e;
+    }
+    void run(int64_t c, const int64_t* ek, const int64_t* eh) {
+        int64_t t = 0;
+        for (; t < c && n < k; ++t) {
+            add((uint32_t)t, eh[t]);
+            if (eh[t] > max_hash) max_hash = eh[t];
+        }
+        for (; t < c; ++t) {
+            const int64_t h = eh[t];
+            if (h < max_hash) {
+                dequeue();
+                add((uint32_t)t, h);
+                max_hash = hh[1];
+            }
+        }
+        he.resize((size_t)k + 2);
+        for (int64_t i = 1; i <= k; ++i) he[i] = ek[ei[i]];
+    }
+};
+
 template <class F>
 static double timed(F f) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -517,6 +638,17 @@ int main(int argc, char** argv) {
         const double t10 = timed([&] { hg2.run(c, lk.data(), lh.data()); });
         std::printf("huge page %.1f (%d) +deep prefetch %.1f (%d)\n", t9, (int)check(hg1.hh, hg1.he), t10,
                     (int)check(hg2.hh, hg2.he));
+        Aos<1> o1(k);
+        const double to1 = timed([&] { o1.run(c, lk.data(), lh.data()); });
+        Aos<2> o2(k);
+        const double to2 = timed([&] { o2.run(c, lk.data(), lh.data()); });
+        Idx32<1> i1(k);
+        const double ti1 = timed([&] { i1.run(c, lk.data(), lh.data()); });
+        Idx32<2> i2(k);
+        const double ti2 = timed([&] { i2.run(c, lk.data(), lh.data()); });
+        std::printf("aos+pf %.1f (%d) aos+pf2 %.1f (%d) | idx32+pf %.1f (%d) idx32+deep %.1f (%d)\n", to1,
+                    (int)check(o1.hh, o1.he), to2, (int)check(o2.hh, o2.he), ti1, (int)check(i1.hh, i1.he), ti2,
+                    (int)check(i2.hh, i2.he));
         Branchless bl(k);
         const double t8 = timed([&] { bl.run(c, lk.data(), lh.data()); });
         std::printf("branchless descent %.1f (%d)\n", t8, (int)check(bl.hh, bl.he));
