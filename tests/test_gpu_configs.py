@@ -93,6 +93,28 @@ def test_c2_full_size_last_writers(cuda, oracle):
     assert [int(v) for v in res] == [(f(0x5EED0000 + int(i)) + 2**63) % 2**64 - 2**63 for i in want_idx]
 
 
+@pytest.mark.parametrize("lo", [7_000_000_005, 8_000_000_003])
+def test_c2_shard_two_group_schedule(cuda, oracle, lo):
+    """A C2-sized shard as rank 7 / 8 of the 8-GPU run sees it (index range [lo, lo + 1.1e9)): K1
+    takes its two-group schedule of half windows (>= ~1e9 draws, rsv_elements.hip k1_plan) with a
+    block-unaligned first and last block; the second range crosses index 2^33, where the resolve
+    leaves its FAST form.  Every slot's last writer equals the oracle's."""
+    import torch
+
+    from reservoir_amd import Sampler
+
+    n, k, seed, stream = 1_100_000_000, 1024, 0xC0FFEE, 0x5A5A
+    keys = torch.empty(n, dtype=torch.int64, device=cuda)
+    _w().splitmix_fill(keys, 0x77)
+    s = Sampler(k, seed=seed, stream_id=stream)()
+    s.seek(lo)
+    s.sample_all(keys)
+    idx, _, _, _ = s.export_state(cuda)
+    want_idx = oracle.algo_r_last_writers(seed, stream, k, lo, n)
+    assert np.array_equal(idx.cpu().numpy(), want_idx)
+    assert (want_idx >= lo).sum() > 50  # ~n / (lo + n) of the slots get a writer in the range
+
+
 # ---------------------------------------------------------------------------------------- C3
 def test_c3_full_launch(cuda, oracle):
     import torch
