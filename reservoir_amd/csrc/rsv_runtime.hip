@@ -1064,6 +1064,23 @@ rsv_status rsv_profile_global(int32_t on) {
     if (on) {
         g_prof_every = on;
         g_prof_seq = 0;
+        // the timing events up front (128 pairs, on the current device), so that no event is
+        // created inside the region being timed: at a 20-step bench region the lazily created
+        // events of its 3 timed launches cost ~3 us per step (tools/probe_region.py)
+        KernelTimer& t = global_timer();
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess && (t.ev.empty() || t.device == dev)) {
+            t.device = dev;
+            hipEvent_t last = nullptr;
+            while (t.ev.size() < 256) {
+                hipEvent_t e;
+                if (pool_event(&e, KernelTimer::kFlags) != hipSuccess) break;
+                (void)hipEventRecord(e, nullptr);  // an event's first record may set it up
+                t.ev.push_back(e);
+                last = e;
+            }
+            if (last) (void)hipEventSynchronize(last);
+        }
     }
     g_prof_on = on != 0;
     return RSV_OK;
