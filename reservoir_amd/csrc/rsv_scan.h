@@ -193,7 +193,8 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
     const uint32_t c1u = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(lo >> 33) | kDomainLevel1));
     const bool hi_uniform = (lo >> 33) == ((hi - 1) >> 33);
     const bool pre_ok = hi <= (1ull << 40);
-    const uint64_t k_hi = (uint64_t)k << 32;
+    const uint64_t k_hi = (uint64_t)k << 32, k_24 = (uint64_t)k << 24;
+    int32_t dpend = 0;  // dense entries appended and not yet resolved (wave-uniform)
     const uint32_t g0 = (uint32_t)g_begin;
     uint32_t base = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * U);
     const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g_begin >> 32));
@@ -206,10 +207,18 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
     // zero bytes go back to the queue; a dense / clipped pair (a z half 0) recomputes both blocks
     auto resolve = [&](bool valid, uint64_t ent) {
         const uint32_t gt = (uint32_t)ent, off = gt - g0, z = (uint32_t)(ent >> 32);
-        const bool dense = valid && ((z & 0xFFFFu) == 0 || (z >> 16) == 0);
-        if (__builtin_amdgcn_ballot_w64(dense)) {
-            resolve_block(dk, dense, g_begin + off, lo, hi, dense_lim, k, cq, cqn, lane, hit);
-            resolve_block(dk, dense && off + 64 < ng, g_begin + off + 64, lo, hi, dense_lim, k, cq, cqn, lane, hit);
+        // the dense test only while a partial iteration's dense entries are pending (the steady
+        // loop appends none: a steady pair with a zero fold half would need 16 zero bytes in a
+        // block, and resolving it as sparse is exact there anyway)
+        bool dense = false;
+        if (dpend > 0) {  // wave-uniform
+            dense = valid && ((z & 0xFFFFu) == 0 || (z >> 16) == 0);
+            const unsigned long long db = __builtin_amdgcn_ballot_w64(dense);
+            if (db) {
+                resolve_block(dk, dense, g_begin + off, lo, hi, dense_lim, k, cq, cqn, lane, hit);
+                resolve_block(dk, dense && off + 64 < ng, g_begin + off + 64, lo, hi, dense_lim, k, cq, cqn, lane, hit);
+                dpend -= std::min<int32_t>(dpend, (int32_t)__popcll(db));
+            }
         }
         const uint32_t zm = (valid && !dense) ? ~z : 0u;
         uint32_t rest = 0;
@@ -222,10 +231,15 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
                 const uint32_t bl = gt + ((e & 16u) << 2);
                 const uint32_t g1lo = (bl << 3) | ((e & 15u) >> 1);
                 const u32x4 w = philox4x32_10_uniform_hi(g1lo, c1u, dk.s0, dk.s1, dk.k0, dk.k1);
-                const uint64_t i = ((((uint64_t)ghi << 32) | bl) << 4) | (e & 15u);
                 const bool odd = e & 1u;
                 const uint32_t Lh = odd ? w.z : w.x;
-                if ((uint64_t)(Lh >> 8) * (i + 1) < k_hi) {
+                // a superset of j < k on 32-bit operands, the 64-bit index formed only behind it:
+                // i >> 8 = ghi:bl >> 4 (i < 2^40) and i + 1 >= (i >> 8) << 8, so (Lh >> 8)(i + 1) <
+                // k 2^32 (itself implied by j < k) implies (Lh >> 8)(i >> 8) < k 2^24.  With the
+                // dense test above skipped: 81.5-82.1 -> 80.6-81.0 us (tools/micro_k1o r)
+                const uint32_t i8 = (ghi << 28) | (bl >> 4);
+                if ((uint64_t)(Lh >> 8) * i8 < k_24) {
+                    const uint64_t i = ((((uint64_t)ghi << 32) | bl) << 4) | (e & 15u);
                     const uint64_t L = ((uint64_t)Lh << 32) | (odd ? w.w : w.y);
                     const uint64_t j = __umul64hi(L >> 8, i + 1);
                     if (j < k) hit((uint32_t)j, i);
@@ -336,6 +350,7 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
             z = (y[0] & 0xFFFFu) | (y[1] << 16);
             has = hb[0] | hb[1];
         }
+        dpend += (int32_t)__popcll(__builtin_amdgcn_ballot_w64(has && ((z & 0xFFFFu) == 0 || (z >> 16) == 0)));
         append(has, gl, z);
         __builtin_amdgcn_wave_barrier();
         rounds();

@@ -97,6 +97,18 @@ __global__ __launch_bounds__(256) void k1_qs(DrawKey dk, uint32_t k, uint64_t lo
     k1_body_q_sched<W, FAST>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], W1, A, B);
 }
 
+// the product body over its two-group plan (round 5: A/B'd against a copy with the trimmed resolve
+// rounds the product then took -- 81.5-82.1 vs 80.6-81.0 us, profiles/r05/micro_k1o_trim.jsonl)
+template <int W, bool FAST, bool TRIM>
+__global__ __launch_bounds__(256) void k1_qp(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                             uint64_t n_groups, unsigned long long* __restrict__ win, uint32_t W1,
+                                             uint32_t A, uint32_t B) {
+    __shared__ K1QLds<W> L;
+    const int w = threadIdx.x >> 6;
+    (void)TRIM;
+    k1_body_q<W, FAST>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], W1, A, B);
+}
+
 template <bool NOP>
 __global__ void fold_check(const uint32_t* in, uint32_t* out) {
     const uint32_t t = blockIdx.x * 64 + threadIdx.x;
