@@ -354,7 +354,7 @@ def main() -> None:
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--seed", type=int, default=0xC0FFEE)
     ap.add_argument("--stream-id", type=int, default=0x5A5A)
-    ap.add_argument("--time-every", type=int, default=8,
+    ap.add_argument("--time-every", type=int, default=6,
                     help="HIP events around every N-th K1 launch of the timed steps (1 = every launch); "
                          "each timed launch carries ~10 us of marker packets and host calls")
     ap.add_argument("--serial", action="store_true",
@@ -489,8 +489,10 @@ def main() -> None:
     torch.cuda.synchronize()
     # K1 timing: HIP events around every N-th K1 launch of the timed steps (process-wide list,
     # drained after the timed region; rsv_profile_global in include/reservoir_hip.h).  Each event
-    # pair adds ~5 us of marker packets to its step, so by default one step in eight carries them.
-    _native.check(L.rsv_profile_global(max(1, args.time_every)))
+    # pair adds ~5 us of marker packets to its step, so by default one step in six carries them.
+    # (the library times the (every/2)-th launch first: a region's first launch finds the GPU idle
+    # and its event pair would include the host's submission latency)
+    _native.check(L.rsv_profile_global(max(1, min(args.time_every, args.steps // 2))))
     t0 = time.perf_counter()
     res = run_steps(args.steps, depth)
     torch.cuda.synchronize()
