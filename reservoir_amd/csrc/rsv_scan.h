@@ -236,7 +236,7 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
                 // a superset of j < k on 32-bit operands, the 64-bit index formed only behind it:
                 // i >> 8 = ghi:bl >> 4 (i < 2^40) and i + 1 >= (i >> 8) << 8, so (Lh >> 8)(i + 1) <
                 // k 2^32 (itself implied by j < k) implies (Lh >> 8)(i >> 8) < k 2^24.  With the
-                // dense test above skipped: 81.5-82.1 -> 80.6-81.0 us (tools/micro_k1o r)
+                // dense test above skipped: 81.5-82.1 -> 80.6-81.0 us (profiles/r05/micro_k1o_trim.jsonl)
                 const uint32_t i8 = (ghi << 28) | (bl >> 4);
                 if ((uint64_t)(Lh >> 8) * i8 < k_24) {
                     const uint64_t i = ((((uint64_t)ghi << 32) | bl) << 4) | (e & 15u);
