@@ -50,6 +50,36 @@ __global__ __launch_bounds__(1024) void resolve(const int64_t* __restrict__ keys
     if (V != 3) publish(flag, gen);
 }
 
+// 256 threads, 4 slots each: every load of a lane issued before any use
+__global__ __launch_bounds__(256) void resolve4(const int64_t* __restrict__ keys, uint32_t k,
+                                                unsigned long long* __restrict__ win, int64_t* __restrict__ slot_key,
+                                                int64_t* __restrict__ slot_idx, int64_t* dst, uint32_t* flag,
+                                                uint32_t gen) {
+    unsigned long long wi[4];
+    int64_t v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t j = threadIdx.x + r * 256;
+        wi[r] = j < k ? win[j] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t j = threadIdx.x + r * 256;
+        v[r] = wi[r] ? keys[wi[r]] : (j < k ? slot_key[j] : 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t j = threadIdx.x + r * 256;
+        if (j >= k) continue;
+        if (wi[r]) {
+            slot_key[j] = v[r];
+            slot_idx[j] = (int64_t)wi[r];
+        }
+        dst[j] = v[r];
+    }
+    publish(flag, gen);
+}
+
 __global__ void gather_only(const int64_t* __restrict__ keys, const unsigned long long* __restrict__ win, uint32_t k,
                             int64_t* out) {
     for (uint32_t j = threadIdx.x; j < k; j += blockDim.x) out[j] = keys[win[j]];
@@ -84,8 +114,8 @@ int main() {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char* names[] = {"full", "no_key_gather", "device_dst", "no_publish", "warm_keys"};
-    for (int v = 0; v < 5; ++v) {
+    const char* names[] = {"full", "no_key_gather", "device_dst", "no_publish", "warm_keys", "full_256x4"};
+    for (int v = 0; v < 6; ++v) {
         std::vector<float> t;
         for (int rep = 0; rep < 200; ++rep) {
             for (auto& x : w) {  // fresh random winners every time: cold key lines
@@ -101,6 +131,9 @@ int main() {
                                       hdst_dev, flag_dev, gen);
             else if (v == 1)
                 hipExtLaunchKernelGGL(resolve<1>, dim3(1), dim3(1024), 0, 0, e0, e1, 0, keys, k, win, slot_key, slot_idx,
+                                      hdst_dev, flag_dev, gen);
+            else if (v == 5)
+                hipExtLaunchKernelGGL(resolve4, dim3(1), dim3(256), 0, 0, e0, e1, 0, keys, k, win, slot_key, slot_idx,
                                       hdst_dev, flag_dev, gen);
             else if (v == 2)
                 hipExtLaunchKernelGGL(resolve<2>, dim3(1), dim3(1024), 0, 0, e0, e1, 0, keys, k, win, slot_key, slot_idx,
