@@ -109,6 +109,13 @@ __global__ __launch_bounds__(256) void k1_qp(DrawKey dk, uint32_t k, uint64_t lo
     k1_body_q<W, FAST>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], W1, A, B);
 }
 
+// a stand-in for a collective running beside K1 (RCCL's all-gather kernel: a few workgroups for tens
+// of us): `blocks` workgroups of 256 threads that spin for `ns` nanoseconds of wall clock
+__global__ __launch_bounds__(256) void occupy(uint64_t ns) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    while ((__builtin_amdgcn_s_memrealtime() - t0) * 10 < ns) __builtin_amdgcn_s_sleep(2);
+}
+
 template <bool NOP>
 __global__ void fold_check(const uint32_t* in, uint32_t* out) {
     const uint32_t t = blockIdx.x * 64 + threadIdx.x;
@@ -216,6 +223,43 @@ int main(int argc, char** argv) {
                 if (time_v(k1_qd<12, true, false>, "q12fast_perwave", g)) return 1;
                 if (time_v(k1_qd<12, true, true>, "q12fast_skiptail(wrong)", g)) return 1;
             }
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'c') {  // K1 beside a concurrent occupier kernel: plan vs grid-stride
+        const uint32_t W1 = 6144, A = 10, B = 2;
+        const uint64_t units = (n_groups + 767) / 768, waves = W1 + (units - (uint64_t)W1 * A + 1) / 2;
+        const int pgrid = (int)((waves + 3) / 4);
+        hipStream_t s1, s2;
+        CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+        CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        for (int rep = 0; rep < 3000; ++rep)
+            hipLaunchKernelGGL((k1_qp<12, true, false>), dim3(pgrid), dim3(256), 0, s1, dk, k, lo, n, 0ull, n_groups, win,
+                               W1, A, B);
+        CK(hipDeviceSynchronize());
+        for (int occ : {0, 16, 64}) {
+            for (int p = 0; p < 3; ++p)
+                for (int v = 0; v < 2; ++v) {
+                    float tot = 0;
+                    const int reps = 20;
+                    for (int rep = 0; rep < reps; ++rep) {
+                        CK(hipEventRecord(e0, s1));
+                        if (v == 0)
+                            hipLaunchKernelGGL((k1_q<12, true>), dim3(5086), dim3(256), 0, s1, dk, k, lo, n, 0ull, n_groups, win);
+                        else
+                            hipLaunchKernelGGL((k1_qp<12, true, false>), dim3(pgrid), dim3(256), 0, s1, dk, k, lo, n, 0ull,
+                                               n_groups, win, W1, A, B);
+                        if (occ) hipLaunchKernelGGL(occupy, dim3(occ), dim3(256), 0, s2, 30000ull);
+                        CK(hipEventRecord(e1, s1));
+                        CK(hipEventSynchronize(e1));
+                        CK(hipStreamSynchronize(s2));
+                        float ms;
+                        CK(hipEventElapsedTime(&ms, e0, e1));
+                        tot += ms;
+                    }
+                    printf("{\"occupier_blocks\": %d, \"layout\": \"%s\", \"us\": %.2f}\n", occ,
+                           v ? "plan" : "grid_stride", tot / reps * 1e3);
+                }
+        }
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'n') {  // the product's grid-stride grid vs its two-group plan over sizes
