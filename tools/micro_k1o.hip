@@ -262,6 +262,48 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (argc > 1 && argv[1][0] == 'w') {  // window length under the two-group plan: W = 8 / 12 / 16
+        auto plan_for = [&](uint64_t UB, uint32_t& A) {
+            const uint64_t units = (n_groups + UB - 1) / UB;
+            A = (uint32_t)((units * 755 / 1000 + 3072) / 6144);
+            const uint64_t waves = 6144 + (units - 6144ull * A + 1) / 2;
+            return (int)((waves + 3) / 4);
+        };
+        uint32_t A8, A12, A16;
+        const int g8 = plan_for(512, A8), g12 = plan_for(768, A12), g16 = plan_for(1024, A16);
+        for (int rep = 0; rep < 3000; ++rep)
+            hipLaunchKernelGGL((k1_qp<12, true, false>), dim3(g12), dim3(256), 0, 0, dk, k, lo, n, 0ull, n_groups, win,
+                               6144u, A12, 2u);
+        CK(hipDeviceSynchronize());
+        for (int p = 0; p < 4; ++p)
+            for (int v = 0; v < 3; ++v) {
+                auto launch = [&]() {
+                    if (v == 0)
+                        hipLaunchKernelGGL((k1_qp<8, true, false>), dim3(g8), dim3(256), 0, 0, dk, k, lo, n, 0ull, n_groups,
+                                           win, 6144u, A8, 2u);
+                    else if (v == 1)
+                        hipLaunchKernelGGL((k1_qp<12, true, false>), dim3(g12), dim3(256), 0, 0, dk, k, lo, n, 0ull, n_groups,
+                                           win, 6144u, A12, 2u);
+                    else
+                        hipLaunchKernelGGL((k1_qp<16, true, false>), dim3(g16), dim3(256), 0, 0, dk, k, lo, n, 0ull, n_groups,
+                                           win, 6144u, A16, 2u);
+                };
+                for (int rep = 0; rep < 3; ++rep) launch();
+                const int reps = 20;
+                CK(hipEventRecord(e0));
+                for (int rep = 0; rep < reps; ++rep) launch();
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                CK(hipMemset(win, 0, k * 8));
+                launch();
+                CK(hipMemcpy(got.data(), win, k * 8, hipMemcpyDeviceToHost));
+                printf("{\"W\": %d, \"us\": %.2f, \"winners_match\": %s}\n", v == 0 ? 8 : v == 1 ? 12 : 16,
+                       ms / reps * 1e3, got == ref ? "true" : "false");
+            }
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 'n') {  // the product's grid-stride grid vs its two-group plan over sizes
         // (replicas of rsv_elements.hip k1_grid / k1_plan); argv[2..]: draw counts
         for (int a = 2; a < argc; ++a) {
