@@ -185,6 +185,7 @@ def secondary(dev) -> list:
             ("C4 default/ordered", lambda: P.c4(dev, "default")),
             ("C4 default/ordered replay branch", lambda: P.c4_replay(dev)),
             ("C2 java_l", lambda: P.c2l(dev)), ("C2 indexed", lambda: P.c2_indexed(dev)),
+            ("C2 host buffer", lambda: P.c2_host(dev)),
             ("C4 combine", lambda: P.c4_merge(dev)),
             ("C4 16-byte UUID keys, set", lambda: P.c4_wide(dev, "set")),
             ("C4 16-byte UUID keys, ordered", lambda: P.c4_wide(dev, "uuid"))]

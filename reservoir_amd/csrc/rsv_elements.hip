@@ -647,6 +647,86 @@ __global__ __launch_bounds__(kBlock) void fill_slots_kernel(const int64_t* __res
     }
 }
 
+// resolve_indices_kernel + publication of offs[] into coherent host memory (flag = gen) in one
+// dispatch, for k <= kIdxPublishMaxK: the host spins on the flag instead of a D2H copy + stream
+// synchronize (the winners-only host batches and rsv_sample_indexed)
+constexpr uint32_t kIdxPublishMaxK = 8192;
+
+__global__ __launch_bounds__(1024) void resolve_indices_publish_kernel(int64_t base, int64_t n, uint32_t k,
+                                                                       unsigned long long* __restrict__ win,
+                                                                       int64_t* __restrict__ slot_idx, int fresh,
+                                                                       uint8_t* __restrict__ slot_key, int key_width,
+                                                                       int64_t* __restrict__ offs, int64_t* offs_host,
+                                                                       uint32_t* flag, uint32_t gen) {
+    for (uint32_t j = threadIdx.x; j < k; j += blockDim.x) {
+        const unsigned long long wi = win[j];
+        int64_t off = -1;
+        if (wi) {
+            slot_idx[j] = (int64_t)wi;
+            win[j] = 0;
+            off = (int64_t)wi - base;
+        } else if ((int64_t)j >= base && (int64_t)j < base + n) {
+            slot_idx[j] = (int64_t)j;
+            off = (int64_t)j - base;
+        } else if (fresh) {
+            slot_idx[j] = -1;
+            for (int q = 0; q < key_width; ++q) slot_key[(size_t)j * key_width + q] = 0;
+        }
+        offs[j] = off;
+        offs_host[j] = off;
+    }
+    publish_flag(flag, gen);
+}
+
+// fill_slots_kernel + publication of the first m slot keys (resolve_publish's form) for k <= 8192
+// and 4- / 8-byte keys: the host-keyed batch's reservoir is published with its last kernel
+template <typename KeyT>
+__global__ __launch_bounds__(1024) void fill_slots_publish_kernel(const int64_t* __restrict__ offs,
+                                                                  const KeyT* __restrict__ keys, uint32_t k,
+                                                                  KeyT* __restrict__ slot_key, int64_t m, KeyT* dst,
+                                                                  uint32_t* flag, uint32_t gen) {
+    for (uint32_t j = threadIdx.x; j < k; j += blockDim.x) {
+        KeyT v;
+        if (offs[j] >= 0) {
+            v = keys[j];
+            slot_key[j] = v;
+        } else {
+            v = slot_key[j];
+        }
+        if ((int64_t)j < m) dst[j] = v;
+    }
+    publish_flag(flag, gen);
+}
+
+bool resolve_indices_publish_ok(uint32_t k) { return k <= kIdxPublishMaxK; }
+
+hipError_t launch_resolve_indices_publish(int64_t base, int64_t n, uint32_t k, unsigned long long* batch_win,
+                                          int64_t* slot_idx, bool fresh, void* slot_key, int key_width, int64_t* offs,
+                                          int64_t* offs_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st) {
+    if (k > kIdxPublishMaxK) return hipErrorInvalidValue;
+    const unsigned threads = std::min<unsigned>(1024, std::max<unsigned>(64, (k + 63) / 64 * 64));
+    hipLaunchKernelGGL(resolve_indices_publish_kernel, dim3(1), dim3(threads), 0, st, base, n, k, batch_win, slot_idx,
+                       (int)fresh, (uint8_t*)slot_key, key_width, offs, offs_host_dev, flag_dev, gen);
+    return hipGetLastError();
+}
+
+bool fill_slots_publish_ok(uint32_t k, int key_width) {
+    return k <= kIdxPublishMaxK && (key_width == 4 || key_width == 8);
+}
+
+hipError_t launch_fill_slots_publish(const int64_t* offs, const void* keys, uint32_t k, int key_width, void* slot_key,
+                                     int64_t m, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st) {
+    if (!fill_slots_publish_ok(k, key_width)) return hipErrorInvalidValue;
+    const unsigned threads = std::min<unsigned>(1024, std::max<unsigned>(64, (k + 63) / 64 * 64));
+    if (key_width == 8)
+        hipLaunchKernelGGL(fill_slots_publish_kernel<int64_t>, dim3(1), dim3(threads), 0, st, offs,
+                           (const int64_t*)keys, k, (int64_t*)slot_key, m, (int64_t*)dst_host_dev, flag_dev, gen);
+    else
+        hipLaunchKernelGGL(fill_slots_publish_kernel<int32_t>, dim3(1), dim3(threads), 0, st, offs,
+                           (const int32_t*)keys, k, (int32_t*)slot_key, m, (int32_t*)dst_host_dev, flag_dev, gen);
+    return hipGetLastError();
+}
+
 hipError_t launch_resolve_indices(int64_t base, int64_t n, uint32_t k, unsigned long long* batch_win, int64_t* slot_idx,
                                   bool fresh, void* slot_key, int key_width, int64_t* offs, hipStream_t st) {
     hipLaunchKernelGGL(resolve_indices_kernel, dim3(grid_for(k, 256 * 64)), dim3(kBlock), 0, st, base, n, k, batch_win,

@@ -115,6 +115,15 @@ hipError_t launch_resolve_indices(int64_t base, int64_t n, uint32_t k, unsigned 
                                   bool fresh, void* slot_key, int key_width, int64_t* offs, hipStream_t st);
 hipError_t launch_fill_slots(const int64_t* offs, const void* keys, uint32_t k, int key_width, void* slot_key,
                              hipStream_t st);
+// one-dispatch forms (k <= 8192): resolve_indices + offs[] also into coherent host memory + flag = gen;
+// fill_slots + the first m slot keys into coherent host memory + flag = gen (4- / 8-byte keys)
+bool resolve_indices_publish_ok(uint32_t k);
+hipError_t launch_resolve_indices_publish(int64_t base, int64_t n, uint32_t k, unsigned long long* batch_win,
+                                          int64_t* slot_idx, bool fresh, void* slot_key, int key_width, int64_t* offs,
+                                          int64_t* offs_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st);
+bool fill_slots_publish_ok(uint32_t k, int key_width);
+hipError_t launch_fill_slots_publish(const int64_t* offs, const void* keys, uint32_t k, int key_width, void* slot_key,
+                                     int64_t m, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st);
 // K1': events (1-based pos, slot) -> batch_win
 hipError_t launch_replay_events(const int64_t* ev_pos, const int32_t* ev_slot, int64_t n_events,
                                 uint32_t k, unsigned long long* batch_win, hipStream_t st);

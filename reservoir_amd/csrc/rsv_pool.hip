@@ -57,7 +57,10 @@ size_t class_of(size_t bytes) {
 }
 
 uint64_t key_of(uint32_t kind, unsigned flags, int device, size_t cls) {
-    return ((uint64_t)kind << 62) | ((uint64_t)(flags & 0xFF) << 54) | ((uint64_t)(device & 0xFF) << 46) |
+    // hipHostMalloc flags in 8 bits: Portable / Mapped / WriteCombined (low nibble) and NumaUser /
+    // Coherent / NonCoherent (bits 29-31) -- a coherent block is never handed out as a default one
+    const uint64_t f8 = (flags & 0x0Fu) | ((flags >> 24) & 0xF0u);
+    return ((uint64_t)kind << 62) | (f8 << 54) | ((uint64_t)(device & 0xFF) << 46) |
            (uint64_t)__builtin_ctzll(cls);
 }
 

@@ -133,6 +133,17 @@ struct rsv_sampler {
     bool idx_fresh = false;
     int64_t idx_base = 0;
     AlgoLState idx_algo_l;  // JAVA_L: java.util.Random and W before the batch's events
+    // the index-only batch's offsets in host memory: k <= 8192 coherent + mapped, published by the
+    // resolve kernel with flag offs_flag = offs_gen; larger k a pinned D2H target
+    int64_t* offs_h = nullptr;
+    int64_t* offs_dev = nullptr;
+    uint32_t* offs_flag = nullptr;
+    uint32_t* offs_flag_dev = nullptr;
+    uint32_t offs_gen = 0;
+    // the winners' keys in slot order (host gather of a winners-only batch, rsv_fill_slots): pinned,
+    // coherent and mapped, read by the fill kernel across PCIe (no H2D copy, no host wait)
+    uint8_t* gath_h = nullptr;
+    void* gath_dev = nullptr;
     // DISTINCT
     DistinctState* distinct = nullptr;
     int hash_kind = kHashIdentity;
@@ -140,8 +151,14 @@ struct rsv_sampler {
     // per-element sample(): two pinned staging buffers; a full one is flushed asynchronously
     // (H2D + kernels, no host wait) while the other fills; an event says when it is free again
     uint8_t* stage_h[2] = {nullptr, nullptr};
+    void* stage_dev[2] = {nullptr, nullptr};  // device aliases (winners-only flushes read them in place)
     int64_t* stage_hash_h[2] = {nullptr, nullptr};
     hipEvent_t stage_free[2] = {nullptr, nullptr};
+    // java_l staged flushes: the batch's Algorithm-L events in pinned memory owned by the staging
+    // buffer (free again with stage_free[b]), so their H2D copies need no host wait
+    int64_t* stage_ev_pos[2] = {nullptr, nullptr};
+    int32_t* stage_ev_slot[2] = {nullptr, nullptr};
+    int64_t stage_ev_cap[2] = {0, 0};
     bool stage_pending[2] = {false, false};
     int stage_cur = 0;
     int64_t stage_n = 0;
@@ -370,8 +387,10 @@ rsv_status resolve_batch(rsv_sampler* s, const void* keys, int64_t base, int64_t
     return RSV_OK;
 }
 
-// one batch of n keys already in device memory, at global indices [count, count+n)
-rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t* hashes, int64_t n) {
+// one batch of n keys already in device memory, at global indices [count, count+n); stage_b >= 0:
+// the batch is staging buffer stage_b, whose pinned event buffers carry java_l's events
+rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t* hashes, int64_t n,
+                                int stage_b = -1) {
     if (n <= 0) return RSV_OK;
     touch(s);
     const int64_t base = s->count;
@@ -409,14 +428,35 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
         const int64_t ne = (int64_t)s->ev_pos_h.size();
         if (ne) {
             if (rsv_status st = ensure_events(s, ne)) return st;
-            RSV_HIP_TRY(hipMemcpyAsync(s->ev_pos_d, s->ev_pos_h.data(), ne * 8, hipMemcpyHostToDevice, s->stream));
-            RSV_HIP_TRY(hipMemcpyAsync(s->ev_slot_d, s->ev_slot_h.data(), ne * 4, hipMemcpyHostToDevice, s->stream));
+            const void* pos_src = s->ev_pos_h.data();
+            const void* slot_src = s->ev_slot_h.data();
+            if (stage_b >= 0) {  // pinned: stage_b's previous flush has completed (stage_slow waited for it)
+                if (s->stage_ev_cap[stage_b] < ne) {
+                    const int64_t cap = std::max<int64_t>(ne, 2 * s->stage_ev_cap[stage_b]);
+                    pool_host_free(s->stage_ev_pos[stage_b]);
+                    pool_host_free(s->stage_ev_slot[stage_b]);
+                    s->stage_ev_pos[stage_b] = nullptr;
+                    s->stage_ev_slot[stage_b] = nullptr;
+                    s->stage_ev_cap[stage_b] = 0;
+                    RSV_HIP_TRY(pool_host_alloc((void**)&s->stage_ev_pos[stage_b], cap * 8, hipHostMallocDefault));
+                    RSV_HIP_TRY(pool_host_alloc((void**)&s->stage_ev_slot[stage_b], cap * 4, hipHostMallocDefault));
+                    s->stage_ev_cap[stage_b] = cap;
+                }
+                memcpy(s->stage_ev_pos[stage_b], pos_src, ne * 8);
+                memcpy(s->stage_ev_slot[stage_b], slot_src, ne * 4);
+                pos_src = s->stage_ev_pos[stage_b];
+                slot_src = s->stage_ev_slot[stage_b];
+            }
+            RSV_HIP_TRY(hipMemcpyAsync(s->ev_pos_d, pos_src, ne * 8, hipMemcpyHostToDevice, s->stream));
+            RSV_HIP_TRY(hipMemcpyAsync(s->ev_slot_d, slot_src, ne * 4, hipMemcpyHostToDevice, s->stream));
             const bool pm = prof_begin(s, s->stream);
             RSV_HIP_TRY(launch_replay_events(s->ev_pos_d, s->ev_slot_d, ne, s->k, s->batch_win, s->stream));
             prof_end(s, s->stream, pm);
         }
         if (rsv_status st = resolve_batch(s, keys, base, n, fresh)) return st;
-        if (ne) RSV_HIP_TRY(sync_stream(s));  // host event vectors are reused
+        // pageable host event vectors are reused by the next batch (a staged batch's pinned copies
+        // are released by its stage_free event instead)
+        if (ne && stage_b < 0) RSV_HIP_TRY(sync_stream(s));
     } else {
         const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
         const uint64_t lo = std::max<uint64_t>((uint64_t)base, s->k), hi = (uint64_t)(base + n);
@@ -478,9 +518,158 @@ rsv_status ensure_chunk(rsv_sampler* s) {
     return RSV_OK;
 }
 
+// Wait until a kernel has published `gen` into the coherent host word `flag` (acquire).  Spins for
+// up to ~2 ms -- the K1 pass of a 1e9-element batch still in flight ahead of it is ~0.1 ms -- then
+// falls back to a blocking stream synchronize, which also reports a failed kernel instead of
+// waiting forever.
+rsv_status spin_flag(rsv_sampler* s, const uint32_t* flag, uint32_t gen, const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == gen) return RSV_OK;
+        __builtin_ia32_pause();
+        if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+    }
+    RSV_HIP_TRY(sync_stream(s));
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == gen) return RSV_OK;
+    return fail(RSV_E_DEVICE, std::string(what) + " flag not set after stream synchronize");
+}
+
+// One index-only batch of n elements at global indices [count, count + n) (the reference's
+// sampleIndexed, Sampler.scala:261-273, which reads only the elements it keeps): K1 (philox_r) or
+// the host's Algorithm-L events (java_l) over the indices alone, the resolve into slot_idx, and per
+// slot the batch offset of its new element (-1: unchanged) in host memory, *offs_out (k entries,
+// valid until the handle's next index-only batch).  No key is read.  The caller then supplies the
+// winners' keys (fill_gathered) or undoes the batch (rsv_abort_indexed).
+rsv_status index_batch(rsv_sampler* s, int64_t n, const int64_t** offs_out) {
+    if (!s->idx_offs_d) RSV_HIP_TRY(pool_device_alloc((void**)&s->idx_offs_d, (size_t)s->k * 8));
+    if (!s->idx_bak_d) RSV_HIP_TRY(pool_device_alloc((void**)&s->idx_bak_d, (size_t)s->k * 8));
+    const bool publish = resolve_indices_publish_ok(s->k);
+    if (!s->offs_h) {
+        if (publish) {  // k offsets + one 64-B flag line, coherent and mapped
+            const size_t flag_off = ((size_t)s->k * 8 + 63) & ~(size_t)63;
+            RSV_HIP_TRY(pool_host_alloc((void**)&s->offs_h, flag_off + 64, hipHostMallocCoherent | hipHostMallocMapped));
+            void* dev = nullptr;
+            RSV_HIP_TRY(hipHostGetDevicePointer(&dev, s->offs_h, 0));
+            s->offs_dev = (int64_t*)dev;
+            s->offs_flag = (uint32_t*)((uint8_t*)s->offs_h + flag_off);
+            s->offs_flag_dev = (uint32_t*)((uint8_t*)dev + flag_off);
+            *s->offs_flag = s->offs_gen;
+        } else {
+            RSV_HIP_TRY(pool_host_alloc((void**)&s->offs_h, (size_t)s->k * 8, hipHostMallocDefault));
+        }
+    }
+    touch(s);
+    const int64_t base = s->count;
+    if (!s->win_zero) {  // never-used block: full init
+        RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream, s->k1_ticket));
+        s->slots_init = s->win_zero = true;
+    }
+    const bool fresh = !s->slots_init;
+    s->win_zero = false;
+    // the state rsv_abort_indexed restores (a throwing `map` leaves the slots consistent)
+    s->idx_fresh = fresh;
+    s->idx_base = base;
+    s->idx_algo_l = s->algo_l;
+    if (!fresh)
+        RSV_HIP_TRY(hipMemcpyAsync(s->idx_bak_d, s->slot_idx, (size_t)s->k * 8, hipMemcpyDeviceToDevice, s->stream));
+    if (s->cfg.engine == RSV_ENGINE_JAVA_L) {  // the reference's own events (S:261-273 skips by them)
+        s->ev_pos_h.clear();
+        s->ev_slot_h.clear();
+        s->algo_l.events(base, n, s->ev_pos_h, s->ev_slot_h);
+        const int64_t ne = (int64_t)s->ev_pos_h.size();
+        if (ne) {
+            if (rsv_status st = ensure_events(s, ne)) return st;
+            RSV_HIP_TRY(hipMemcpyAsync(s->ev_pos_d, s->ev_pos_h.data(), ne * 8, hipMemcpyHostToDevice, s->stream));
+            RSV_HIP_TRY(hipMemcpyAsync(s->ev_slot_d, s->ev_slot_h.data(), ne * 4, hipMemcpyHostToDevice, s->stream));
+            const bool pm = prof_begin(s, s->stream);
+            RSV_HIP_TRY(launch_replay_events(s->ev_pos_d, s->ev_slot_d, ne, s->k, s->batch_win, s->stream));
+            prof_end(s, s->stream, pm);
+        }
+    } else {
+        const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
+        const uint64_t lo = std::max<uint64_t>((uint64_t)base, s->k), hi = (uint64_t)(base + n);
+        const bool pm = prof_begin(s, s->stream);
+        RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
+        prof_end(s, s->stream, pm);
+    }
+    if (publish) {  // the offsets straight into coherent host memory + flag: no copy, no stream sync
+        const uint32_t gen = ++s->offs_gen;
+        RSV_HIP_TRY(launch_resolve_indices_publish(base, n, s->k, s->batch_win, s->slot_idx, fresh, s->slot_key, s->kw,
+                                                   s->idx_offs_d, s->offs_dev, s->offs_flag_dev, gen, s->stream));
+        // the event vectors above were read by copies that precede the flag in stream order
+        if (rsv_status st = spin_flag(s, s->offs_flag, gen, "index batch")) return st;
+        if (s->offs_gen == gen) s->ops_done = s->ops;  // the publication was this handle's last work
+    } else {
+        RSV_HIP_TRY(launch_resolve_indices(base, n, s->k, s->batch_win, s->slot_idx, fresh, s->slot_key, s->kw,
+                                           s->idx_offs_d, s->stream));
+        RSV_HIP_TRY(hipMemcpyAsync(s->offs_h, s->idx_offs_d, (size_t)s->k * 8, hipMemcpyDeviceToHost, s->stream));
+        RSV_HIP_TRY(sync_stream(s));
+    }
+    s->slots_init = s->win_zero = true;
+    s->pub_valid = false;
+    s->count = base + n;
+    *offs_out = s->offs_h;
+    return RSV_OK;
+}
+
+rsv_status ensure_gather(rsv_sampler* s) {
+    if (s->gath_h) return RSV_OK;
+    RSV_HIP_TRY(pool_host_alloc((void**)&s->gath_h, (size_t)s->k * s->kw, hipHostMallocCoherent | hipHostMallocMapped));
+    RSV_HIP_TRY(hipHostGetDevicePointer(&s->gath_dev, s->gath_h, 0));
+    return RSV_OK;
+}
+
+// The winners' keys, gathered by the host into gath_h (slot order; only the slots index_batch
+// changed are read), into the reservoir: one kernel reading them across PCIe, which for small
+// reservoirs also publishes the result -- enqueued, no host wait.  The gather buffer is rewritten
+// only after the handle's next index_batch has waited for its own publication, which follows this
+// kernel in stream order.
+rsv_status fill_gathered(rsv_sampler* s) {
+    touch(s);
+    if (fill_slots_publish_ok(s->k, s->kw)) {
+        if (rsv_status st = ensure_result_buffer(s)) return st;
+        if (s->result_publish) {
+            const uint32_t gen = ++s->result_gen;
+            const int64_t m = std::min<int64_t>(s->count, (int64_t)s->k);
+            RSV_HIP_TRY(launch_fill_slots_publish(s->idx_offs_d, s->gath_dev, s->k, s->kw, s->slot_key, m,
+                                                  s->result_dev, s->result_flag_dev, gen, s->stream));
+            s->pub_ops = s->ops;
+            s->pub_gen = gen;
+            s->pub_valid = true;
+            s->keys_owed = false;
+            return RSV_OK;
+        }
+    }
+    RSV_HIP_TRY(launch_fill_slots(s->idx_offs_d, s->gath_dev, s->k, s->kw, s->slot_key, s->stream));
+    s->pub_valid = false;
+    s->keys_owed = false;
+    return RSV_OK;
+}
+
+// A host batch of an ELEMENTS sampler moves only its winners: the batch is sampled by index
+// (index_batch), the host copies the <= k winning keys out of the caller's buffer, and they reach
+// the slots across PCIe (fill_gathered) -- 8 B per winner instead of 8 B per element.
+rsv_status host_batch_elements(rsv_sampler* s, const void* keys, int64_t n) {
+    const int64_t* offs = nullptr;
+    if (rsv_status st = index_batch(s, n, &offs)) return st;
+    if (rsv_status st = ensure_gather(s)) return st;
+    const uint8_t* src = (const uint8_t*)keys;
+    const size_t kw = (size_t)s->kw;
+    if (kw == 8) {
+        for (uint32_t j = 0; j < s->k; ++j)
+            if (offs[j] >= 0) memcpy(s->gath_h + (size_t)j * 8, src + (size_t)offs[j] * 8, 8);
+    } else {
+        for (uint32_t j = 0; j < s->k; ++j)
+            if (offs[j] >= 0) memcpy(s->gath_h + (size_t)j * kw, src + (size_t)offs[j] * kw, kw);
+    }
+    return fill_gathered(s);
+}
+
 rsv_status process_host_batch(rsv_sampler* s, const void* keys, const int64_t* hashes, int64_t n) {
     if (n <= 0) return RSV_OK;
+    if (s->cfg.kind == RSV_KIND_ELEMENTS) return host_batch_elements(s, keys, n);
     if (rsv_status st = ensure_chunk(s)) return st;
+    join_side(s);  // (a forked resolve reads its batch's keys; none for DISTINCT, kept for symmetry)
     for (int64_t off = 0; off < n; off += s->chunk_cap) {
         const int64_t c = std::min(s->chunk_cap, n - off);
         RSV_HIP_TRY(hipMemcpyAsync(s->chunk_d, (const uint8_t*)keys + off * s->kw, c * s->kw,
@@ -496,18 +685,57 @@ rsv_status process_host_batch(rsv_sampler* s, const void* keys, const int64_t* h
 
 // Flush the current staging buffer: H2D into the device chunk, record "buffer free", launch the
 // batch's kernels -- all stream-ordered, no host wait -- and switch to the other buffer.
+// Expected number of slots a batch of n elements at global indices [base, base + n) changes: the
+// fill of slots [base, k), then ~k/(i+1) evictions per index i >= k (Algorithm R; Algorithm L has
+// the same expectation), at most k.
+double expected_changes(const rsv_sampler* s, int64_t base, int64_t n) {
+    const double k = s->k;
+    const double fill = std::min<double>(std::max<double>(k - (double)base, 0.0), (double)n);
+    const double lo = std::max<double>((double)base, k), hi = (double)base + (double)n;
+    const double ev = hi > lo ? k * std::log(hi / lo) : 0.0;
+    return std::min(fill + ev, std::min<double>((double)n, k));
+}
+
+// A staged batch of an ELEMENTS sampler is sampled in place when its expected winners are few
+// against its size: the resolve reads the <= k winning keys straight from the pinned staging
+// buffer across PCIe instead of a DMA of the whole batch.  RSV_STAGE_ZC_RATIO (default 16): in
+// place when expected changes x ratio <= n; 0 = always copy.
+bool stage_in_place(const rsv_sampler* s, int64_t n) {
+    static const double ratio = [] {
+        const char* e = std::getenv("RSV_STAGE_ZC_RATIO");
+        return e ? std::atof(e) : 16.0;
+    }();
+    if (s->cfg.kind != RSV_KIND_ELEMENTS || ratio <= 0) return false;
+    return expected_changes(s, s->count, n) * ratio <= (double)n;
+}
+
 rsv_status flush_stage(rsv_sampler* s) {
     if (s->stage_n == 0) return RSV_OK;
     const int64_t n = s->stage_n;
     const int b = s->stage_cur;
     s->stage_n = 0;
+    if (stage_in_place(s, n)) {
+        s->stage_pending[b] = true;
+        s->stage_cur = b ^ 1;
+        if (rsv_status st = process_device_batch(s, s->stage_dev[b], nullptr, n, b)) return st;
+        // the buffer is free once the resolve that reads it has run (on the resolve stream if forked)
+        RSV_HIP_TRY(hipEventRecord(s->stage_free[b], s->side_pending ? s->rstream : s->stream));
+        return RSV_OK;
+    }
     if (rsv_status st = ensure_chunk(s)) return st;
+    join_side(s);  // a forked resolve may still read the chunk's previous batch
     RSV_HIP_TRY(hipMemcpyAsync(s->chunk_d, s->stage_h[b], n * s->kw, hipMemcpyHostToDevice, s->stream));
     if (s->chunk_hash_d && s->stage_hash_h[b])
         RSV_HIP_TRY(hipMemcpyAsync(s->chunk_hash_d, s->stage_hash_h[b], n * 8, hipMemcpyHostToDevice, s->stream));
-    RSV_HIP_TRY(hipEventRecord(s->stage_free[b], s->stream));
     s->stage_pending[b] = true;
     s->stage_cur = b ^ 1;
+    if (s->cfg.kind == RSV_KIND_ELEMENTS && s->cfg.engine == RSV_ENGINE_JAVA_L) {
+        // the batch's events travel from stage b's pinned event buffers: free after their copies
+        if (rsv_status st = process_device_batch(s, s->chunk_d, nullptr, n, b)) return st;
+        RSV_HIP_TRY(hipEventRecord(s->stage_free[b], s->stream));
+        return RSV_OK;
+    }
+    RSV_HIP_TRY(hipEventRecord(s->stage_free[b], s->stream));
     return process_device_batch(s, s->chunk_d, s->chunk_hash_d, n);
 }
 
@@ -519,9 +747,13 @@ void free_all(rsv_sampler* s) {
     for (int b = 0; b < 2; ++b) {
         pool_host_free(s->stage_h[b]);
         pool_host_free(s->stage_hash_h[b]);
+        pool_host_free(s->stage_ev_pos[b]);
+        pool_host_free(s->stage_ev_slot[b]);
         pool_release_event(s->device, s->stage_free[b], hipEventDisableTiming);
     }
     pool_host_free(s->result_h);
+    pool_host_free(s->offs_h);
+    pool_host_free(s->gath_h);
     // the handover record has completed: the stream waiting on it was synchronized, or its
     // publication seen, before this
     if (s->handover) pool_release_event(s->device, s->handover, hipEventDisableTiming);
@@ -689,7 +921,10 @@ static rsv_status stage_slow(rsv_sampler* s, bool pre) {
     }
     if (!s->stage_h[0]) {
         for (int b = 0; b < 2; ++b) {
-            RSV_HIP_TRY(pool_host_alloc((void**)&s->stage_h[b], kStageKeys * s->kw, hipHostMallocDefault));
+            // coherent + mapped: a winners-only flush's resolve reads the keys in place (flush_stage)
+            RSV_HIP_TRY(pool_host_alloc((void**)&s->stage_h[b], kStageKeys * s->kw,
+                                        hipHostMallocCoherent | hipHostMallocMapped));
+            RSV_HIP_TRY(hipHostGetDevicePointer(&s->stage_dev[b], s->stage_h[b], 0));
             if (pre) RSV_HIP_TRY(pool_host_alloc((void**)&s->stage_hash_h[b], kStageKeys * 8, hipHostMallocDefault));
             RSV_HIP_TRY(pool_event(&s->stage_free[b], hipEventDisableTiming));
         }
@@ -773,47 +1008,9 @@ rsv_status rsv_sample_indexed(rsv_sampler* s, int64_t n, int64_t* slot_offsets_h
     }
     DeviceGuard g(s->device);
     if (rsv_status st = flush_stage(s)) return st;  // keep global index order
-    if (!s->idx_offs_d) RSV_HIP_TRY(pool_device_alloc((void**)&s->idx_offs_d, (size_t)s->k * 8));
-    if (!s->idx_bak_d) RSV_HIP_TRY(pool_device_alloc((void**)&s->idx_bak_d, (size_t)s->k * 8));
-    touch(s);
-    const int64_t base = s->count;
-    if (!s->win_zero) {  // never-used block: full init
-        RSV_HIP_TRY(launch_init_slots(s->slot_key, s->kw, s->slot_idx, s->batch_win, s->k, s->stream, s->k1_ticket));
-        s->slots_init = s->win_zero = true;
-    }
-    const bool fresh = !s->slots_init;
-    s->win_zero = false;
-    // the state rsv_abort_indexed restores (a throwing `map` leaves the slots consistent)
-    s->idx_fresh = fresh;
-    s->idx_base = base;
-    s->idx_algo_l = s->algo_l;
-    if (!fresh)
-        RSV_HIP_TRY(hipMemcpyAsync(s->idx_bak_d, s->slot_idx, (size_t)s->k * 8, hipMemcpyDeviceToDevice, s->stream));
-    if (s->cfg.engine == RSV_ENGINE_JAVA_L) {  // the reference's own events (S:261-273 skips by them)
-        s->ev_pos_h.clear();
-        s->ev_slot_h.clear();
-        s->algo_l.events(base, n, s->ev_pos_h, s->ev_slot_h);
-        const int64_t ne = (int64_t)s->ev_pos_h.size();
-        if (ne) {
-            if (rsv_status st = ensure_events(s, ne)) return st;
-            RSV_HIP_TRY(hipMemcpyAsync(s->ev_pos_d, s->ev_pos_h.data(), ne * 8, hipMemcpyHostToDevice, s->stream));
-            RSV_HIP_TRY(hipMemcpyAsync(s->ev_slot_d, s->ev_slot_h.data(), ne * 4, hipMemcpyHostToDevice, s->stream));
-            RSV_HIP_TRY(launch_replay_events(s->ev_pos_d, s->ev_slot_d, ne, s->k, s->batch_win, s->stream));
-        }
-    } else {
-        const DrawParams dp{s->cfg.seed, s->cfg.stream_id};
-        const uint64_t lo = std::max<uint64_t>((uint64_t)base, s->k), hi = (uint64_t)(base + n);
-        const bool pm = prof_begin(s, s->stream);
-        RSV_HIP_TRY(launch_k1_last_writer(dp, s->k, lo, hi, s->batch_win, s->stream));
-        prof_end(s, s->stream, pm);
-    }
-    RSV_HIP_TRY(launch_resolve_indices(base, n, s->k, s->batch_win, s->slot_idx, fresh, s->slot_key, s->kw,
-                                       s->idx_offs_d, s->stream));
-    RSV_HIP_TRY(hipMemcpyAsync(slot_offsets_host, s->idx_offs_d, (size_t)s->k * 8, hipMemcpyDeviceToHost, s->stream));
-    RSV_HIP_TRY(sync_stream(s));
-    s->slots_init = s->win_zero = true;
-    s->pub_valid = false;
-    s->count = base + n;
+    const int64_t* offs = nullptr;
+    if (rsv_status st = index_batch(s, n, &offs)) return st;
+    memcpy(slot_offsets_host, offs, (size_t)s->k * 8);
     s->keys_owed = true;
     return RSV_OK;
 }
@@ -823,25 +1020,15 @@ rsv_status rsv_fill_slots(rsv_sampler* s, const void* keys_host) {
     if (!s->keys_owed) return fail(RSV_E_ILLEGAL_STATE, "rsv_fill_slots without a pending rsv_sample_indexed");
     if (!keys_host) return fail(RSV_E_NULL_POINTER, "keys_host is NULL");
     DeviceGuard g(s->device);
-    const size_t bytes = (size_t)s->k * s->kw;
-    void* dev = nullptr;
-    touch(s);
-    if ((int64_t)s->k <= kChunkKeys) {  // the handle's host-batch chunk
-        if (rsv_status st = ensure_chunk(s)) return st;
-        dev = s->chunk_d;
-    } else {
-        RSV_HIP_TRY(hipMallocAsync(&dev, bytes, s->stream));
-    }
-    hipError_t e = hipMemcpyAsync(dev, keys_host, bytes, hipMemcpyHostToDevice, s->stream);
-    if (e == hipSuccess) e = launch_fill_slots(s->idx_offs_d, dev, s->k, s->kw, s->slot_key, s->stream);
-    if (dev != s->chunk_d) {
-        const hipError_t e2 = hipFreeAsync(dev, s->stream);
-        if (e == hipSuccess) e = e2;
-    }
-    RSV_HIP_TRY(e);
-    RSV_HIP_TRY(sync_stream(s));  // the caller's buffer is theirs again
-    s->keys_owed = false;
-    return RSV_OK;
+    if (rsv_status st = ensure_gather(s)) return st;
+    // the changed slots' keys into the pinned gather buffer: the caller's buffer is theirs again on
+    // return, and no copy or host wait follows
+    const int64_t* offs = s->offs_h;
+    const size_t kw = (size_t)s->kw;
+    const uint8_t* src = (const uint8_t*)keys_host;
+    for (uint32_t j = 0; j < s->k; ++j)
+        if (offs[j] >= 0) memcpy(s->gath_h + (size_t)j * kw, src + (size_t)j * kw, kw);
+    return fill_gathered(s);
 }
 
 rsv_status rsv_abort_indexed(rsv_sampler* s) {
@@ -862,20 +1049,8 @@ rsv_status rsv_abort_indexed(rsv_sampler* s) {
     return RSV_OK;
 }
 
-// Wait until publish_kernel has stored `gen` (acquire).  Spins for up to ~2 ms -- the K1 pass of a
-// 1e9-element batch still in flight ahead of it is ~0.13 ms -- then falls back to a blocking stream
-// synchronize, which also reports a failed kernel instead of waiting forever.
-static rsv_status wait_flag(rsv_sampler* s, uint32_t gen) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t spin = 1;; ++spin) {
-        if (__atomic_load_n(s->result_flag, __ATOMIC_ACQUIRE) == gen) return RSV_OK;
-        __builtin_ia32_pause();
-        if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
-    }
-    RSV_HIP_TRY(sync_stream(s));
-    if (__atomic_load_n(s->result_flag, __ATOMIC_ACQUIRE) == gen) return RSV_OK;
-    return fail(RSV_E_DEVICE, "result publish flag not set after stream synchronize");
-}
+// Wait until a publication kernel has stored `gen` in the result flag (spin_flag)
+static rsv_status wait_flag(rsv_sampler* s, uint32_t gen) { return spin_flag(s, s->result_flag, gen, "result publish"); }
 
 static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* out_n, bool device_out,
                               bool take = false) {

@@ -187,6 +187,7 @@ class GpuSampler:
         N.check(self._L.rsv_create(C.byref(cfg), C.byref(h)))
         self._h = h
         self._stream = int(self._L.rsv_get_stream(h) or 0)
+        self._rstream = 0  # set_resolve_stream
         self._precomputed = hash_kind == N.HASH_PRECOMPUTED
         self._rows = None  # the last merge_packed's rows (a distinct merge reads them until it settles)
         self._ordered = False
@@ -237,6 +238,7 @@ class GpuSampler:
         queue behind them (include/reservoir_hip.h rsv_set_resolve_stream).  The batch's keys must
         stay unchanged until result() returns."""
         N.check(self._L.rsv_set_resolve_stream(self._h, C.c_void_p(hip_stream or 0)))
+        self._rstream = int(hip_stream or 0)
 
     def synchronize(self) -> None:
         N.check(self._L.rsv_synchronize(self._h))
@@ -283,6 +285,9 @@ class GpuSampler:
                 # and torch must not hand the block to another tensor while this handle's stream
                 # still reads it (the caller may drop `elements` as soon as we return)
                 t.record_stream(torch.cuda.ExternalStream(self._stream, device=t.device))
+            if self._rstream and self._rstream != cur:
+                # the batch's resolve reads the keys on the resolve stream, after this call returns
+                t.record_stream(torch.cuda.ExternalStream(self._rstream, device=t.device))
             if self._width <= 8:
                 if t.element_size() != self._width:
                     raise IllegalArgumentException("device tensor dtype does not match key_type")

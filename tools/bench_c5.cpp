@@ -89,5 +89,34 @@ int main(int argc, char** argv) {
                     k, engine ? "java_l" : "philox_r", (long long)n, n / ds / 1e6, n / de / 1e6, (long long)m);
         rsv_destroy(s);
     }
+    // the source alone: the same loop writing the same pinned staging memory with no sampler work
+    // (nothing committed) -- the host-side ceiling of the zero-copy legs above
+    {
+        rsv_config cfg;
+        reservoir::check(rsv_config_init(&cfg));
+        cfg.max_sample_size = k;
+        rsv_sampler* s = nullptr;
+        reservoir::check(rsv_create(&cfg, &s));
+        void* buf = nullptr;
+        int64_t cap = 0;
+        reservoir::check(rsv_stage_acquire(s, &buf, nullptr, &cap));
+        int64_t* kb = (int64_t*)buf;
+        const size_t mask = src.size() - 1;
+        auto t0 = std::chrono::steady_clock::now();
+        for (int64_t i = 0; i < n;) {
+            const int64_t c = std::min<int64_t>(cap, n - i);
+            for (int64_t t = 0; t < c; ++t) kb[t] = src[(size_t)(i + t) & mask];
+            asm volatile("" ::: "memory");  // every chunk's stores happen
+            i += c;
+        }
+        auto t1 = std::chrono::steady_clock::now();
+        volatile int64_t sink = kb[cap - 1];
+        (void)sink;
+        const double ds = std::chrono::duration<double>(t1 - t0).count();
+        std::printf("{\"config\": \"C5 source alone: the zero-copy legs' fill loop into the same pinned staging buffer, "
+                    "no sampler work\", \"elements\": %lld, \"sustained_Melem_s\": %.1f}\n",
+                    (long long)n, n / ds / 1e6);
+        rsv_destroy(s);
+    }
     return 0;
 }

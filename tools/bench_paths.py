@@ -299,6 +299,43 @@ def c2l(dev):
             "elements": n, "seconds": t, "Gelem_s": n / t / 1e9}
 
 
+def c2_host(dev):
+    """C2 from a 1e9-key HOST buffer through rsv_sample_batch(RSV_MEM_HOST) (what the JVM bindings
+    call with keys extracted into a host batch): the batch is sampled by index and only the <= k
+    winners' keys leave host memory (round 6; before it every key crossed PCIe, ~0.5 s per 8 GB).
+    Both engines; a step = create, sampleAll(host keys), result(), close; wall clock, median."""
+    import numpy as np
+
+    from reservoir_amd import Sampler, _native as N
+
+    L = N.load()
+    n, k = 1_000_000_000, 1024
+    keys_d = torch.empty(n, dtype=torch.int64, device=dev)
+    splitmix_fill(keys_d, 0x5EED0000)
+    keys = keys_d.cpu().numpy()  # pageable host memory, as a JVM-side batch would be
+    del keys_d
+    torch.cuda.empty_cache()
+    ptr = keys.ctypes.data_as(C.c_void_p)
+    out = []
+    for engine in ("philox_r", "java_l"):
+        ts = []
+        res = None
+        for rep in range(14):
+            s = Sampler(k, seed=0xC0FFEE, stream_id=0x5A5A, engine=engine)()
+            t0 = time.perf_counter()
+            N.check(L.rsv_sample_batch(s.handle, ptr, n, N.MEM_HOST, None))
+            res = s.result()
+            ts.append(time.perf_counter() - t0)
+            s.close()
+        t = sorted(ts[4:])[len(ts[4:]) // 2]
+        out.append({"config": f"C2 from a 1e9-key host buffer via rsv_sample_batch(RSV_MEM_HOST), engine={engine}: "
+                              "winners-only (index-only batch + host gather of the <= k winning keys)",
+                    "elements": n, "seconds": t, "Gelem_s": n / t / 1e9, "result_n": int(res.size),
+                    "what": "wall clock of create + sampleAll + result() + close, median of 10 after 4 warm-up"})
+    del keys
+    return out
+
+
 def c2_indexed(dev):
     """sampleAll over a 1e9-element IndexedSeq through the C ABI (the FFM/JNI bindings' override):
     K1 over the indices, k x 8 B of slot offsets back, the winners' keys forward -- no key buffer."""
@@ -392,6 +429,9 @@ def main():
         print(json.dumps(c2l(dev)), flush=True)
     if "c2i" in todo:
         print(json.dumps(c2_indexed(dev)), flush=True)
+    if "c2h" in todo:
+        for r in c2_host(dev):
+            print(json.dumps(r), flush=True)
     if "c3k" in todo:
         for r in c3_large_k(dev):
             print(json.dumps(r), flush=True)
