@@ -254,15 +254,23 @@ JNIEXPORT jint JNICALL JNI_FN(resultWords)(JNIEnv* env, jobject self, jlong s, j
 
 JNIEXPORT void JNICALL JNI_FN(fillWords)(JNIEnv* env, jobject self, jlong s, jlongArray keys) {
     (void)self;
-    const jint kw = session(s)->k * (session(s)->key_width / 8);
-    jlong* buf = (jlong*)malloc((size_t)kw * sizeof(jlong));
+    /* k * key_width / 8 <= Int.MaxValue (rsv_jvm_create refuses larger byte-key samplers) */
+    const size_t kw = (size_t)session(s)->k * (size_t)(session(s)->key_width / 8);
+    jlong* buf = (jlong*)malloc(kw * sizeof(jlong));
     if (!buf) {
         throw_status(env, RSV_E_OUT_OF_MEMORY);
         return;
     }
-    (*env)->GetLongArrayRegion(env, keys, 0, kw, buf);
+    (*env)->GetLongArrayRegion(env, keys, 0, (jsize)kw, buf);
     rsv_status st = (*env)->ExceptionCheck(env) ? RSV_OK : rsv_jvm_fill_slots(session(s), buf);
     free(buf);
+    if (st != RSV_OK) throw_status(env, st);
+}
+
+/* ObjectSampler (any B): accept the index-only batch; the B values stay in the JVM's slot array */
+JNIEXPORT void JNICALL JNI_FN(commitIndexed)(JNIEnv* env, jobject self, jlong s) {
+    (void)self;
+    rsv_status st = rsv_jvm_commit_indexed(session(s));
     if (st != RSV_OK) throw_status(env, st);
 }
 

@@ -17,6 +17,12 @@ static rsv_status closed(void) {
 rsv_status rsv_jvm_create(rsv_jvm* s, const rsv_config* cfg) {
     memset(s, 0, sizeof(*s));
     g_local_error = 0;
+    /* byte keys travel as k * key_width / 8 Longs in one JVM array (JniSampler / FfmSampler): more
+     * than Int.MaxValue of them cannot be allocated there -- refuse the sampler up front */
+    if (cfg->key_width > 8 && (int64_t)cfg->max_sample_size * (cfg->key_width / 8) > 2147483647) {
+        g_local_error = "requirement failed: maxSampleSize * key words exceeds the JVM array limit";
+        return RSV_E_ILLEGAL_ARGUMENT;
+    }
     rsv_status st = rsv_create(cfg, &s->h);
     if (st != RSV_OK) return st;
     s->open = 1;
@@ -131,6 +137,12 @@ rsv_status rsv_jvm_abort_indexed(rsv_jvm* s) {
     g_local_error = 0;
     if (!s->open) return closed();
     return rsv_abort_indexed(s->h);
+}
+
+rsv_status rsv_jvm_commit_indexed(rsv_jvm* s) {
+    g_local_error = 0;
+    if (!s->open) return closed();
+    return rsv_commit_indexed(s->h);
 }
 
 rsv_status rsv_jvm_result(rsv_jvm* s, void* out, int64_t cap, int64_t* out_n) {

@@ -57,6 +57,9 @@ rsv_status rsv_jvm_fill_slots(rsv_jvm* s, const void* keys);
 /* `map` threw on an element owed after rsv_jvm_sample_indexed: drop that batch (rsv_abort_indexed)
  * so the sampler stays usable; the binding rethrows the exception */
 rsv_status rsv_jvm_abort_indexed(rsv_jvm* s);
+/* a `Sampler[A, B]` for any other B (ObjectSampler.scala): accept the pending index-only batch
+ * without keys -- the binding keeps the B values in its own slot array (rsv_commit_indexed) */
+rsv_status rsv_jvm_commit_indexed(rsv_jvm* s);
 /* Sampler.result (S:59-60): writes min(count, k) keys; a single-use sampler closes (S:345-350) */
 rsv_status rsv_jvm_result(rsv_jvm* s, void* out, int64_t cap, int64_t* out_n);
 /* zero-copy form for a producer that writes keys itself (keys-only samplers): the free tail of

@@ -16,6 +16,10 @@ private[reservoir] trait SamplerFactory {
       map: A => B,
       hash: B => Long,
   ): Sampler[A, B]
+
+  /** Sampler.apply for a `B` with no fixed-width key: index-only batches, the elements kept on the
+    * JVM ([[ObjectSampler]]) */
+  def makeObjects[A, B: ClassTag](k: Int, reusable: Boolean, engine: Int, seed: Long)(map: A => B): Sampler[A, B]
 }
 
 private[reservoir] object JniFactory extends SamplerFactory {
@@ -23,12 +27,18 @@ private[reservoir] object JniFactory extends SamplerFactory {
       map: A => B,
       hash: B => Long,
   ): Sampler[A, B] = new JniSampler[A, B](kind, k, reusable, keys, hashKind, engine, seed)(map, hash)
+
+  def makeObjects[A, B: ClassTag](k: Int, reusable: Boolean, engine: Int, seed: Long)(map: A => B): Sampler[A, B] =
+    new ObjectSampler[A, B](k, reusable, new JniIndexOps(k, reusable, engine, seed))(map)
 }
 
 /** Backend selection behind the unchanged factories `Sampler.apply` / `Sampler.distinct`
   * (Sampler.scala:128-136, :171-180; SURVEY.md section 5 "Config / flags"): no signature changes.
   *
-  *   -Dreservoir.backend=gpu        use the MI355X engine for B = Long or Int (else the JVM classes)
+  *   -Dreservoir.backend=gpu        use the MI355X engine: Sampler.apply for every B (Long, Int and
+  *                                  java.util.UUID keys live on the GPU; any other B is sampled by
+  *                                  index and its elements stay on the JVM, ObjectSampler);
+  *                                  Sampler.distinct for B = Long, Int or UUID (else the JVM classes)
   *   -Dreservoir.binding=ffm|jni    default: FFM when the JDK is 22+ and the reservoir-gpu-ffm jar is
   *                                  on the class path, JNI otherwise
   *   -Dreservoir.engine=java_l      the reference's Algorithm L over java.util.Random, bit-identical
@@ -75,7 +85,12 @@ private[reservoir] object Backend {
   /** Sampler.apply (validation already done by validateNonDistinctParams). */
   def elements[A, B: ClassTag](maxSampleSize: Int, reusable: Boolean)(map: A => B): Option[Sampler[A, B]] =
     if (!enabled) None
-    else KeyKind.of[B].map(kk => make[A, B](Abi.KindElements, maxSampleSize, reusable, kk, Abi.HashDefault)(map, null))
+    else
+      KeyKind.of[B] match {
+        case Some(kk) => Some(make[A, B](Abi.KindElements, maxSampleSize, reusable, kk, Abi.HashDefault)(map, null))
+        case None => // any other B: which element each slot holds is decided on the GPU, the B stays here
+          Some(factory.makeObjects[A, B](maxSampleSize, reusable, engine, seeds.nextLong())(map))
+      }
 
   /** Sampler.distinct: the default `hashCode` and the identity hash run on the GPU; any other `hash`
     * is evaluated here per element and shipped beside the key (RSV_HASH_PRECOMPUTED). */

@@ -46,6 +46,7 @@ private[reservoir] object Jni {
   @native def resultWords(session: Long, out: Array[Long]): Int
   @native def fillWords(session: Long, words: Array[Long]): Unit
   @native def abortIndexed(session: Long): Unit
+  @native def commitIndexed(session: Long): Unit
 }
 
 /** One native session (a malloc'd rsv_jvm, reservoir_jni.c) released exactly once: by a single-use
@@ -92,7 +93,7 @@ private[gpu] object JniCleaner {
   }
 }
 
-/** A GPU-backed `Sampler[A, B]` over JNI, B = Long, Int or UUID: keys are buffered in a JVM array and
+/** A GPU-backed `Sampler[A, B]` over JNI, B = Long, Int or UUID (any other B: [[ObjectSampler]]): keys are buffered in a JVM array and
   * handed over 65536 at a time (one JNI call per batch, none per element); the native session copies
   * them into the engine's pinned staging buffer.  Lifecycle as FfmSampler: `isOpen` tracked here, the
   * single-use `result()` destroys the session at once. */
@@ -158,46 +159,35 @@ private[reservoir] final class JniSampler[A, B](
       val offsets = new Array[Long](maxSampleSize)
       Jni.sampleIndexed(session.get, seq.length.toLong, offsets)
       // a throwing `map` drops the batch (the sampler stays usable) and propagates, as the
-      // reference's sampleIndexed propagates it
+      // reference's sampleIndexed propagates it; the fill downcall runs outside the try, as in
+      // FfmSampler (a failed fill is the engine's error, not the user's)
+      val longKeys = if (isUuid) new Array[Long](2 * maxSampleSize) else if (isLong) new Array[Long](maxSampleSize) else null
+      val intKeys  = if (longKeys == null) new Array[Int](maxSampleSize) else null
       try {
-        if (isUuid) {
-          val ks = new Array[Long](2 * maxSampleSize)
-          var j  = 0
-          while (j < maxSampleSize) {
-            val o = offsets(j)
-            if (o >= 0) {
-              val u = map(seq(o.toInt)).asInstanceOf[java.util.UUID]
-              ks(2 * j) = u.getMostSignificantBits
-              ks(2 * j + 1) = u.getLeastSignificantBits
-            }
-            j += 1
+        var j = 0
+        while (j < maxSampleSize) {
+          val o = offsets(j)
+          if (o >= 0) {
+            val b = map(seq(o.toInt))
+            if (isUuid) {
+              val u = b.asInstanceOf[java.util.UUID]
+              longKeys(2 * j) = u.getMostSignificantBits
+              longKeys(2 * j + 1) = u.getLeastSignificantBits
+            } else if (isLong) longKeys(j) = b.asInstanceOf[Long]
+            else intKeys(j) = b.asInstanceOf[Int]
           }
-          Jni.fillWords(session.get, ks)
-        } else if (isLong) {
-          val ks = new Array[Long](maxSampleSize)
-          var j  = 0
-          while (j < maxSampleSize) {
-            val o = offsets(j)
-            if (o >= 0) ks(j) = map(seq(o.toInt)).asInstanceOf[Long]
-            j += 1
-          }
-          Jni.fillLongs(session.get, ks)
-        } else {
-          val ks = new Array[Int](maxSampleSize)
-          var j  = 0
-          while (j < maxSampleSize) {
-            val o = offsets(j)
-            if (o >= 0) ks(j) = map(seq(o.toInt)).asInstanceOf[Int]
-            j += 1
-          }
-          Jni.fillInts(session.get, ks)
+          j += 1
         }
       } catch {
         case t: Throwable =>
-          Jni.abortIndexed(session.get)
+          try Jni.abortIndexed(session.get)
+          catch { case e: Throwable => t.addSuppressed(e) }
           fence = 1
           throw t
       }
+      if (isUuid) Jni.fillWords(session.get, longKeys)
+      else if (isLong) Jni.fillLongs(session.get, longKeys)
+      else Jni.fillInts(session.get, intKeys)
       fence = 1
     case _ => super.sampleAll(elements)
   }
@@ -228,4 +218,18 @@ private[reservoir] final class JniSampler[A, B](
   }
 
   def isOpen: Boolean = open
+}
+
+/** [[IndexOps]] over JNI: an ELEMENTS session whose slots the engine fills by index only
+  * (rsv_commit_indexed); the B values live in the [[ObjectSampler]]. */
+private[reservoir] final class JniIndexOps(k: Int, reusable: Boolean, engine: Int, seed: Long) extends IndexOps {
+  private[this] val session =
+    new JniSession(Jni.create(Abi.KindElements, k, 8, reusable, engine, Abi.HashDefault, Abi.OrderAuto, seed, 0L, -1))
+  JniCleaner.register(this, session)
+  @volatile private[this] var fence = 0 // keeps `this` reachable across each native call (JniSampler)
+
+  def sampleIndexed(n: Long, offsets: Array[Long]): Unit = { Jni.sampleIndexed(session.get, n, offsets); fence = 1 }
+  def commitIndexed(): Unit                              = { Jni.commitIndexed(session.get); fence = 1 }
+  def abortIndexed(): Unit                               = { Jni.abortIndexed(session.get); fence = 1 }
+  def release(): Unit                                    = session.release()
 }

@@ -9,9 +9,10 @@ import java.lang.invoke.MethodHandle
 import java.lang.ref.Cleaner
 
 import scala.collection.immutable.ArraySeq
+import scala.reflect.ClassTag
 
 import lgbt.princess.reservoir.Sampler
-import lgbt.princess.reservoir.gpu.{Abi, KeyKind, SamplerFactory}
+import lgbt.princess.reservoir.gpu.{Abi, IndexOps, KeyKind, ObjectSampler, SamplerFactory}
 
 /** Panama FFM downcall handles of libreservoir_hip.so (JDK 22+, run with --enable-native-access).
   * Names carry an `rsv` prefix so nothing here shadows a Sampler member (e.g. `isOpen`). */
@@ -51,6 +52,7 @@ private[reservoir] object Native {
     downcall("rsv_sample_indexed", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS))
   val rsvFillSlots: MethodHandle = downcall("rsv_fill_slots", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS))
   val rsvAbortIndexed: MethodHandle = downcall("rsv_abort_indexed", FunctionDescriptor.of(JAVA_INT, ADDRESS))
+  val rsvCommitIndexed: MethodHandle = downcall("rsv_commit_indexed", FunctionDescriptor.of(JAVA_INT, ADDRESS))
 
   val cleaner: Cleaner = Cleaner.create()
 
@@ -87,6 +89,9 @@ private[reservoir] final class FfmSampler[A, B](
   private[this] val isUuid      = keys eq KeyKind.UuidKey
   private[this] val precomputed = kind == Abi.KindDistinct && hashKind == Abi.HashPrecomputed
   private[this] val handle: MemorySegment = {
+    // UUID keys travel as 2 Longs each in one segment / JVM array (result, sampleAll): as rsv_jvm_create
+    if (isUuid && 2L * maxSampleSize > Int.MaxValue)
+      throw new IllegalArgumentException("requirement failed: maxSampleSize * key words exceeds the JVM array limit")
     val cfg = arena.allocate(Config)
     check(rsvConfigInit.invoke(cfg).asInstanceOf[Int])
     cfg.set(JAVA_INT, 4L, kind)
@@ -181,7 +186,8 @@ private[reservoir] final class FfmSampler[A, B](
           }
         } catch { // `map` threw: drop the batch, keep the sampler usable, propagate (sampleIndexed does)
           case t: Throwable =>
-            check(rsvAbortIndexed.invoke(handle).asInstanceOf[Int])
+            try check(rsvAbortIndexed.invoke(handle).asInstanceOf[Int])
+            catch { case e: Throwable => t.addSuppressed(e) }
             throw t
         }
         check(rsvFillSlots.invoke(handle, ks).asInstanceOf[Int])
@@ -229,4 +235,42 @@ private[reservoir] final class FfmFactory extends SamplerFactory {
       map: A => B,
       hash: B => Long,
   ): Sampler[A, B] = new FfmSampler[A, B](kind, k, reusable, keys, hashKind, engine, seed)(map, hash)
+
+  def makeObjects[A, B: ClassTag](k: Int, reusable: Boolean, engine: Int, seed: Long)(map: A => B): Sampler[A, B] =
+    new ObjectSampler[A, B](k, reusable, new FfmIndexOps(k, reusable, engine, seed))(map)
+}
+
+/** [[IndexOps]] over the FFM downcalls: an ELEMENTS handle (8-byte key width, never used for keys)
+  * whose slots the engine fills by index only (rsv_commit_indexed); the B values live in the
+  * [[ObjectSampler]].  The offsets come back through one native k-entry buffer. */
+private[reservoir] final class FfmIndexOps(k: Int, reusable: Boolean, engine: Int, seed: Long) extends IndexOps {
+  import Native._
+
+  private[this] val arena = Arena.ofShared()
+  private[this] val handle: MemorySegment = {
+    val cfg = arena.allocate(Config)
+    check(rsvConfigInit.invoke(cfg).asInstanceOf[Int])
+    cfg.set(JAVA_INT, 4L, Abi.KindElements)
+    cfg.set(JAVA_INT, 8L, k)
+    cfg.set(JAVA_INT, 16L, if (reusable) 1 else 0)
+    cfg.set(JAVA_INT, 24L, engine)
+    cfg.set(JAVA_LONG, 40L, seed)
+    val out = arena.allocate(ADDRESS)
+    check(rsvCreate.invoke(cfg, out).asInstanceOf[Int])
+    out.get(ADDRESS, 0L)
+  }
+  private[this] val offs = arena.allocate(8L * k, 8L)
+  private[this] val cleanable = {
+    val h = handle
+    val a = arena
+    cleaner.register(this, () => { rsvDestroy.invoke(h); a.close() })
+  }
+
+  def sampleIndexed(n: Long, offsets: Array[Long]): Unit = {
+    check(rsvSampleIndexed.invoke(handle, n, offs).asInstanceOf[Int])
+    MemorySegment.copy(offs, JAVA_LONG, 0L, offsets, 0, k)
+  }
+  def commitIndexed(): Unit = check(rsvCommitIndexed.invoke(handle).asInstanceOf[Int])
+  def abortIndexed(): Unit  = check(rsvAbortIndexed.invoke(handle).asInstanceOf[Int])
+  def release(): Unit       = cleanable.clean()
 }

@@ -163,6 +163,16 @@ rsv_status rsv_fill_slots(rsv_sampler* s, const void* keys_host);
  * throw: after a throwing `map` the two differ in which of the batch's elements count.
  * RSV_E_ILLEGAL_STATE without a pending rsv_sample_indexed. */
 rsv_status rsv_abort_indexed(rsv_sampler* s);
+/* Accept the pending rsv_sample_indexed batch without keys: the caller keeps the elements itself.
+ * For a `Sampler[A, B]` whose B has no fixed-width key (a case class, a String, any JVM object:
+ * S:128-136 takes any B with a ClassTag), the binding holds the k-slot array of B references
+ * (RandomElements.samples, S:200-202) and writes slots[j] = map(seq(slot_offsets[j])) (or the
+ * already mapped element of a buffered batch) -- the engine decides WHICH element each slot holds
+ * from the indices alone and never sees a B.  Afterwards the handle's slots hold no keys:
+ * rsv_result / rsv_result_device / rsv_export_* return RSV_E_ILLEGAL_STATE, and every further batch
+ * must be index-only (rsv_sample_indexed + rsv_commit_indexed or rsv_abort_indexed).
+ * ELEMENTS samplers; RSV_E_ILLEGAL_STATE without a pending rsv_sample_indexed. */
+rsv_status rsv_commit_indexed(rsv_sampler* s);
 
 /* Sampler.result() (S:59-60; resultImpl S:318-331; RandomValues.result S:411).  Writes
  * min(count, k) keys (ELEMENTS: slot order, which is part of the reference result) or the distinct

@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
     "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read", "rsv_stage_acquire",
     "rsv_stage_commit", "rsv_get_distinct_info", "rsv_export_log", "rsv_merge_log",
-    "rsv_sample_indexed", "rsv_fill_slots", "rsv_abort_indexed", "rsv_retain_log",
+    "rsv_sample_indexed", "rsv_fill_slots", "rsv_abort_indexed", "rsv_retain_log", "rsv_commit_indexed",
 )
 
 
@@ -142,6 +142,7 @@ def load():
     L.rsv_sample_indexed.argtypes = [vp, i64, vp]
     L.rsv_fill_slots.argtypes = [vp, vp]
     L.rsv_abort_indexed.argtypes = [vp]
+    L.rsv_commit_indexed.argtypes = [vp]
     L.rsv_retain_log.argtypes = [vp, i32]
     for name in ("rsv_config_init", "rsv_create", "rsv_sample", "rsv_sample_batch", "rsv_result",
                  "rsv_result_device", "rsv_result_take", "rsv_set_stream", "rsv_set_resolve_stream",
@@ -150,7 +151,8 @@ def load():
                  "rsv_export_draws", "rsv_profile_enable", "rsv_profile_read", "rsv_export_packed",
                  "rsv_merge_packed", "rsv_profile_global", "rsv_profile_global_read", "rsv_stage_acquire",
                  "rsv_stage_commit", "rsv_get_distinct_info", "rsv_export_log", "rsv_merge_log",
-                 "rsv_sample_indexed", "rsv_fill_slots", "rsv_abort_indexed", "rsv_retain_log"):
+                 "rsv_sample_indexed", "rsv_fill_slots", "rsv_abort_indexed", "rsv_retain_log",
+                 "rsv_commit_indexed"):
         getattr(L, name).restype = i32
     if L.rsv_abi_version() != 1:
         raise ImportError("libreservoir_hip.so ABI version mismatch")

@@ -128,6 +128,8 @@ struct rsv_sampler {
     // whether the caller still owes those elements' keys (rsv_fill_slots)
     int64_t* idx_offs_d = nullptr;
     bool keys_owed = false;
+    // rsv_commit_indexed: the caller keeps the elements (any JVM B); the slots hold no keys
+    bool keys_external = false;
     // rsv_abort_indexed: the slot indices before the pending index-only batch, and its start
     int64_t* idx_bak_d = nullptr;
     bool idx_fresh = false;
@@ -275,6 +277,14 @@ rsv_status check_open(const rsv_sampler* s) {  // SingleUse.checkOpen, Sampler.s
     if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
     if (!s->open) return fail(RSV_E_ILLEGAL_STATE, "use of sampler after calling `result()`");
     if (s->keys_owed) return fail(RSV_E_ILLEGAL_STATE, "rsv_fill_slots is pending after rsv_sample_indexed");
+    return RSV_OK;
+}
+
+// entry points that read or write keys: not on a handle whose caller keeps the elements
+rsv_status check_keyed(const rsv_sampler* s) {
+    if (rsv_status st = check_open(s)) return st;
+    if (s->keys_external)
+        return fail(RSV_E_ILLEGAL_STATE, "the slots hold no keys (rsv_commit_indexed): index-only batches only");
     return RSV_OK;
 }
 
@@ -940,7 +950,7 @@ static rsv_status stage_slow(rsv_sampler* s, bool pre) {
 
 rsv_status rsv_sample(rsv_sampler* s, const void* key, const int64_t* hash) {
     // per-element hot path (the akka operator calls this per element): no HIP call here
-    if (!s || !s->open) return check_open(s);
+    if (!s || !s->open || s->keys_external) return check_keyed(s);
     if (!key) return fail(RSV_E_NULL_POINTER, "key is NULL");
     const bool pre = s->hash_kind == kHashPrecomputed && s->cfg.kind == RSV_KIND_DISTINCT;
     if (pre && !hash) return fail(RSV_E_NULL_POINTER, "hash is NULL for RSV_HASH_PRECOMPUTED");
@@ -957,7 +967,7 @@ rsv_status rsv_sample(rsv_sampler* s, const void* key, const int64_t* hash) {
 }
 
 rsv_status rsv_stage_acquire(rsv_sampler* s, void** keys_out, int64_t** hashes_out, int64_t* capacity) {
-    if (!s || !s->open) return check_open(s);
+    if (!s || !s->open || s->keys_external) return check_keyed(s);
     if (!keys_out || !capacity) return fail(RSV_E_NULL_POINTER, "keys_out/capacity is NULL");
     const bool pre = s->hash_kind == kHashPrecomputed && s->cfg.kind == RSV_KIND_DISTINCT;
     if (s->stage_n == 0 || s->stage_n == s->stage_cap) {
@@ -971,7 +981,7 @@ rsv_status rsv_stage_acquire(rsv_sampler* s, void** keys_out, int64_t** hashes_o
 }
 
 rsv_status rsv_stage_commit(rsv_sampler* s, int64_t n) {
-    if (!s || !s->open) return check_open(s);
+    if (!s || !s->open || s->keys_external) return check_keyed(s);
     if (n < 0 || n > s->stage_cap - s->stage_n)
         return fail(RSV_E_ILLEGAL_ARGUMENT, "commit exceeds the acquired staging capacity");
     s->stage_n += n;
@@ -983,7 +993,7 @@ rsv_status rsv_stage_commit(rsv_sampler* s, int64_t n) {
 }
 
 rsv_status rsv_sample_batch(rsv_sampler* s, const void* keys, int64_t n, int32_t mem, const int64_t* hashes) {
-    if (rsv_status st = check_open(s)) return st;
+    if (rsv_status st = check_keyed(s)) return st;
     if (n < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative batch size");
     if (n == 0) return RSV_OK;
     if (!keys) return fail(RSV_E_NULL_POINTER, "keys is NULL");
@@ -1018,6 +1028,8 @@ rsv_status rsv_sample_indexed(rsv_sampler* s, int64_t n, int64_t* slot_offsets_h
 rsv_status rsv_fill_slots(rsv_sampler* s, const void* keys_host) {
     if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
     if (!s->keys_owed) return fail(RSV_E_ILLEGAL_STATE, "rsv_fill_slots without a pending rsv_sample_indexed");
+    if (s->keys_external)
+        return fail(RSV_E_ILLEGAL_STATE, "the slots hold no keys (rsv_commit_indexed): commit or abort the batch");
     if (!keys_host) return fail(RSV_E_NULL_POINTER, "keys_host is NULL");
     DeviceGuard g(s->device);
     if (rsv_status st = ensure_gather(s)) return st;
@@ -1049,12 +1061,22 @@ rsv_status rsv_abort_indexed(rsv_sampler* s) {
     return RSV_OK;
 }
 
+rsv_status rsv_commit_indexed(rsv_sampler* s) {
+    if (!s) return fail(RSV_E_NULL_POINTER, "sampler is NULL");
+    if (!s->keys_owed) return fail(RSV_E_ILLEGAL_STATE, "rsv_commit_indexed without a pending rsv_sample_indexed");
+    // the slot indices are final (index_batch); the keys stay with the caller
+    s->keys_owed = false;
+    s->keys_external = true;
+    s->pub_valid = false;
+    return RSV_OK;
+}
+
 // Wait until a publication kernel has stored `gen` in the result flag (spin_flag)
 static rsv_status wait_flag(rsv_sampler* s, uint32_t gen) { return spin_flag(s, s->result_flag, gen, "result publish"); }
 
 static rsv_status result_impl(rsv_sampler* s, void* out, int64_t cap, int64_t* out_n, bool device_out,
                               bool take = false) {
-    if (rsv_status st = check_open(s)) return st;
+    if (rsv_status st = check_keyed(s)) return st;
     if (!out_n) return fail(RSV_E_NULL_POINTER, "out_n is NULL");
     DeviceGuard g(s->device);
     if (rsv_status st = flush_stage(s)) return st;
@@ -1145,7 +1167,7 @@ rsv_status rsv_result_device(rsv_sampler* s, void* out_dev, int64_t cap, int64_t
 }
 
 rsv_status rsv_result_take(rsv_sampler* s, void** buf, int64_t* out_n) {
-    if (rsv_status st = check_open(s)) return st;
+    if (rsv_status st = check_keyed(s)) return st;
     if (!buf || !out_n) return fail(RSV_E_NULL_POINTER, "buf / out_n is NULL");
     if (s->cfg.reusable || (int64_t)s->k * s->kw > kPublishMaxBytes)
         return fail(RSV_E_UNSUPPORTED, "rsv_result_take: single-use samplers with a published result only");
@@ -1294,7 +1316,7 @@ rsv_status rsv_seek(rsv_sampler* s, int64_t index) {
 
 rsv_status rsv_export_state(rsv_sampler* s, int64_t* idx_dev, void* keys_dev, int64_t* hash_dev,
                             int64_t* out_n) {
-    if (rsv_status st = check_open(s)) return st;
+    if (rsv_status st = check_keyed(s)) return st;
     if (!out_n) return fail(RSV_E_NULL_POINTER, "out_n is NULL");
     DeviceGuard g(s->device);
     touch(s);
@@ -1318,7 +1340,7 @@ rsv_status rsv_export_state(rsv_sampler* s, int64_t* idx_dev, void* keys_dev, in
 
 rsv_status rsv_merge_state(rsv_sampler* s, const int64_t* idx_dev, const void* keys_dev, const int64_t* hash_dev,
                            const int64_t* part_n_host, int32_t parts, int64_t part_len, int64_t total_count) {
-    if (rsv_status st = check_open(s)) return st;
+    if (rsv_status st = check_keyed(s)) return st;
     if (parts < 0 || part_len < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative parts/part_len");
     if (parts > 0 && !keys_dev) return fail(RSV_E_NULL_POINTER, "keys_dev is NULL");
     DeviceGuard g(s->device);
@@ -1397,7 +1419,7 @@ rsv_status rsv_retain_log(rsv_sampler* s, int32_t on) {
 }
 
 rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev) {
-    if (rsv_status st = check_open(s)) return st;
+    if (rsv_status st = check_keyed(s)) return st;
     if (!row_dev) return fail(RSV_E_NULL_POINTER, "row_dev is NULL");
     DeviceGuard g(s->device);
     touch(s);
@@ -1415,7 +1437,7 @@ rsv_status rsv_export_packed(rsv_sampler* s, int64_t* row_dev) {
 
 rsv_status rsv_merge_packed(rsv_sampler* s, const int64_t* rows_dev, int32_t parts, int64_t row_stride,
                             int64_t total_count) {
-    if (rsv_status st = check_open(s)) return st;
+    if (rsv_status st = check_keyed(s)) return st;
     if (parts < 0) return fail(RSV_E_ILLEGAL_ARGUMENT, "negative parts");
     if (s->cfg.kind == RSV_KIND_DISTINCT) {
         // [keys (k, as int64 words: key_width / 8 each for byte keys) | hashes (k) | 6 meta words]

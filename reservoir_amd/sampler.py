@@ -152,8 +152,13 @@ class GpuSampler:
                  key_type: str = "long", engine: str = "philox_r", seed: int | None = None,
                  stream_id: int = 0, device: int | None = None, order: str = "auto",
                  retain_log: bool = False):
+        self._objects = key_type == "object"
+        if self._objects:
+            if kind != N.KIND_ELEMENTS:
+                raise IllegalArgumentException("key_type 'object' is for Sampler.apply (distinct needs keys)")
+            key_type = "long"  # the handle's key width; its slots never hold keys (rsv_commit_indexed)
         if key_type not in _KEY and not _wide_width(key_type):
-            raise IllegalArgumentException(f"key_type must be one of {sorted(_KEY)} or 'bytesN'")
+            raise IllegalArgumentException(f"key_type must be one of {sorted(_KEY)}, 'bytesN' or 'object'")
         if engine not in _ENGINE:
             raise IllegalArgumentException(f"engine must be one of {sorted(_ENGINE)}")
         if order not in _ORDER:
@@ -191,6 +196,10 @@ class GpuSampler:
         self._precomputed = hash_kind == N.HASH_PRECOMPUTED
         self._rows = None  # the last merge_packed's rows (a distinct merge reads them until it settles)
         self._ordered = False
+        if self._objects:  # ObjectSampler's state: the slot array and the buffered mapped elements
+            self._slots: list = []
+            self._pending: list = []
+            self._obj_count = 0
         if kind == N.KIND_DISTINCT:
             self._ordered = bool(self.distinct_info()["ordered"])  # no device work at creation
             if retain_log:
@@ -251,8 +260,53 @@ class GpuSampler:
             hv = C.c_int64(int(self._hash_fn(key)))
         return key, hv
 
+    # -- any B (key_type="object"): bindings/scala/core/.../gpu/ObjectSampler.scala's protocol ----
+    _OBJ_BATCH = 65536
+
+    def _obj_check_open(self) -> None:
+        if self._h is None or not self._L.rsv_is_open(self._h):
+            raise IllegalStateException("use of sampler after calling `result()`")
+
+    def _obj_place(self, offs, values_at) -> None:
+        """the batch's new slot holders into the slot array (values_at(offset) -> B)"""
+        for j in np.flatnonzero(offs >= 0).tolist():
+            if j >= len(self._slots):
+                self._slots.extend([None] * (j + 1 - len(self._slots)))
+            self._slots[j] = values_at(int(offs[j]))
+
+    def _obj_flush(self) -> None:
+        n = len(self._pending)
+        if not n:
+            return
+        offs = np.empty(self._k, dtype=np.int64)
+        N.check(self._L.rsv_sample_indexed(self._h, n, offs.ctypes.data_as(C.c_void_p)))
+        N.check(self._L.rsv_commit_indexed(self._h))
+        pending, self._pending = self._pending, []
+        self._obj_place(offs, pending.__getitem__)
+        self._obj_count += n
+
+    def _obj_sample_indexed(self, seq) -> None:
+        self._obj_flush()
+        n = len(seq)
+        offs = np.empty(self._k, dtype=np.int64)
+        N.check(self._L.rsv_sample_indexed(self._h, n, offs.ctypes.data_as(C.c_void_p)))
+        try:  # map the new holders first: the slots change only once all of them are mapped
+            vals = {int(o): self._map(seq[int(o)]) for o in offs[offs >= 0].tolist()}
+        except BaseException:
+            N.check(self._L.rsv_abort_indexed(self._h))
+            raise
+        N.check(self._L.rsv_commit_indexed(self._h))
+        self._obj_place(offs, vals.__getitem__)
+        self._obj_count += n
+
     def sample(self, element: Any) -> None:
         """Sampler.sample (Sampler.scala:37-38)."""
+        if self._objects:
+            self._obj_check_open()
+            self._pending.append(self._map(element))
+            if len(self._pending) == self._OBJ_BATCH:
+                self._obj_flush()
+            return
         if not self._L.rsv_is_open(self._h):
             raise IllegalStateException("use of sampler after calling `result()`")
         key, hv = self._key_hash(element)
@@ -271,6 +325,14 @@ class GpuSampler:
         device) instead of calling ``hash`` per element on the host."""
         if hashes is not None:
             self._sample_device_hashed(elements, hashes)
+            return
+        if self._objects:
+            self._obj_check_open()
+            if _indexed(elements) and len(elements) > 0:
+                self._obj_sample_indexed(elements)
+            else:
+                for x in elements:
+                    self.sample(x)
             return
         if _is_torch_cuda(elements) and self._map is identity and not self._precomputed:
             # device fast path; checkOpen() first, as the reference does before any other work
@@ -396,6 +458,13 @@ class GpuSampler:
 
     def result(self) -> np.ndarray:
         """Sampler.result (Sampler.scala:59-60). Slot order for element samplers."""
+        if self._objects:  # a list of the B values in slot order
+            self._obj_check_open()
+            self._obj_flush()
+            out = list(self._slots[: min(self._obj_count, self._k)])
+            if not self._reusable:
+                self.close()
+            return out
         if self._h is None or not self._L.rsv_is_open(self._h):
             raise IllegalStateException("use of sampler after calling `result()`")
         if not self._reusable and self._width <= 8:

@@ -11,6 +11,10 @@
 //         elements per element first, then the rest of the sequence by index -- map (here: the
 //         key of offset i) runs only for the slots' new holders, no key buffer for the sequence
 //   jidx  the same through rsv_jvm (JniSampler.sampleAll's natives)
+//   fobj  ObjectSampler.scala (a Sampler[A, B] for any B: the B values stay on the JVM) over the
+//         FFM downcalls: buffered sample() batches and IndexedSeq batches by index only
+//         (rsv_sample_indexed + rsv_commit_indexed), a throwing map undone by rsv_abort_indexed
+//   jobj  the same through rsv_jvm (JniIndexOps)
 // Each case line of argv[1] names the sampler, its keys (splitmix64(base + i), or a binary key file)
 // and a binary file with the oracle's expected result (tests/test_gpu_ffm.py writes them);
 // distinct results compare as sets.
@@ -140,6 +144,117 @@ struct FfmMirror {
     }
     ~FfmMirror() {
         if (handle) rsv_destroy(handle);  // the Cleaner of a reusable sampler
+    }
+};
+
+// ---- ObjectMirror: ObjectSampler.scala (a Sampler[A, B] for any B), line for line ----------------
+// The B values are int64 "references" here; the IndexOps are the FFM downcalls (FfmIndexOps) or the
+// rsv_jvm session functions every JNI native of JniIndexOps calls.
+struct MapThrew : std::runtime_error {
+    MapThrew() : std::runtime_error("map threw") {}
+};
+
+struct ObjectMirror {
+    static constexpr int Batch = 65536;
+    bool via_jvm, reusable, open = true, aliased = false;
+    int k;
+    rsv_sampler* handle = nullptr;  // FfmIndexOps
+    rsv_jvm js;                     // JniIndexOps
+    std::vector<int64_t> slots, pending, offsets;
+    int n = 0;
+    int64_t count = 0;
+
+    ObjectMirror(const rsv_config& c, bool jvm) : via_jvm(jvm), reusable(c.reusable != 0), k(c.max_sample_size) {
+        rsv_config cfg = c;
+        cfg.key_width = 8;  // never used for keys
+        if (via_jvm) check(rsv_jvm_create(&js, &cfg));
+        else check(rsv_create(&cfg, &handle));
+        slots.resize((size_t)std::min(16, k));
+        pending.resize(Batch);
+    }
+    ~ObjectMirror() { release(); }
+    void release() {
+        if (via_jvm) rsv_jvm_destroy(&js);
+        else if (handle) rsv_destroy(handle);
+        handle = nullptr;
+    }
+    // IndexOps
+    void sample_indexed(int64_t len, int64_t* o) {
+        check(via_jvm ? rsv_jvm_sample_indexed(&js, len, o) : rsv_sample_indexed(handle, len, o));
+    }
+    void commit() { check(via_jvm ? rsv_jvm_commit_indexed(&js) : rsv_commit_indexed(handle)); }
+    void abort() { check(via_jvm ? rsv_jvm_abort_indexed(&js) : rsv_abort_indexed(handle)); }
+
+    void ensure_size(int j) {
+        if ((int)slots.size() <= j) {
+            const size_t len = slots.size();
+            const size_t grow = std::min<size_t>((size_t)k, len << 1);
+            slots.resize(std::max<size_t>(grow, (size_t)j + 1));
+        }
+    }
+    int64_t* offset_array() {
+        if (offsets.empty()) offsets.resize((size_t)k);
+        return offsets.data();
+    }
+    void flush() {
+        if (n == 0) return;
+        int64_t* o = offset_array();
+        sample_indexed(n, o);
+        commit();
+        aliased = false;  // (a copy in the JVM; the vector here is never shared)
+        for (int j = 0; j < k; ++j)
+            if (o[j] >= 0) {
+                ensure_size(j);
+                slots[(size_t)j] = pending[(size_t)o[j]];
+            }
+        count += n;
+        n = 0;
+    }
+    void sample(int64_t b) {
+        if (!open) throw JvmException(RSV_E_ILLEGAL_STATE, "use of sampler after calling `result()`");
+        pending[(size_t)n++] = b;
+        if (n == Batch) flush();
+    }
+    // sampleAll over a known-size IndexedSeq; map(i) = the element at offset i (may throw MapThrew).
+    // Returns the number of map calls.
+    template <class Map>
+    int64_t sample_all_indexed(int64_t len, Map map) {
+        if (!open) throw JvmException(RSV_E_ILLEGAL_STATE, "use of sampler after calling `result()`");
+        flush();
+        int64_t* o = offset_array();
+        sample_indexed(len, o);
+        std::vector<int> js_;
+        std::vector<int64_t> vals;
+        int64_t calls = 0;
+        try {
+            for (int j = 0; j < k; ++j)
+                if (o[j] >= 0) {
+                    ++calls;
+                    vals.push_back(map(o[j]));
+                    js_.push_back(j);
+                }
+        } catch (...) {
+            abort();
+            throw;
+        }
+        commit();
+        for (size_t c = 0; c < js_.size(); ++c) {
+            ensure_size(js_[c]);
+            slots[(size_t)js_[c]] = vals[c];
+        }
+        count += len;
+        return calls;
+    }
+    std::vector<int64_t> result() {
+        if (!open) throw JvmException(RSV_E_ILLEGAL_STATE, "use of sampler after calling `result()`");
+        flush();
+        const int64_t m = std::min<int64_t>(count, k);
+        std::vector<int64_t> out(slots.begin(), slots.begin() + m);
+        if (!reusable) {
+            open = false;
+            release();
+        }
+        return out;
     }
 };
 
@@ -383,6 +498,59 @@ static void run_indexed(const Case& c, bool ffm) {
                 (long long)(c.n - pre));
 }
 
+// A Sampler[A, B] for any B (ObjectSampler): element i of the stream is the "reference" i, so the
+// reservoir must hold the oracle's last-writer indices.  The first `pre` elements go through
+// sample() (one full 65536-element buffer flushed by index, the rest buffered), then the remaining
+// ones as an IndexedSeq whose map throws on its third call (the batch is dropped, the exception
+// propagates), then the same IndexedSeq again with a map that succeeds.
+static void run_objects(const Case& c, bool jvm) {
+    ObjectMirror s(config_of(c), jvm);
+    const int64_t pre = std::min<int64_t>(c.n, 100003);
+    for (int64_t i = 0; i < pre; ++i) s.sample(i);
+    const int64_t rest = c.n - pre;
+    int64_t calls = 0;
+    if (rest > 0) {
+        int64_t seen = 0;
+        bool threw = false;
+        try {
+            s.sample_all_indexed(rest, [&](int64_t o) -> int64_t {
+                if (++seen == 3) throw MapThrew();
+                return pre + o;
+            });
+        } catch (const MapThrew&) {
+            threw = true;
+        }
+        EXPECT(threw || seen < 3, c.name.c_str());
+        if (!jvm && pre > 0) {  // the handle's slots hold no keys now: keyed calls are refused
+            int64_t x = 0, nn = 0;
+            EXPECT(rsv_sample(s.handle, &x, nullptr) == RSV_E_ILLEGAL_STATE, c.name.c_str());
+            EXPECT(rsv_sample_batch(s.handle, &x, 1, RSV_MEM_HOST, nullptr) == RSV_E_ILLEGAL_STATE, c.name.c_str());
+            EXPECT(rsv_result(s.handle, &x, 1, &nn) == RSV_E_ILLEGAL_STATE, c.name.c_str());
+            EXPECT(rsv_commit_indexed(s.handle) == RSV_E_ILLEGAL_STATE, c.name.c_str());  // nothing pending
+        }
+        calls = s.sample_all_indexed(rest, [&](int64_t o) -> int64_t { return pre + o; });
+    }
+    std::vector<int64_t> got = s.result();
+    const std::vector<uint8_t> wb = read_file(c.expected);
+    std::vector<int64_t> want(wb.size() / 8);
+    std::memcpy(want.data(), wb.data(), wb.size());
+    EXPECT(got == want, c.name.c_str());
+    EXPECT(calls <= c.k, c.name.c_str());  // map ran only for the reservoir's new holders
+    if (c.reusable) {
+        EXPECT(s.result() == got && s.open, c.name.c_str());
+    } else {
+        bool ise = false;
+        try {
+            s.sample(0);
+        } catch (const JvmException& e) {
+            ise = e.status == RSV_E_ILLEGAL_STATE;
+        }
+        EXPECT(ise && !s.open, c.name.c_str());
+    }
+    std::printf("  %s: %lld indexed elements, map called %lld times\n", c.name.c_str(), (long long)rest,
+                (long long)calls);
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s cases.txt\n", argv[0]);
@@ -414,6 +582,8 @@ int main(int argc, char** argv) {
             else if (c.path == "abi") run_abi(c);
             else if (c.path == "fidx") run_indexed(c, true);
             else if (c.path == "jidx") run_indexed(c, false);
+            else if (c.path == "fobj") run_objects(c, false);
+            else if (c.path == "jobj") run_objects(c, true);
             else throw std::runtime_error("unknown path " + c.path);
         } catch (const std::exception& e) {
             std::printf("FAIL %s: exception %s\n", c.name.c_str(), e.what());

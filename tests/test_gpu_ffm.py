@@ -183,3 +183,40 @@ def test_indexed_sample_all_through_the_bindings(tmp_path, cuda, oracle):
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("PASS") == len(cases), r.stdout
+
+
+@pytest.mark.gpu
+def test_object_sampler_call_sequences(tmp_path, cuda, oracle):
+    """A Sampler[A, B] for any B (ObjectSampler.scala, round 6): the engine decides which element
+    each slot holds from the indices alone (rsv_sample_indexed + rsv_commit_indexed) and the JVM
+    keeps the B values.  With element i standing for the reference i, the reservoir must be the
+    oracle's last-writer indices (philox_r) and the reference's own Algorithm-L sampleIndexed walk
+    (java_l, Sampler.scala:261-273) -- at C2's 1e9 elements on both JVM paths, after buffered
+    sample() batches and a first sampleAll whose map throws (rsv_abort_indexed undoes it)."""
+    exe = build(tmp_path)
+    cases = []
+
+    def add(name, path, k, reusable, engine, seed, stream, n, want):
+        f = tmp_path / f"{name}.bin"
+        np.ascontiguousarray(want, dtype=np.int64).tofile(f)
+        cases.append(f"{name} {path} 0 {k} 8 {reusable} 0 0 {engine} {seed} {stream} {n} 0 {f}")
+
+    n = 1_000_000_000
+    win = oracle.algo_r_last_writers(0xC0FFEE, 0x5A5A, 1024, 0, n)
+    ref = oracle.AlgoL(1000, 0)
+    ref.sample_all_iota(0, n)
+    for path in ("fobj", "jobj"):
+        add(f"{path}_c2_philox", path, 1024, 0, 0, 0xC0FFEE, 0x5A5A, n, win)
+        add(f"{path}_c2_java_l", path, 1000, 1, 1, 0, 0, n, ref.result())
+    for n_small, k in ((500, 1024), (100_003, 70_000), (300_000, 64), (2_000_000, 100_000)):
+        w = oracle.algo_r_last_writers(7, 8, k, 0, n_small)
+        add(f"fobj_small_{n_small}_{k}", "fobj", k, 1, 0, 7, 8, n_small, w[w >= 0])
+        r = oracle.AlgoL(k, 3)
+        r.sample_all_iota(0, n_small)
+        add(f"jobj_small_java_l_{n_small}_{k}", "jobj", k, 0, 1, 3, 0, n_small, r.result())
+    f = tmp_path / "cases.txt"
+    f.write_text("\n".join(cases) + "\n")
+    r = subprocess.run([str(exe), str(f)], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("PASS") == len(cases), r.stdout
