@@ -227,6 +227,42 @@ __host__ __device__ __forceinline__ int64_t hash_of(KeyT key) {
     }
 }
 
+// lane ^ s exchange (wave64) without the LDS crossbar (ds_bpermute: an LDS round trip on the sort networks'
+// dependent chains): quad_perm DPP for s = 1, 2, two row shifts for 4, row_ror for 8, the gfx950
+// permlane16/32 swaps for 16, 32.  s folds to a constant once the networks are unrolled.
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v, int s) {
+    switch (s) {
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    case 4: {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xF, 0xF, false);  // row_shl:4 (i + 4)
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, false);  // row_shr:4 (i - 4)
+        return (threadIdx.x & 4) ? dn : up;
+    }
+    case 8: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    case 16: {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (threadIdx.x & 16) ? r[0] : r[1];
+    }
+    case 32: {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (threadIdx.x & 32) ? r[0] : r[1];
+    }
+    default: return (uint32_t)__shfl_xor((int)v, s);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T xor_any(T v, int s) {
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t x = (uint64_t)v;
+        const uint32_t lo = xor_lane32((uint32_t)x, s), hi = xor_lane32((uint32_t)(x >> 32), s);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)xor_lane32((uint32_t)v, s);
+    }
+}
+
 // End of a one-workgroup host publication: every wave waits for its own stores, the workgroup
 // barrier orders them before lane 0, and lane 0 alone runs the system-scope release (L2 write-back)
 // and stores the flag.  (A __threadfence_system() in every wave cost ~4 us more per publication.)

@@ -511,6 +511,322 @@ __global__ __launch_bounds__(kWBlock) void wide_export_row(const int64_t* __rest
     }
 }
 
+// ---- bucketed merge (round 6) --------------------------------------------------------------------
+// set ∪ candidates -> buckets by h (a monotone map of [INT64_MIN, span_hi] onto B = 2^lb buckets,
+// ~64 entries each: the scrambled hash is uniform) -> one wave per bucket sorts (h, entry) in
+// registers (bitonic network over DPP lane exchanges), puts each run of equal h in key-word order in
+// LDS (the lane at the run's start; runs are one key's repeats or colliding hashes), keeps the first
+// of each distinct (h, key) with its element's first arrival -> each bucket's distinct entries land
+// at their global rank (the first k are the new set).  Three dispatches instead of the radix sort's
+// eight passes, the scan and the flag kernels.  A bucket above kWCap entries or a run above kRunMax
+// (a degenerate hash) sets ctl[1]: the host then runs the sort-based merge instead.
+//   bucket area: bh / be / ba [B x kWCap] (h, entry id, first arrival), cnt [B x kWStride] (one
+//   128-B line per counter: neighbouring atomics would serialise on a shared line; wb_sort re-zeroes
+//   what it consumed), bdist [B] distinct per bucket, gsum [B / 16 + 1] their group sums.
+constexpr uint32_t kWCap = 256;
+constexpr uint32_t kWAvgLog = 6;
+constexpr uint32_t kWStride = 32;
+constexpr uint32_t kWEmitBuckets = 16;
+
+// bucket of u = h - INT64_MIN in [0, span]: floor(u B / (span + 1)) as umulhi(u, q B), q =
+// floor((2^64 - 1) / (span + 1)) from the host; a span below B buckets u directly
+struct WBucketMap {
+    uint64_t mult;
+    uint32_t last;
+    __device__ __forceinline__ WBucketMap(uint64_t q, uint32_t lb) {
+        last = lb ? (1u << lb) - 1u : 0u;
+        mult = lb == 0 ? 0ull : ((q >> (64 - lb)) ? 0ull : q << lb);
+    }
+    __device__ __forceinline__ uint32_t operator()(int64_t h) const {
+        const uint64_t u = (uint64_t)h ^ 0x8000000000000000ull;
+        const uint64_t b = mult ? __umul64hi(u, mult) : (last ? u : 0ull);
+        return (uint32_t)(b < last ? b : last);
+    }
+};
+
+__global__ __launch_bounds__(kWBlock) void wb_scatter(const int64_t* __restrict__ set_h, int64_t m,
+                                                      const int64_t* __restrict__ cand_h, int64_t c, uint64_t q,
+                                                      uint32_t lb, int64_t* __restrict__ bh, uint32_t* __restrict__ be,
+                                                      uint32_t* __restrict__ cnt, uint32_t* __restrict__ gsum,
+                                                      int64_t* __restrict__ ctl) {
+    if (blockIdx.x == 0)
+        for (uint32_t i = threadIdx.x; i <= ((1u << lb) >> 4); i += blockDim.x) gsum[i] = 0;
+    const WBucketMap map(q, lb);
+    const int64_t total = m + c, stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+        const int64_t h = e < m ? set_h[e] : cand_h[e - m];
+        const uint32_t b = map(h);
+        const uint32_t p = atomicAdd(&cnt[(size_t)b * kWStride], 1u);
+        if (p < kWCap) {
+            bh[(size_t)b * kWCap + p] = h;
+            be[(size_t)b * kWCap + p] = (uint32_t)e;
+        } else {
+            ctl[1] = 1;
+        }
+    }
+}
+
+// (u, e) ascending, u = h - INT64_MIN (unsigned order = signed order of h), e the entry id
+__device__ __forceinline__ bool ue_less(uint64_t ua, uint32_t ea, uint64_t ub, uint32_t eb) {
+    return ua < ub || (ua == ub && ea < eb);
+}
+
+// bitonic network over 64 R entries, entry i = r * 64 + lane in register slot r
+template <int R>
+__device__ __forceinline__ void wb_bitonic(uint64_t (&u)[R], uint32_t (&e)[R]) {
+    const uint32_t lane = threadIdx.x & 63;
+    constexpr uint32_t N = 64u * R;
+#pragma unroll
+    for (uint32_t size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 64) {
+                const uint32_t rs = stride / 64;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if ((r & rs) == 0) {
+                        const int r2 = r + rs;
+                        const bool up = ((r * 64u + lane) & size) == 0;
+                        if (ue_less(u[r2], e[r2], u[r], e[r]) == up) {
+                            const uint64_t tu = u[r];
+                            const uint32_t te = e[r];
+                            u[r] = u[r2];
+                            e[r] = e[r2];
+                            u[r2] = tu;
+                            e[r2] = te;
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint64_t ou = xor_any(u[r], (int)stride);
+                    const uint32_t oe = xor_any(e[r], (int)stride);
+                    const bool lower = (lane & stride) == 0;
+                    const bool up = ((r * 64u + lane) & size) == 0;
+                    const bool take = (lower == up) ? ue_less(ou, oe, u[r], e[r]) : ue_less(u[r], e[r], ou, oe);
+                    if (take) {
+                        u[r] = ou;
+                        e[r] = oe;
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void wb_sort_regs(const int64_t* gh, const uint32_t* ge, uint32_t n, uint64_t* su,
+                                             uint32_t* se) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t u[R];
+    uint32_t e[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = r * 64u + lane;
+        u[r] = i < n ? ((uint64_t)gh[i] ^ 0x8000000000000000ull) : ~0ull;
+        e[r] = i < n ? ge[i] : ~0u;
+    }
+    wb_bitonic<R>(u, e);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = r * 64u + lane;
+        if (i < n) {
+            su[i] = u[r];
+            se[i] = e[r];
+        }
+    }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// One wave per bucket: sort, order runs of equal h by the key words, keep the first entry of each
+// distinct (h, key) compacted at the bucket's start (with the element's first arrival when cand_i is
+// given: -1 for a set member, else the earliest batch offset among its candidate entries).
+__global__ __launch_bounds__(kWBlock) void wb_sort(int64_t m, uint32_t lb, int64_t* __restrict__ bh,
+                                                   uint32_t* __restrict__ be, int64_t* __restrict__ ba,
+                                                   uint32_t* __restrict__ cnt, uint32_t* __restrict__ bdist,
+                                                   uint32_t* __restrict__ gsum, WRows R,
+                                                   const int64_t* __restrict__ cand_i, int64_t* __restrict__ ctl) {
+    __shared__ uint64_t s_u[kWBlock / 64][kWCap];
+    __shared__ uint32_t s_e[kWBlock / 64][kWCap];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t b = blockIdx.x * (kWBlock / 64) + w;
+    if (b >= (1u << lb)) return;
+    uint32_t* pc = cnt + (size_t)b * kWStride;
+    const uint32_t n = *pc;
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) *pc = 0;  // consumed: zero for the next merge
+    if (n == 0 || n > kWCap) {  // (an overfull bucket set ctl[1] in the scatter)
+        if (lane == 0) bdist[b] = 0;
+        return;
+    }
+    int64_t* gh = bh + (size_t)b * kWCap;
+    uint32_t* ge = be + (size_t)b * kWCap;
+    uint64_t* su = s_u[w];
+    uint32_t* se = s_e[w];
+    if (n <= 64) wb_sort_regs<1>(gh, ge, n, su, se);
+    else if (n <= 128) wb_sort_regs<2>(gh, ge, n, su, se);
+    else wb_sort_regs<4>(gh, ge, n, su, se);
+    wave_lds_sync();
+    // runs of equal h: the lane at the run's start orders it by the key words (insertion sort)
+    for (uint32_t i = lane; i < n; i += 64) {
+        if ((i > 0 && su[i - 1] == su[i]) || i + 1 >= n || su[i + 1] != su[i]) continue;
+        uint32_t L = 2;
+        while (i + L < n && su[i + L] == su[i] && L <= (uint32_t)kRunMax) ++L;
+        if (L > (uint32_t)kRunMax) {
+            ctl[1] = 1;
+            continue;
+        }
+        for (uint32_t a = 1; a < L; ++a) {
+            const uint32_t x = se[i + a];
+            uint32_t j = a;
+            while (j > 0 && row_cmp(R(se[i + j - 1]), R(x), R.words) > 0) {
+                se[i + j] = se[i + j - 1];
+                --j;
+            }
+            se[i + j] = x;
+        }
+    }
+    wave_lds_sync();
+    // the first of each distinct (h, key), compacted; its element's first arrival
+    uint32_t base = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        bool first = false;
+        if (i < n) first = i == 0 || su[i - 1] != su[i] || row_cmp(R(se[i - 1]), R(se[i]), R.words) != 0;
+        const unsigned long long bal = __ballot(first);
+        if (first) {
+            const uint32_t o = base + (uint32_t)__popcll(bal & lanemask_lt_w());
+            if (ba) {
+                const uint32_t e0 = se[i];
+                int64_t a = (int64_t)e0 < m ? -1 : cand_i[(int64_t)e0 - m];
+                for (uint32_t j = i + 1; j < n && su[j] == su[i] && row_cmp(R(se[j]), R(e0), R.words) == 0; ++j) {
+                    const int64_t aj = (int64_t)se[j] < m ? -1 : cand_i[(int64_t)se[j] - m];
+                    a = aj < a ? aj : a;
+                }
+                ba[(size_t)b * kWCap + o] = a;
+            }
+            gh[o] = (int64_t)(su[i] ^ 0x8000000000000000ull);
+            ge[o] = se[i];
+        }
+        base += (uint32_t)__popcll(bal);
+    }
+    if (lane == 0) {
+        bdist[b] = base;
+        atomicAdd(gsum + (b >> 4), base);
+    }
+}
+
+// each bucket's distinct entries to their global rank (ranks < k): the set's hashes and key rows.
+// ctl[2] = distinct count, ctl[3] = the largest kept h, ctl[4] = rank k ties rank k - 1 on h (equal h
+// share a bucket: the map is monotone)
+__global__ __launch_bounds__(kWBlock) void wb_emit(uint32_t lb, const int64_t* __restrict__ bh,
+                                                   const uint32_t* __restrict__ be, const uint32_t* __restrict__ bdist,
+                                                   const uint32_t* __restrict__ gsum, int64_t k, WRows R,
+                                                   int64_t* __restrict__ out_h, uint64_t* __restrict__ out_k,
+                                                   int64_t* __restrict__ ctl) {
+    __shared__ uint64_t s_pre[kWBlock / 64], s_tot[kWBlock / 64];
+    __shared__ uint64_t s_base[kWEmitBuckets + 1];
+    const uint32_t B = 1u << lb;
+    const uint32_t b0 = blockIdx.x * kWEmitBuckets;
+    if (b0 >= B) return;
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t G = (B + 15) >> 4, g0 = b0 >> 4;
+    uint64_t pre = 0, tot = 0;
+    for (uint32_t i = t; i < G; i += kWBlock) {
+        const uint64_t v = gsum[i];
+        tot += v;
+        if (i < g0) pre += v;
+    }
+    for (uint32_t i = (g0 << 4) + t; i < b0; i += kWBlock) pre += bdist[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        pre += (uint64_t)__shfl_xor((long long)pre, off);
+        tot += (uint64_t)__shfl_xor((long long)tot, off);
+    }
+    if (lane == 0) {
+        s_pre[w] = pre;
+        s_tot[w] = tot;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint64_t p = 0, q = 0;
+        for (int i = 0; i < kWBlock / 64; ++i) {
+            p += s_pre[i];
+            q += s_tot[i];
+        }
+        const uint32_t nb = std::min<uint32_t>(kWEmitBuckets, B - b0);
+        for (uint32_t i = 0; i < nb; ++i) {
+            s_base[i] = p;
+            p += bdist[b0 + i];
+        }
+        s_base[kWEmitBuckets] = q;
+        if (b0 == 0) ctl[2] = (int64_t)q;
+    }
+    __syncthreads();
+    tot = s_base[kWEmitBuckets];
+    const uint64_t mk = std::min<uint64_t>(tot, (uint64_t)k);
+    for (uint32_t j = 0; j < kWEmitBuckets / (kWBlock / 64); ++j) {
+        const uint32_t bi = w * (kWEmitBuckets / (kWBlock / 64)) + j;
+        const uint32_t b = b0 + bi;
+        if (b >= B) break;
+        const uint64_t base = s_base[bi];
+        if (base > (uint64_t)k) break;  // later buckets rank higher still
+        const uint32_t cnt = bdist[b];
+        const int64_t* gh = bh + (size_t)b * kWCap;
+        const uint32_t* ge = be + (size_t)b * kWCap;
+        for (uint32_t r = lane; r < cnt; r += 64) {
+            const uint64_t rank = base + r;
+            if (rank < (uint64_t)k) {
+                const int64_t h = gh[r];
+                out_h[rank] = h;
+                const uint64_t* src = R(ge[r]);
+                for (int32_t q = 0; q < R.words; ++q) out_k[rank * R.words + q] = src[q];
+                if (rank + 1 == mk) ctl[3] = h;
+            } else if (rank == (uint64_t)k && r > 0 && gh[r - 1] == gh[r]) {
+                ctl[4] = 1;
+            }
+        }
+    }
+}
+
+// the scheduled pass's proof over the bucketed merge (wide_verify's rule: each distinct element with
+// first arrival a and hash h counts for the ranges r with range(a) < r and B_r > h)
+__global__ __launch_bounds__(kWBlock) void wb_verify(uint32_t lb, const int64_t* __restrict__ bh,
+                                                     const int64_t* __restrict__ ba, const uint32_t* __restrict__ bdist,
+                                                     const int64_t* __restrict__ rtab, int32_t R,
+                                                     unsigned long long* __restrict__ diff) {
+    __shared__ int64_t s_rs[kWMaxR + 1], s_rb[kWMaxR];
+    __shared__ int s_d[kWMaxR + 1];
+    WRanges rg{s_rs, s_rb, R};
+    for (int t = threadIdx.x; t <= R; t += blockDim.x) s_d[t] = 0;
+    rg.load(rtab);
+    const uint32_t B = 1u << lb, lane = threadIdx.x & 63;
+    const uint32_t wstride = gridDim.x * (kWBlock / 64);
+    for (uint32_t b = blockIdx.x * (kWBlock / 64) + (threadIdx.x >> 6); b < B; b += wstride) {
+        const uint32_t cnt = bdist[b];
+        for (uint32_t r = lane; r < cnt; r += 64) {
+            const int64_t h = bh[(size_t)b * kWCap + r], a = ba[(size_t)b * kWCap + r];
+            int32_t ra = -1;  // the range holding a
+            while (ra + 1 < R && s_rs[ra + 1] <= a) ++ra;
+            int32_t rh = -1;  // the last range whose bound exceeds h (bounds fall with r)
+            while (rh + 1 < R && s_rb[rh + 1] > h) ++rh;
+            if (ra + 1 <= rh) {
+                atomicAdd(&s_d[ra + 1], 1);
+                atomicAdd(&s_d[rh + 1], -1);
+            }
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t <= R; t += blockDim.x)
+        if (s_d[t]) atomicAdd(&diff[t], (unsigned long long)(int64_t)s_d[t]);
+}
+
 }  // namespace
 
 struct WideDistinct {
@@ -555,12 +871,21 @@ struct WideDistinct {
     std::vector<int64_t> arch_h;  // consumed candidates in arrival order
     std::vector<uint64_t> arch_k;
     // ordered mode's scheduled pass: range table + verification counts (device [0, 2 kWMaxR + 1) the
-    // table, [kSchedCounts, + kWMaxR + 1) the counts; pinned staging alike), and the set before the pass
+    // table, [kSchedCounts, + kWMaxR + 1) the counts; pinned staging alike)
     int64_t* sched = nullptr;
     int64_t* hsched = nullptr;
-    int64_t* bk_h = nullptr;
-    uint64_t* bk_k = nullptr;
-    int64_t bk_cap = 0;
+    // the bucketed merge's area (wb_scatter / wb_sort / wb_emit), sized for wb_cap buckets
+    int64_t* wb_h = nullptr;
+    uint32_t* wb_e = nullptr;
+    int64_t* wb_a = nullptr;
+    uint32_t* wb_cnt = nullptr;
+    uint32_t* wb_dist = nullptr;
+    uint32_t* wb_gsum = nullptr;
+    uint32_t wb_cap = 0;
+    bool bucketed_on = true;      // RSV_WIDE_BUCKETED=0: the sort-based merge only (A/B, tests)
+    bool last_bucketed = false;   // the last merge's sorted entries are in the bucket area (wb_verify)
+    uint32_t last_lb = 0;
+    int64_t merges = 0;           // merges applied (a set swap each)
     double sched_beta = 1.6;      // bound margin over the predicted k-th smallest hash
     int64_t first_min = 4096;     // logs at least this long replay through first-occurrence flags
     bool sched_on = true;
@@ -660,13 +985,77 @@ hipError_t read_ctl(WideDistinct* d, hipStream_t st) {
     return e;
 }
 
-// set ∪ candidates [0, c) -> bottom-k by (h, key words), distinct by (h, key); `tied` from this merge
-hipError_t merge_cands(WideDistinct* d, int64_t c, hipStream_t st) {
+// the bucket area for B buckets (the counters zeroed: every merge leaves the ones it used zero)
+hipError_t ensure_buckets(WideDistinct* d, uint32_t B, hipStream_t st) {
+    if (B <= d->wb_cap) return hipSuccess;
+    const size_t c = std::max<uint32_t>(B, 64);
+    hipError_t e;
+    if ((e = wgrow((void**)&d->wb_h, 0, c * kWCap * 8, false, st))) return e;
+    if ((e = wgrow((void**)&d->wb_e, 0, c * kWCap * 4, false, st))) return e;
+    if ((e = wgrow((void**)&d->wb_a, 0, c * kWCap * 8, false, st))) return e;
+    if ((e = wgrow((void**)&d->wb_dist, 0, c * 4, false, st))) return e;
+    if ((e = wgrow((void**)&d->wb_gsum, 0, (c / 16 + 1) * 4, false, st))) return e;
+    if ((e = wgrow((void**)&d->wb_cnt, 0, c * kWStride * 4, false, st))) return e;
+    if ((e = hipMemsetAsync(d->wb_cnt, 0, c * kWStride * 4, st))) return e;
+    d->wb_cap = (uint32_t)c;
+    return hipSuccess;
+}
+
+// The bucketed merge (wb_scatter -> wb_sort -> wb_emit) of set ∪ candidates [0, c); span_hi bounds
+// every entry's h.  *done = false when a bucket or a run of equal h overflowed (a degenerate hash):
+// the sort-based merge then runs instead (the counters are zero again, the set untouched).
+hipError_t merge_bucketed(WideDistinct* d, int64_t c, int64_t span_hi, bool arrivals, hipStream_t st, bool* done) {
+    *done = false;
+    const int64_t N = d->m + c;
+    uint32_t lb = 0;
+    while (((int64_t)1 << (lb + kWAvgLog)) < N && lb < 24) ++lb;
+    const uint32_t B = 1u << lb;
+    hipError_t e;
+    if ((e = ensure_buckets(d, B, st))) return e;
+    int64_t hi = span_hi;
+    if (d->m > 0 && d->top > hi) hi = d->top;
+    const uint64_t span = (uint64_t)hi - (uint64_t)INT64_MIN;
+    const uint64_t q = span == ~0ull ? 1ull : ~0ull / (span + 1);
+    const WRows R{d->set_k, d->cand_k, d->m, d->words};
+    if ((e = hipMemsetAsync(d->ctl, 0, 8 * 8, st))) return e;
+    hipLaunchKernelGGL(wb_scatter, dim3(wgrid(N, 8192)), dim3(kWBlock), 0, st, d->set_h, d->m, d->cand_h, c, q, lb,
+                       d->wb_h, d->wb_e, d->wb_cnt, d->wb_gsum, d->ctl);
+    hipLaunchKernelGGL(wb_sort, dim3((B + kWBlock / 64 - 1) / (kWBlock / 64)), dim3(kWBlock), 0, st, d->m, lb, d->wb_h,
+                       d->wb_e, arrivals ? d->wb_a : nullptr, d->wb_cnt, d->wb_dist, d->wb_gsum, R, d->cand_i, d->ctl);
+    hipLaunchKernelGGL(wb_emit, dim3((B + kWEmitBuckets - 1) / kWEmitBuckets), dim3(kWBlock), 0, st, lb, d->wb_h,
+                       d->wb_e, d->wb_dist, d->wb_gsum, (int64_t)d->k, R, d->set_h2, d->set_k2, d->ctl);
+    if ((e = hipGetLastError())) return e;
+    if ((e = read_ctl(d, st))) return e;
+    if (d->hctl[1]) return hipSuccess;
+    d->m = std::min<int64_t>(d->hctl[2], d->k);
+    d->top = d->hctl[3];
+    d->tied = d->m == d->k && d->hctl[4] != 0;
+    std::swap(d->set_h, d->set_h2);
+    std::swap(d->set_k, d->set_k2);
+    d->last_bucketed = true;
+    d->last_lb = lb;
+    ++d->merges;
+    *done = true;
+    return hipSuccess;
+}
+
+// set ∪ candidates [0, c) -> bottom-k by (h, key words), distinct by (h, key); `tied` from this merge.
+// span_hi: no candidate's h exceeds it (the filter's bound); arrivals: keep each element's first
+// arrival for the scheduled pass's proof
+hipError_t merge_cands(WideDistinct* d, int64_t c, hipStream_t st, int64_t span_hi = INT64_MAX,
+                       bool arrivals = false) {
     if (c <= 0) return hipSuccess;
     const int64_t N = d->m + c;
     hipError_t e;
-    if ((e = ensure_merge(d, N, st))) return e;
     if ((e = ensure_set(d, std::min<int64_t>(N, d->k), st))) return e;
+    d->last_bucketed = false;
+    if (d->bucketed_on && N < ((int64_t)1 << 30)) {
+        bool done = false;
+        if ((e = merge_bucketed(d, c, span_hi, arrivals, st, &done))) return e;
+        if (done) return hipSuccess;
+    }
+    // the sort-based merge: a 64-bit radix sort by h, runs of equal h by the key words
+    if ((e = ensure_merge(d, N, st))) return e;
     const WRows R{d->set_k, d->cand_k, d->m, d->words};
     const unsigned g = wgrid(N, 4096);
     hipLaunchKernelGGL(wide_merge_init, dim3(g), dim3(kWBlock), 0, st, d->set_h, d->cand_h, d->m, N, d->eh0, d->ev0);
@@ -704,6 +1093,7 @@ hipError_t merge_cands(WideDistinct* d, int64_t c, hipStream_t st) {
     d->tied = d->m == d->k && d->hctl[4] != 0;
     std::swap(d->set_h, d->set_h2);
     std::swap(d->set_k, d->set_k2);
+    ++d->merges;
     return hipSuccess;
 }
 
@@ -856,10 +1246,23 @@ hipError_t ensure_log(WideDistinct* d, int64_t need, hipStream_t st) {
     if (need <= d->log_cap) return hipSuccess;
     const int64_t c = wgrown(d->log_cap, need);
     const size_t W = (size_t)d->words * 8;
-    hipError_t e;
-    if ((e = wgrow((void**)&d->log_h, (size_t)d->log_n * 8, (size_t)c * 8, true, st))) return e;
-    if ((e = wgrow((void**)&d->log_g, (size_t)d->log_n * 8, (size_t)c * 8, true, st))) return e;
-    if ((e = wgrow((void**)&d->log_k, (size_t)d->log_n * W, (size_t)c * W, true, st))) return e;
+    void* nb[3] = {nullptr, nullptr, nullptr};
+    const size_t bytes[3] = {(size_t)c * 8, (size_t)c * 8, (size_t)c * W};
+    const size_t used[3] = {(size_t)d->log_n * 8, (size_t)d->log_n * 8, (size_t)d->log_n * W};
+    void** old[3] = {(void**)&d->log_h, (void**)&d->log_g, (void**)&d->log_k};
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 3 && e == hipSuccess; ++i) e = walloc(&nb[i], bytes[i]);
+    for (int i = 0; i < 3 && e == hipSuccess; ++i)
+        if (*old[i] && used[i]) e = hipMemcpyAsync(nb[i], *old[i], used[i], hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess && (d->log_h || d->log_g || d->log_k)) e = hipStreamSynchronize(st);  // one wait, three copies
+    if (e != hipSuccess) {
+        for (void* p : nb) pool_device_free(p);
+        return e;
+    }
+    for (int i = 0; i < 3; ++i) {
+        pool_device_free(*old[i]);
+        *old[i] = nb[i];
+    }
     d->log_cap = c;
     return hipSuccess;
 }
@@ -922,7 +1325,10 @@ hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes
         if ((e = hipGetLastError())) return e;
         d->log_n += c;
     }
-    if ((e = merge_cands(d, c, st))) return e;
+    // no candidate's h exceeds the filter's bound (hash_all: any h)
+    const int64_t span_hi = (d->m < d->k && !bound_in) ? INT64_MAX : (bound_in ? *bound_in : d->top);
+    const int64_t hi = R > 0 ? d->hsched[R + 1] : span_hi;  // the scheduled pass: range 0's bound is the largest
+    if ((e = merge_cands(d, c, st, std::max(hi, span_hi), d->ordered))) return e;
     if (d->ordered) d->exact = !d->tied;  // an uncut boundary bucket leaves one possible set
     return hipSuccess;
 }
@@ -942,11 +1348,6 @@ hipError_t sample_sched(WideDistinct* d, const void* keys, const int64_t* hashes
     if (!d->sched) {
         if ((e = walloc((void**)&d->sched, kSchedWords * 8))) return e;
         if ((e = pool_host_alloc((void**)&d->hsched, kSchedWords * 8, hipHostMallocDefault))) return e;
-    }
-    if (d->bk_cap < d->k) {
-        if ((e = wgrow((void**)&d->bk_h, 0, (size_t)d->k * 8, false, st))) return e;
-        if ((e = wgrow((void**)&d->bk_k, 0, (size_t)d->k * d->words * 8, false, st))) return e;
-        d->bk_cap = d->k;
     }
     // a bounded log is replayed first (as sample_chunk would), so the state saved below is the one
     // the pass starts from
@@ -977,21 +1378,31 @@ hipError_t sample_sched(WideDistinct* d, const void* keys, const int64_t* hashes
     // a set whose maximum sits high in the hash range (few distinct keys beyond k) would make most of
     // the rest candidates: the chunk loop bounds each chunk's instead
     if (expect > 32.0 * (double)d->k + (double)(1 << 22)) return hipSuccess;
-    if ((e = ensure_cand(d, (int64_t)(1.25 * expect) + 65536, st))) return e;
+    const int64_t room = (int64_t)(1.25 * expect) + 65536;
+    if ((e = ensure_cand(d, room, st))) return e;
+    if (d->ordered && (e = ensure_log(d, d->log_n + room, st))) return e;  // no log growth after the filter
     if ((e = hipMemcpyAsync(d->sched, rs, (size_t)(2 * R + 1) * 8, hipMemcpyHostToDevice, st))) return e;
     if ((e = hipMemsetAsync(d->sched + kSchedCounts, 0, (kWMaxR + 1) * 8, st))) return e;
-    // the set and the scalars before the pass
-    const int64_t m0 = d->m, top0 = d->top, log0 = d->log_n;
+    // the set and the scalars before the pass: the pass's one merge writes the other set buffers, so
+    // a failed proof swaps back instead of restoring a copy
+    const int64_t m0 = d->m, top0 = d->top, log0 = d->log_n, merges0 = d->merges;
     const bool tied0 = d->tied, exact0 = d->exact;
-    if ((e = hipMemcpyAsync(d->bk_h, d->set_h, (size_t)m0 * 8, hipMemcpyDeviceToDevice, st))) return e;
-    if ((e = hipMemcpyAsync(d->bk_k, d->set_k, (size_t)m0 * d->words * 8, hipMemcpyDeviceToDevice, st))) return e;
     int64_t c = 0;
     if ((e = sample_chunk(d, keys, hashes, off, rest, gbase, st, nullptr, R, &c))) return e;
+    if (d->merges - merges0 > 1) {  // (sample_chunk's bounded-log replay cannot run here: sample_sched ran it)
+        set_error("wide scheduled pass: more than one merge");
+        return hipErrorUnknown;
+    }
     bool good = false;
-    if (c > 0 && d->m == d->k) {  // the merge's sorted entries are still in eh1 / ev1 / flags
+    if (c > 0 && d->m == d->k) {  // the merge's sorted entries: the bucket area, or eh1 / ev1 / flags
         const int64_t N = m0 + c;
-        hipLaunchKernelGGL(wide_verify, dim3(wgrid(N, 4096)), dim3(kWBlock), 0, st, d->eh1, d->ev1, d->flags, N, m0,
-                           d->cand_i, d->sched, R, (unsigned long long*)(d->sched + kSchedCounts));
+        if (d->last_bucketed)
+            hipLaunchKernelGGL(wb_verify, dim3(std::min<uint32_t>(((1u << d->last_lb) + 3) / 4, 4096)), dim3(kWBlock), 0,
+                               st, d->last_lb, d->wb_h, d->wb_a, d->wb_dist, d->sched, R,
+                               (unsigned long long*)(d->sched + kSchedCounts));
+        else
+            hipLaunchKernelGGL(wide_verify, dim3(wgrid(N, 4096)), dim3(kWBlock), 0, st, d->eh1, d->ev1, d->flags, N, m0,
+                               d->cand_i, d->sched, R, (unsigned long long*)(d->sched + kSchedCounts));
         if ((e = hipGetLastError())) return e;
         if ((e = hipMemcpyAsync(d->hsched + kSchedCounts, d->sched + kSchedCounts, (size_t)(R + 1) * 8, hipMemcpyDeviceToHost, st)))
             return e;
@@ -1011,9 +1422,12 @@ hipError_t sample_sched(WideDistinct* d, const void* keys, const int64_t* hashes
         *ok = true;
         return hipSuccess;
     }
-    // the proof failed: the set and the log as before the pass
-    if ((e = hipMemcpyAsync(d->set_h, d->bk_h, (size_t)m0 * 8, hipMemcpyDeviceToDevice, st))) return e;
-    if ((e = hipMemcpyAsync(d->set_k, d->bk_k, (size_t)m0 * d->words * 8, hipMemcpyDeviceToDevice, st))) return e;
+    // the proof failed: the set (the merge's input, intact in the other buffers) and the log as before
+    if (d->merges != merges0) {
+        std::swap(d->set_h, d->set_h2);
+        std::swap(d->set_k, d->set_k2);
+        d->merges = merges0;
+    }
     d->m = m0;
     d->top = top0;
     d->tied = tied0;
@@ -1094,7 +1508,9 @@ WideDistinct* wide_create(int32_t k, int key_width, int src, int64_t r0, int64_t
         d->sched_beta = std::atof(v);
     if (const char* v = std::getenv("RSV_FIRST_MIN"))  // test hook: which replay form serves a log
         d->first_min = std::max<int64_t>(0, std::atoll(v));
+    if (const char* v = std::getenv("RSV_WIDE_BUCKETED")) d->bucketed_on = std::atoi(v) != 0;  // A/B hook
     hipError_t e = walloc((void**)&d->ctl, 8 * 8);
+    if (e == hipSuccess) e = hipMemset(d->ctl, 0, 8 * 8);  // ctl[7]: the publication ticket
     if (e == hipSuccess) e = pool_host_alloc((void**)&d->hctl, 8 * 8, hipHostMallocDefault);
     if (e != hipSuccess) {
         *status = fail_hip(e, "distinct_create (wide keys)");
@@ -1111,8 +1527,8 @@ void wide_destroy(WideDistinct* d) {
                   d->ev0, d->ev1, d->flags, d->pos, d->temp, d->ctl, d->log_h, d->log_g, d->log_k};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
     pool_device_free(d->sched);
-    pool_device_free(d->bk_h);
-    pool_device_free(d->bk_k);
+    void* wb[] = {d->wb_h, d->wb_e, d->wb_a, d->wb_cnt, d->wb_dist, d->wb_gsum};
+    for (void* p : wb) pool_device_free(p);
     pool_host_free(d->hsched);
     pool_host_free(d->hctl);
     delete d;
@@ -1200,7 +1616,13 @@ int wide_finalize(WideDistinct* d, hipStream_t st) {
 }
 
 int wide_publish(WideDistinct* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st) {
-    RSV_HIP_TRY(launch_publish(d->set_k, d->m * d->words * 8, dst_host_dev, flag_dev, gen, st));
+    const int64_t bytes = d->m * d->words * 8;
+    // one workgroup's posted PCIe writes run at ~20 GB/s (a 1 MB UUID set: 45 us): large sets from
+    // several workgroups (ctl[7] is the ticket: zero at creation, re-armed by every publication)
+    if (bytes >= (64 << 10))
+        RSV_HIP_TRY(launch_publish_multi(d->set_k, bytes, dst_host_dev, flag_dev, gen, (uint32_t*)(d->ctl + 7), st));
+    else
+        RSV_HIP_TRY(launch_publish(d->set_k, bytes, dst_host_dev, flag_dev, gen, st));
     return RSV_OK;
 }
 

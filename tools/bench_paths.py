@@ -440,6 +440,10 @@ def main():
         for mode in ("set", "uuid", "twins"):
             print(json.dumps(c4_wide(dev, mode)), flush=True)
             torch.cuda.empty_cache()
+    if "c4ws" in todo:  # UUID keys, set mode only (for traces)
+        print(json.dumps(c4_wide(dev, "set")), flush=True)
+    if "c4wu" in todo:  # UUID keys, UUID.hashCode ordered mode only (for traces)
+        print(json.dumps(c4_wide(dev, "uuid")), flush=True)
     if "c4m" in todo:
         for r in c4_merge(dev):
             print(json.dumps(r), flush=True)

@@ -8,6 +8,7 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <algorithm>
 #include <vector>
 
 __device__ unsigned long long g_dbg[8];
@@ -107,6 +108,25 @@ __global__ __launch_bounds__(256) void k1_qp(DrawKey dk, uint32_t k, uint64_t lo
     const int w = threadIdx.x >> 6;
     (void)TRIM;
     k1_body_q<W, FAST>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], W1, A, B);
+}
+
+// the product body over its plan with each wave's shader clock stamped at entry and exit (a separate
+// diagnostic kernel, MI355X_MICROARCH.md DVFS item 6: in the product no stamp executes): per wave
+// dt = s_memtime ticks (shader cycles), dr = s_memrealtime ticks (100 MHz) -> the in-kernel clock
+template <int W, bool FAST>
+__global__ __launch_bounds__(256) void k1_qclk(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                               uint64_t n_groups, unsigned long long* __restrict__ win, uint32_t W1,
+                                               uint32_t A, uint32_t B, unsigned long long* __restrict__ stamps) {
+    __shared__ K1QLds<W> L;
+    const int w = threadIdx.x >> 6;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    k1_body_q<W, FAST>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], W1, A, B);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if ((threadIdx.x & 63) == 0) {  // vector stores
+        stamps[2 * wave] = t1 - t0;
+        stamps[2 * wave + 1] = r1 - r0;
+    }
 }
 
 // a stand-in for a collective running beside K1 (RCCL's all-gather kernel: a few workgroups for tens
@@ -259,6 +279,41 @@ int main(int argc, char** argv) {
                     printf("{\"occupier_blocks\": %d, \"layout\": \"%s\", \"us\": %.2f}\n", occ,
                            v ? "plan" : "grid_stride", tot / reps * 1e3);
                 }
+        }
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'k') {  // K1's in-kernel clock (stamped diagnostic kernel, see k1_qclk)
+        const uint32_t W1 = 6144, A = 10, B = 2;
+        const uint64_t units = (n_groups + 767) / 768, waves = W1 + (units - (uint64_t)W1 * A + 1) / 2;
+        const int pgrid = (int)((waves + 3) / 4);
+        unsigned long long* stamps;
+        CK(hipMalloc(&stamps, (size_t)pgrid * 4 * 16));
+        // >= 2 s of back-to-back launches first (the clock settles under load)
+        for (int rep = 0; rep < 25000; ++rep)
+            hipLaunchKernelGGL((k1_qp<12, true, false>), dim3(pgrid), dim3(256), 0, 0, dk, k, lo, n, 0ull, n_groups, win,
+                               W1, A, B);
+        CK(hipDeviceSynchronize());
+        for (int p = 0; p < 5; ++p) {
+            const int reps = 20;
+            CK(hipEventRecord(e0));
+            for (int rep = 0; rep < reps; ++rep)
+                hipLaunchKernelGGL((k1_qp<12, true, false>), dim3(pgrid), dim3(256), 0, 0, dk, k, lo, n, 0ull, n_groups,
+                                   win, W1, A, B);
+            CK(hipEventRecord(e1));
+            hipLaunchKernelGGL((k1_qclk<12, true>), dim3(pgrid), dim3(256), 0, 0, dk, k, lo, n, 0ull, n_groups, win, W1, A,
+                               B, stamps);
+            CK(hipDeviceSynchronize());
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            std::vector<unsigned long long> st((size_t)pgrid * 4 * 2);
+            CK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
+            std::vector<double> clk;
+            for (size_t w = 0; w < st.size() / 2; ++w)
+                if (st[2 * w + 1] >= 100) clk.push_back((double)st[2 * w] / (double)st[2 * w + 1] * 0.1);  // GHz
+            std::sort(clk.begin(), clk.end());
+            printf("{\"mode\": \"k1_in_kernel_clock\", \"launch_us\": %.2f, \"waves\": %zu, \"clock_GHz_median\": %.3f, "
+                   "\"clock_GHz_p10\": %.3f, \"clock_GHz_p90\": %.3f}\n", ms / reps * 1e3, clk.size(),
+                   clk[clk.size() / 2], clk[clk.size() / 10], clk[clk.size() * 9 / 10]);
         }
         return 0;
     }
