@@ -4,9 +4,9 @@ A step is one full pass of the hot path over the batch: a fresh Sampler (Sampler
 and closed inside the step) samples the device-resident keys (K1 last-writer kernel + resolve),
 then result() brings the k-slot reservoir to the host.  Two steps are in flight (step t+1's
 sampling is queued on the stream before step t's result is read, so the host turnaround overlaps
-the GPU), and each step's one-workgroup slot resolve + publication runs on a second stream after
-its K1 (rsv_set_resolve_stream), so step t+1's K1 does not queue behind it; the one-at-a-time figure
-is reported beside it ("serial"; --serial times that instead).  With N GPUs the stream is N x 1e9 elements
+the GPU); the one-at-a-time figure is reported beside it ("serial"; --serial times that instead).
+(RSV_BENCH_RESOLVE_STREAM=1 moves each step's one-workgroup slot resolve + publication to a second
+stream after its K1, rsv_set_resolve_stream: measured slower, off by default.)  With N GPUs the stream is N x 1e9 elements
 split by index range (each rank seeks to its offset, weak scaling) and the per-rank reservoirs are
 combined with one all_gather + merge kernel inside the step.
 
@@ -355,9 +355,10 @@ def main() -> None:
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--seed", type=int, default=0xC0FFEE)
     ap.add_argument("--stream-id", type=int, default=0x5A5A)
-    ap.add_argument("--time-every", type=int, default=6,
-                    help="HIP events around every N-th K1 launch of the timed steps (1 = every launch); "
-                         "each timed launch carries ~10 us of marker packets and host calls")
+    ap.add_argument("--time-every", type=int, default=2,
+                    help="HIP events around every N-th K1 launch of the timed steps (1 = every launch): "
+                         "every 2nd times 10 launches of the driver's 20-step form; against every 6th (3 "
+                         "launches) the headline moved < 0.5 %% (profiles/r06/bench_time_every_ab.jsonl)")
     ap.add_argument("--serial", action="store_true",
                     help="one step at a time (no second sampler in flight) for the timed steps")
     ap.add_argument("--depth", type=int, default=int(os.environ.get("RSV_BENCH_DEPTH", "2")),
@@ -490,7 +491,7 @@ def main() -> None:
     torch.cuda.synchronize()
     # K1 timing: HIP events around every N-th K1 launch of the timed steps (process-wide list,
     # drained after the timed region; rsv_profile_global in include/reservoir_hip.h).  Each event
-    # pair adds ~5 us of marker packets to its step, so by default one step in six carries them.
+    # pair adds marker packets to its step; every 2nd step carries them (the 20-step form: 10 launches).
     # (the library times the (every/2)-th launch first: a region's first launch finds the GPU idle
     # and its event pair would include the host's submission latency)
     _native.check(L.rsv_profile_global(max(1, min(args.time_every, args.steps // 2))))
