@@ -2036,7 +2036,7 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
         d->k = k;
         d->kw = key_width;
         d->hash_kind = hash_kind;
-        d->spec_min = INT64_MAX;  // no speculative publication
+        // set mode's one-pass batches publish speculatively (rsv_wide.hip wide_spec_target)
         d->wide = wide_create(k, key_width, hash_kind == kHashUuid ? kWideSrcUuid : kWideSrcHashes, r0, r1, ordered,
                               status);
         if (!d->wide) {
@@ -2136,7 +2136,11 @@ const void* distinct_keys_dev(const DistinctState* d) { return d->wide ? wide_ke
 
 void distinct_spec_target(DistinctState* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t* gen_counter) {
     // the bucketed merge only: set mode behind ctl_publish, ordered mode behind the scheduled pass
-    if (d->log_bmax < 0 || d->wide) return;
+    if (d->wide) {
+        wide_spec_target(d->wide, dst_host_dev, flag_dev, gen_counter);
+        return;
+    }
+    if (d->log_bmax < 0) return;
     d->spec_dst = dst_host_dev;
     d->spec_flag = flag_dev;
     d->spec_gen_ctr = gen_counter;
@@ -2147,6 +2151,7 @@ bool distinct_is_ordered(const DistinctState* d) { return d->ordered; }
 int64_t distinct_spec_min(const DistinctState* d) { return d->spec_min; }
 
 bool distinct_spec_take(DistinctState* d, uint32_t* gen) {
+    if (d->wide) return wide_spec_take(d->wide, gen);
     const bool ok = d->spec_ok && d->spec_dst;
     if (ok) *gen = d->spec_gen;
     d->spec_dst = nullptr;

@@ -219,6 +219,10 @@ int wide_merge_parts(WideDistinct* d, const void* keys_dev, const int64_t* hash_
 int wide_export_row(WideDistinct* d, int64_t* row, int64_t count, hipStream_t st);
 int wide_merge_rows(WideDistinct* d, const int64_t* rows, int32_t parts, int64_t stride, hipStream_t st);
 void wide_retain_log(WideDistinct* d, bool on);
+// set mode's one-pass batches: the merged set published into dst_host_dev + flag_dev (generation
+// ++*gen_counter) right behind the merge; wide_spec_take says whether it holds the batch's final set
+void wide_spec_target(WideDistinct* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t* gen_counter);
+bool wide_spec_take(WideDistinct* d, uint32_t* gen);
 int wide_log_export(WideDistinct* d, int64_t bound, int64_t* out_h, void* out_k, int64_t cap, int64_t* out_n,
                     hipStream_t st);
 int wide_log_merge(WideDistinct* d, const int64_t* h, const void* keys, int64_t n, int64_t seen, hipStream_t st);

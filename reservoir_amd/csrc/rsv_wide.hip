@@ -528,30 +528,50 @@ constexpr uint32_t kWAvgLog = 6;
 constexpr uint32_t kWStride = 32;
 constexpr uint32_t kWEmitBuckets = 16;
 
-// bucket of u = h - INT64_MIN in [0, span]: floor(u B / (span + 1)) as umulhi(u, q B), q =
-// floor((2^64 - 1) / (span + 1)) from the host; a span below B buckets u directly
-struct WBucketMap {
-    uint64_t mult;
-    uint32_t last;
-    __device__ __forceinline__ WBucketMap(uint64_t q, uint32_t lb) {
-        last = lb ? (1u << lb) - 1u : 0u;
-        mult = lb == 0 ? 0ull : ((q >> (64 - lb)) ? 0ull : q << lb);
-    }
+// The bucket map: a piecewise-linear, monotone map of h onto B buckets.  Segment s covers h in
+// [lo_s, lo_(s+1)) (lo_0 = INT64_MIN) and owns buckets [b0_s, b0_s + nb_s), linearly:
+// floor((h - lo_s) nb_s / (span_s + 1)) = umulhi(h - lo_s, mult_s), mult_s = nb_s floor((2^64 - 1) /
+// (span_s + 1)) (0: a span below nb_s buckets directly).  The host gives each segment buckets in
+// proportion to the entries expected there, so a merge whose density varies along h (the scheduled
+// pass: every range adds candidates below its own bound, the lowest band ~2^R / (1.6 R) times the
+// mean) still fills ~64 entries a bucket.  Table (int64 words, device): lo [kWSegMax + 1] | b0
+// [kWSegMax + 1] | mult [kWSegMax] | nb [kWSegMax].
+constexpr int kWSegMax = 72;
+constexpr int kWSegWords = 4 * kWSegMax + 2;
+
+struct WSegMap {
+    const int64_t* lo;
+    const int64_t* b0;
+    const int64_t* mult;
+    const int64_t* nb;
+    int32_t ns;
     __device__ __forceinline__ uint32_t operator()(int64_t h) const {
-        const uint64_t u = (uint64_t)h ^ 0x8000000000000000ull;
-        const uint64_t b = mult ? __umul64hi(u, mult) : (last ? u : 0ull);
-        return (uint32_t)(b < last ? b : last);
+        int32_t a = 0, z = ns - 1;  // the last segment with lo <= h (lo[0] = INT64_MIN)
+        while (a < z) {
+            const int32_t mid = (a + z + 1) >> 1;
+            if (lo[mid] <= h) a = mid;
+            else z = mid - 1;
+        }
+        const uint64_t u = (uint64_t)h - (uint64_t)lo[a];
+        const uint64_t mu = (uint64_t)mult[a], n = (uint64_t)nb[a];
+        uint64_t b = mu ? __umul64hi(u, mu) : u;
+        b = b < n ? b : n - 1;
+        return (uint32_t)((uint64_t)b0[a] + b);
     }
 };
 
 __global__ __launch_bounds__(kWBlock) void wb_scatter(const int64_t* __restrict__ set_h, int64_t m,
-                                                      const int64_t* __restrict__ cand_h, int64_t c, uint64_t q,
-                                                      uint32_t lb, int64_t* __restrict__ bh, uint32_t* __restrict__ be,
+                                                      const int64_t* __restrict__ cand_h, int64_t c,
+                                                      const int64_t* __restrict__ seg, int32_t ns, uint32_t B,
+                                                      int64_t* __restrict__ bh, uint32_t* __restrict__ be,
                                                       uint32_t* __restrict__ cnt, uint32_t* __restrict__ gsum,
                                                       int64_t* __restrict__ ctl) {
+    __shared__ int64_t s_seg[kWSegWords];
+    for (int i = threadIdx.x; i < kWSegWords; i += blockDim.x) s_seg[i] = seg[i];
     if (blockIdx.x == 0)
-        for (uint32_t i = threadIdx.x; i <= ((1u << lb) >> 4); i += blockDim.x) gsum[i] = 0;
-    const WBucketMap map(q, lb);
+        for (uint32_t i = threadIdx.x; i <= (B >> 4); i += blockDim.x) gsum[i] = 0;
+    __syncthreads();
+    const WSegMap map{s_seg, s_seg + kWSegMax + 1, s_seg + 2 * kWSegMax + 2, s_seg + 3 * kWSegMax + 2, ns};
     const int64_t total = m + c, stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
         const int64_t h = e < m ? set_h[e] : cand_h[e - m];
@@ -647,7 +667,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // One wave per bucket: sort, order runs of equal h by the key words, keep the first entry of each
 // distinct (h, key) compacted at the bucket's start (with the element's first arrival when cand_i is
 // given: -1 for a set member, else the earliest batch offset among its candidate entries).
-__global__ __launch_bounds__(kWBlock) void wb_sort(int64_t m, uint32_t lb, int64_t* __restrict__ bh,
+__global__ __launch_bounds__(kWBlock) void wb_sort(int64_t m, uint32_t B, int64_t* __restrict__ bh,
                                                    uint32_t* __restrict__ be, int64_t* __restrict__ ba,
                                                    uint32_t* __restrict__ cnt, uint32_t* __restrict__ bdist,
                                                    uint32_t* __restrict__ gsum, WRows R,
@@ -656,7 +676,7 @@ __global__ __launch_bounds__(kWBlock) void wb_sort(int64_t m, uint32_t lb, int64
     __shared__ uint32_t s_e[kWBlock / 64][kWCap];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t b = blockIdx.x * (kWBlock / 64) + w;
-    if (b >= (1u << lb)) return;
+    if (b >= B) return;
     uint32_t* pc = cnt + (size_t)b * kWStride;
     const uint32_t n = *pc;
     __builtin_amdgcn_wave_barrier();
@@ -725,14 +745,13 @@ __global__ __launch_bounds__(kWBlock) void wb_sort(int64_t m, uint32_t lb, int64
 // each bucket's distinct entries to their global rank (ranks < k): the set's hashes and key rows.
 // ctl[2] = distinct count, ctl[3] = the largest kept h, ctl[4] = rank k ties rank k - 1 on h (equal h
 // share a bucket: the map is monotone)
-__global__ __launch_bounds__(kWBlock) void wb_emit(uint32_t lb, const int64_t* __restrict__ bh,
+__global__ __launch_bounds__(kWBlock) void wb_emit(uint32_t B, const int64_t* __restrict__ bh,
                                                    const uint32_t* __restrict__ be, const uint32_t* __restrict__ bdist,
                                                    const uint32_t* __restrict__ gsum, int64_t k, WRows R,
                                                    int64_t* __restrict__ out_h, uint64_t* __restrict__ out_k,
                                                    int64_t* __restrict__ ctl) {
     __shared__ uint64_t s_pre[kWBlock / 64], s_tot[kWBlock / 64];
     __shared__ uint64_t s_base[kWEmitBuckets + 1];
-    const uint32_t B = 1u << lb;
     const uint32_t b0 = blockIdx.x * kWEmitBuckets;
     if (b0 >= B) return;
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -797,7 +816,7 @@ __global__ __launch_bounds__(kWBlock) void wb_emit(uint32_t lb, const int64_t* _
 
 // the scheduled pass's proof over the bucketed merge (wide_verify's rule: each distinct element with
 // first arrival a and hash h counts for the ranges r with range(a) < r and B_r > h)
-__global__ __launch_bounds__(kWBlock) void wb_verify(uint32_t lb, const int64_t* __restrict__ bh,
+__global__ __launch_bounds__(kWBlock) void wb_verify(uint32_t B, const int64_t* __restrict__ bh,
                                                      const int64_t* __restrict__ ba, const uint32_t* __restrict__ bdist,
                                                      const int64_t* __restrict__ rtab, int32_t R,
                                                      unsigned long long* __restrict__ diff) {
@@ -806,7 +825,7 @@ __global__ __launch_bounds__(kWBlock) void wb_verify(uint32_t lb, const int64_t*
     WRanges rg{s_rs, s_rb, R};
     for (int t = threadIdx.x; t <= R; t += blockDim.x) s_d[t] = 0;
     rg.load(rtab);
-    const uint32_t B = 1u << lb, lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63;
     const uint32_t wstride = gridDim.x * (kWBlock / 64);
     for (uint32_t b = blockIdx.x * (kWBlock / 64) + (threadIdx.x >> 6); b < B; b += wstride) {
         const uint32_t cnt = bdist[b];
@@ -884,8 +903,18 @@ struct WideDistinct {
     uint32_t wb_cap = 0;
     bool bucketed_on = true;      // RSV_WIDE_BUCKETED=0: the sort-based merge only (A/B, tests)
     bool last_bucketed = false;   // the last merge's sorted entries are in the bucket area (wb_verify)
-    uint32_t last_lb = 0;
+    uint32_t last_B = 0;
+    int64_t* wb_seg = nullptr;    // the bucket map's segment table (device) and its pinned staging
+    int64_t* hwb_seg = nullptr;
     int64_t merges = 0;           // merges applied (a set swap each)
+    // speculative publication (set mode's one-pass batches, wide_spec_target): armed around the pass,
+    // enqueued behind its merge; valid when the pass proved its bound and no other merge followed
+    void* spec_dst = nullptr;
+    uint32_t* spec_flag = nullptr;
+    uint32_t* spec_gen_ctr = nullptr;
+    bool spec_arm = false, spec_ok = false;
+    uint32_t spec_gen = 0;
+    int64_t spec_merges = -1;
     double sched_beta = 1.6;      // bound margin over the predicted k-th smallest hash
     int64_t first_min = 4096;     // logs at least this long replay through first-occurrence flags
     bool sched_on = true;
@@ -1001,39 +1030,89 @@ hipError_t ensure_buckets(WideDistinct* d, uint32_t B, hipStream_t st) {
     return hipSuccess;
 }
 
+// A stretch of the hash axis with the entries expected in it: the bucket map's segments ascend
+// by `lo` (the first from INT64_MIN), each reaching the next one's lo (the last: the merge's largest h)
+struct WSeg {
+    int64_t lo;
+    double expect;
+};
+
 // The bucketed merge (wb_scatter -> wb_sort -> wb_emit) of set ∪ candidates [0, c); span_hi bounds
-// every entry's h.  *done = false when a bucket or a run of equal h overflowed (a degenerate hash):
-// the sort-based merge then runs instead (the counters are zero again, the set untouched).
-hipError_t merge_bucketed(WideDistinct* d, int64_t c, int64_t span_hi, bool arrivals, hipStream_t st, bool* done) {
+// every entry's h; `segs` (optional) describe how the entries spread along h (default: uniform).
+// *done = false when a bucket or a run of equal h overflowed (a degenerate hash): the sort-based
+// merge then runs instead (the counters are zero again, the set untouched).
+hipError_t merge_bucketed(WideDistinct* d, int64_t c, int64_t span_hi, bool arrivals,
+                          const std::vector<WSeg>* segs, hipStream_t st, bool* done) {
     *done = false;
     const int64_t N = d->m + c;
-    uint32_t lb = 0;
-    while (((int64_t)1 << (lb + kWAvgLog)) < N && lb < 24) ++lb;
-    const uint32_t B = 1u << lb;
-    hipError_t e;
-    if ((e = ensure_buckets(d, B, st))) return e;
     int64_t hi = span_hi;
     if (d->m > 0 && d->top > hi) hi = d->top;
-    const uint64_t span = (uint64_t)hi - (uint64_t)INT64_MIN;
-    const uint64_t q = span == ~0ull ? 1ull : ~0ull / (span + 1);
+    std::vector<WSeg> one{WSeg{INT64_MIN, 1.0}};
+    const std::vector<WSeg>& sg = segs && !segs->empty() && (int)segs->size() <= kWSegMax ? *segs : one;
+    const int32_t ns = (int32_t)sg.size();
+    hipError_t e;
+    if (!d->wb_seg) {
+        if ((e = walloc((void**)&d->wb_seg, kWSegWords * 8))) return e;
+        if ((e = pool_host_alloc((void**)&d->hwb_seg, kWSegWords * 8, hipHostMallocDefault))) return e;
+    }
+    // buckets: ~64 entries each overall, shared out in proportion to each segment's expected entries
+    const int64_t Bt = std::min<int64_t>(std::max<int64_t>((N + (1 << kWAvgLog) - 1) >> kWAvgLog, 1), 1 << 24);
+    double tot = 0;
+    for (const WSeg& x : sg) tot += std::max(x.expect, 0.0);
+    int64_t* lo = d->hwb_seg;
+    int64_t* b0 = lo + kWSegMax + 1;
+    int64_t* mult = lo + 2 * kWSegMax + 2;
+    int64_t* nb = lo + 3 * kWSegMax + 2;
+    double cum = 0;
+    int64_t B = 0;
+    for (int32_t i = 0; i < ns; ++i) {
+        cum += std::max(sg[i].expect, 0.0);
+        const int64_t end = tot > 0 ? (int64_t)((double)Bt * cum / tot + 0.5) : Bt * (i + 1) / ns;
+        const int64_t n = std::max<int64_t>(end - B, 1);
+        lo[i] = i == 0 ? INT64_MIN : sg[i].lo;
+        b0[i] = B;
+        nb[i] = n;
+        const int64_t seg_hi = i + 1 < ns ? sg[i + 1].lo - 1 : std::max(hi, lo[i]);
+        const uint64_t span = (uint64_t)seg_hi - (uint64_t)lo[i];
+        const uint64_t q = span == ~0ull ? 1ull : ~0ull / (span + 1);
+        mult[i] = (int64_t)(q <= ~0ull / (uint64_t)n ? q * (uint64_t)n : 0ull);
+        B += n;
+    }
+    lo[ns] = INT64_MAX;
+    b0[ns] = B;
+    if ((e = ensure_buckets(d, (uint32_t)B, st))) return e;
     const WRows R{d->set_k, d->cand_k, d->m, d->words};
+    if ((e = hipMemcpyAsync(d->wb_seg, d->hwb_seg, kWSegWords * 8, hipMemcpyHostToDevice, st))) return e;
     if ((e = hipMemsetAsync(d->ctl, 0, 8 * 8, st))) return e;
-    hipLaunchKernelGGL(wb_scatter, dim3(wgrid(N, 8192)), dim3(kWBlock), 0, st, d->set_h, d->m, d->cand_h, c, q, lb,
-                       d->wb_h, d->wb_e, d->wb_cnt, d->wb_gsum, d->ctl);
-    hipLaunchKernelGGL(wb_sort, dim3((B + kWBlock / 64 - 1) / (kWBlock / 64)), dim3(kWBlock), 0, st, d->m, lb, d->wb_h,
-                       d->wb_e, arrivals ? d->wb_a : nullptr, d->wb_cnt, d->wb_dist, d->wb_gsum, R, d->cand_i, d->ctl);
-    hipLaunchKernelGGL(wb_emit, dim3((B + kWEmitBuckets - 1) / kWEmitBuckets), dim3(kWBlock), 0, st, lb, d->wb_h,
-                       d->wb_e, d->wb_dist, d->wb_gsum, (int64_t)d->k, R, d->set_h2, d->set_k2, d->ctl);
+    hipLaunchKernelGGL(wb_scatter, dim3(wgrid(N, 8192)), dim3(kWBlock), 0, st, d->set_h, d->m, d->cand_h, c, d->wb_seg,
+                       ns, (uint32_t)B, d->wb_h, d->wb_e, d->wb_cnt, d->wb_gsum, d->ctl);
+    hipLaunchKernelGGL(wb_sort, dim3((unsigned)((B + kWBlock / 64 - 1) / (kWBlock / 64))), dim3(kWBlock), 0, st, d->m,
+                       (uint32_t)B, d->wb_h, d->wb_e, arrivals ? d->wb_a : nullptr, d->wb_cnt, d->wb_dist, d->wb_gsum, R,
+                       d->cand_i, d->ctl);
+    hipLaunchKernelGGL(wb_emit, dim3((unsigned)((B + kWEmitBuckets - 1) / kWEmitBuckets)), dim3(kWBlock), 0, st,
+                       (uint32_t)B, d->wb_h, d->wb_e, d->wb_dist, d->wb_gsum, (int64_t)d->k, R, d->set_h2, d->set_k2,
+                       d->ctl);
     if ((e = hipGetLastError())) return e;
-    if ((e = read_ctl(d, st))) return e;
-    if (d->hctl[1]) return hipSuccess;
+    if (d->spec_arm && d->spec_dst) {  // the merged set straight to the host, before the host reads ctl
+        const uint32_t gen = ++*d->spec_gen_ctr;
+        if ((e = launch_publish_multi(d->set_k2, (int64_t)d->k * d->words * 8, d->spec_dst, d->spec_flag, gen,
+                                      (uint32_t*)(d->ctl + 7), st)))
+            return e;
+        d->spec_gen = gen;
+        d->spec_merges = d->merges + 1;
+    }
+    if ((e = read_ctl(d, st))) return e;  // (the pinned segment table is free again after this wait)
+    if (d->hctl[1]) {
+        d->spec_merges = -1;  // what was published is not a merge result
+        return hipSuccess;
+    }
     d->m = std::min<int64_t>(d->hctl[2], d->k);
     d->top = d->hctl[3];
     d->tied = d->m == d->k && d->hctl[4] != 0;
     std::swap(d->set_h, d->set_h2);
     std::swap(d->set_k, d->set_k2);
     d->last_bucketed = true;
-    d->last_lb = lb;
+    d->last_B = (uint32_t)B;
     ++d->merges;
     *done = true;
     return hipSuccess;
@@ -1043,7 +1122,7 @@ hipError_t merge_bucketed(WideDistinct* d, int64_t c, int64_t span_hi, bool arri
 // span_hi: no candidate's h exceeds it (the filter's bound); arrivals: keep each element's first
 // arrival for the scheduled pass's proof
 hipError_t merge_cands(WideDistinct* d, int64_t c, hipStream_t st, int64_t span_hi = INT64_MAX,
-                       bool arrivals = false) {
+                       bool arrivals = false, const std::vector<WSeg>* segs = nullptr) {
     if (c <= 0) return hipSuccess;
     const int64_t N = d->m + c;
     hipError_t e;
@@ -1051,7 +1130,7 @@ hipError_t merge_cands(WideDistinct* d, int64_t c, hipStream_t st, int64_t span_
     d->last_bucketed = false;
     if (d->bucketed_on && N < ((int64_t)1 << 30)) {
         bool done = false;
-        if ((e = merge_bucketed(d, c, span_hi, arrivals, st, &done))) return e;
+        if ((e = merge_bucketed(d, c, span_hi, arrivals, segs, st, &done))) return e;
         if (done) return hipSuccess;
     }
     // the sort-based merge: a 64-bit radix sort by h, runs of equal h by the key words
@@ -1271,7 +1350,7 @@ hipError_t ensure_log(WideDistinct* d, int64_t need, hipStream_t st) {
 // rows, log, merge
 hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes, int64_t off, int64_t L,
                         int64_t gbase, hipStream_t st, const int64_t* bound_in = nullptr, int32_t R = 0,
-                        int64_t* c_out = nullptr) {
+                        int64_t* c_out = nullptr, const std::vector<WSeg>* segs = nullptr) {
     const uint64_t* rows = (const uint64_t*)keys + (size_t)off * d->words;
     const int64_t* hv = hashes ? hashes + off : nullptr;
     hipError_t e;
@@ -1328,7 +1407,7 @@ hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes
     // no candidate's h exceeds the filter's bound (hash_all: any h)
     const int64_t span_hi = (d->m < d->k && !bound_in) ? INT64_MAX : (bound_in ? *bound_in : d->top);
     const int64_t hi = R > 0 ? d->hsched[R + 1] : span_hi;  // the scheduled pass: range 0's bound is the largest
-    if ((e = merge_cands(d, c, st, std::max(hi, span_hi), d->ordered))) return e;
+    if ((e = merge_cands(d, c, st, std::max(hi, span_hi), d->ordered, segs))) return e;
     if (d->ordered) d->exact = !d->tied;  // an uncut boundary bucket leaves one possible set
     return hipSuccess;
 }
@@ -1387,8 +1466,28 @@ hipError_t sample_sched(WideDistinct* d, const void* keys, const int64_t* hashes
     // a failed proof swaps back instead of restoring a copy
     const int64_t m0 = d->m, top0 = d->top, log0 = d->log_n, merges0 = d->merges;
     const bool tied0 = d->tied, exact0 = d->exact;
+    // how the pass's merge entries spread along h (the bucket map, merge_bucketed): range r adds its
+    // candidates uniformly below its bound B_r, so band (B_(j+1), B_j] holds ranges 0..j's; the set's
+    // members spread uniformly below its maximum
+    std::vector<WSeg> segs;
+    {
+        const double two64 = 18446744073709551616.0;
+        const double tspan = (double)((uint64_t)d->top - (uint64_t)INT64_MIN) + 1.0;
+        auto width = [](int64_t a, int64_t b) { return (double)((uint64_t)b - (uint64_t)a); };
+        double lens = 0;  // ranges 0..R-1: all of them contribute to the lowest band
+        for (int32_t r = 0; r < R; ++r) lens += (double)(rs[r + 1] - rs[r]);
+        const double w0 = width(INT64_MIN, rb[R - 1]) + 1.0;
+        segs.push_back(WSeg{INT64_MIN, lens * w0 / two64 + (double)d->m * w0 / tspan});
+        for (int32_t j = R - 2; j >= 0; --j) {
+            if (rb[j] <= rb[j + 1]) continue;  // an empty band (equal bounds)
+            double lj = 0;
+            for (int32_t r = 0; r <= j; ++r) lj += (double)(rs[r + 1] - rs[r]);
+            const double wj = width(rb[j + 1], rb[j]);
+            segs.push_back(WSeg{rb[j + 1] + 1, lj * wj / two64 + (double)d->m * wj / tspan});
+        }
+    }
     int64_t c = 0;
-    if ((e = sample_chunk(d, keys, hashes, off, rest, gbase, st, nullptr, R, &c))) return e;
+    if ((e = sample_chunk(d, keys, hashes, off, rest, gbase, st, nullptr, R, &c, &segs))) return e;
     if (d->merges - merges0 > 1) {  // (sample_chunk's bounded-log replay cannot run here: sample_sched ran it)
         set_error("wide scheduled pass: more than one merge");
         return hipErrorUnknown;
@@ -1397,8 +1496,8 @@ hipError_t sample_sched(WideDistinct* d, const void* keys, const int64_t* hashes
     if (c > 0 && d->m == d->k) {  // the merge's sorted entries: the bucket area, or eh1 / ev1 / flags
         const int64_t N = m0 + c;
         if (d->last_bucketed)
-            hipLaunchKernelGGL(wb_verify, dim3(std::min<uint32_t>(((1u << d->last_lb) + 3) / 4, 4096)), dim3(kWBlock), 0,
-                               st, d->last_lb, d->wb_h, d->wb_a, d->wb_dist, d->sched, R,
+            hipLaunchKernelGGL(wb_verify, dim3(std::min<uint32_t>((d->last_B + 3) / 4, 4096)), dim3(kWBlock), 0,
+                               st, d->last_B, d->wb_h, d->wb_a, d->wb_dist, d->sched, R,
                                (unsigned long long*)(d->sched + kSchedCounts));
         else
             hipLaunchKernelGGL(wide_verify, dim3(wgrid(N, 4096)), dim3(kWBlock), 0, st, d->eh1, d->ev1, d->flags, N, m0,
@@ -1416,8 +1515,8 @@ hipError_t sample_sched(WideDistinct* d, const void* keys, const int64_t* hashes
     }
     const bool debug = std::getenv("RSV_WIDE_SCHED_DEBUG") != nullptr;  // (read per pass: tests toggle it)
     if (debug)
-        std::fprintf(stderr, "[rsv wide sched] rest=%lld ranges=%d candidates=%lld proof=%s\n", (long long)rest, R,
-                     (long long)c, good ? "ok" : "failed");
+        std::fprintf(stderr, "[rsv wide sched] rest=%lld ranges=%d candidates=%lld proof=%s merge=%s\n", (long long)rest,
+                     R, (long long)c, good ? "ok" : "failed", d->last_bucketed ? "bucketed" : "sort");
     if (good) {
         *ok = true;
         return hipSuccess;
@@ -1527,8 +1626,9 @@ void wide_destroy(WideDistinct* d) {
                   d->ev0, d->ev1, d->flags, d->pos, d->temp, d->ctl, d->log_h, d->log_g, d->log_k};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
     pool_device_free(d->sched);
-    void* wb[] = {d->wb_h, d->wb_e, d->wb_a, d->wb_cnt, d->wb_dist, d->wb_gsum};
+    void* wb[] = {d->wb_h, d->wb_e, d->wb_a, d->wb_cnt, d->wb_dist, d->wb_gsum, d->wb_seg};
     for (void* p : wb) pool_device_free(p);
+    pool_host_free(d->hwb_seg);
     pool_host_free(d->hsched);
     pool_host_free(d->hctl);
     delete d;
@@ -1572,9 +1672,12 @@ int wide_sample_device(WideDistinct* d, const void* keys, const int64_t* hashes,
             predicted = true;
             const double frac = 2.5 * (double)d->k / (double)rest;
             const int64_t B = (int64_t)((uint64_t)INT64_MIN + (uint64_t)(18446744073709551616.0 * frac));
-            if (hipError_t e = sample_chunk(d, keys, hashes, off, rest, seen0, st, &B))
-                return fail_hip(e, "distinct sample");
+            d->spec_arm = true;
+            hipError_t e = sample_chunk(d, keys, hashes, off, rest, seen0, st, &B);
+            d->spec_arm = false;
+            if (e) return fail_hip(e, "distinct sample");
             if (d->m == d->k && d->top <= B) {
+                d->spec_ok = d->spec_dst && d->merges == d->spec_merges;  // the published set is the final one
                 d->seen += rest;
                 break;
             }
@@ -1691,6 +1794,22 @@ int wide_merge_rows(WideDistinct* d, const int64_t* rows, int32_t parts, int64_t
         ties.push_back(mt[2] != 0);
     }
     return merge_external(d, src, counts, tops, ties, st);
+}
+
+void wide_spec_target(WideDistinct* d, void* dst_host_dev, uint32_t* flag_dev, uint32_t* gen_counter) {
+    if (d->ordered) return;  // (ordered mode: the scheduled pass's result waits for its proof)
+    d->spec_dst = dst_host_dev;
+    d->spec_flag = flag_dev;
+    d->spec_gen_ctr = gen_counter;
+    d->spec_ok = false;
+}
+
+bool wide_spec_take(WideDistinct* d, uint32_t* gen) {
+    const bool ok = d->spec_ok && d->spec_dst;
+    if (ok) *gen = d->spec_gen;
+    d->spec_dst = nullptr;
+    d->spec_arm = d->spec_ok = false;
+    return ok;
 }
 
 void wide_retain_log(WideDistinct* d, bool on) {

@@ -139,16 +139,20 @@ def test_wide_distinct_uuid_default_hash(cuda, k):
 
 @pytest.mark.parametrize("k", [1, 100, 5000])
 @pytest.mark.parametrize("hkind", ["random", "collide", "uuid"])
-def test_wide_sched_pass(cuda, capfd, monkeypatch, k, hkind):
+@pytest.mark.parametrize("merge", ["bucketed", "sort"])
+def test_wide_sched_pass(cuda, capfd, monkeypatch, k, hkind, merge):
     """Ordered mode over one long batch takes the scheduled pass (falling per-range bounds, proved
-    by wide_verify): equal to the oracle, to the chunk loop (RSV_WIDE_SCHED=0), and -- with bounds
-    made too tight (RSV_WIDE_SCHED_BETA) -- the failed proof restores the set and the log and the
-    chunk loop gives the same set."""
+    by wb_verify / wide_verify): equal to the oracle, to the chunk loop (RSV_WIDE_SCHED=0), and --
+    with bounds made too tight (RSV_WIDE_SCHED_BETA) -- the failed proof restores the set and the log
+    and the chunk loop gives the same set.  Both merges: the bucketed one (round 6: its bucket map
+    follows the pass's uneven density along h) and the sort-based one (RSV_WIDE_BUCKETED=0)."""
     import torch
 
     from reservoir_amd import Sampler
 
     monkeypatch.setenv("RSV_WIDE_SCHED_DEBUG", "1")
+    if merge == "sort":
+        monkeypatch.setenv("RSV_WIDE_BUCKETED", "0")
     n = 400_000
     ids = _stream(n, 7 * k + len(hkind))
     rows = _rows(ids, 16)
@@ -176,6 +180,7 @@ def test_wide_sched_pass(cuda, capfd, monkeypatch, k, hkind):
     assert ("[rsv wide sched]" in err) == sched, err
     if sched and hkind != "collide":  # (97 hash values: no k-th smallest falls below a predicted bound)
         assert "proof=ok" in err, err
+        assert f"merge={merge}" in err, err  # no bucket overflowed: the map followed the density
     got0, err0 = run(RSV_WIDE_SCHED="0")
     assert got0 == want and "[rsv wide sched]" not in err0
     got1, err1 = run(RSV_WIDE_SCHED_BETA="0.02")
