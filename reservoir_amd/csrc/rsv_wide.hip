@@ -283,7 +283,12 @@ __global__ __launch_bounds__(kWBlock) void wide_hash_all(const int64_t* __restri
 // candidate rows: out[j] = keys[idx[j]] (one thread per 8-B word: a row's words are adjacent lanes)
 __global__ __launch_bounds__(kWBlock) void wide_gather_rows(const uint64_t* __restrict__ keys,
                                                             const int64_t* __restrict__ idx, int64_t c, int32_t words,
-                                                            uint64_t* __restrict__ out) {
+                                                            uint64_t* __restrict__ out,
+                                                            const int64_t* __restrict__ cdev = nullptr) {
+    if (cdev) {  // the count on the device (the filter's counter; above the room c: nothing to gather)
+        const int64_t cd = *cdev;
+        c = cd <= c ? cd : 0;
+    }
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t total = c * words;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
@@ -565,12 +570,20 @@ __global__ __launch_bounds__(kWBlock) void wb_scatter(const int64_t* __restrict_
                                                       const int64_t* __restrict__ seg, int32_t ns, uint32_t B,
                                                       int64_t* __restrict__ bh, uint32_t* __restrict__ be,
                                                       uint32_t* __restrict__ cnt, uint32_t* __restrict__ gsum,
-                                                      int64_t* __restrict__ ctl) {
+                                                      int64_t* __restrict__ ctl, bool c_on_device) {
     __shared__ int64_t s_seg[kWSegWords];
     for (int i = threadIdx.x; i < kWSegWords; i += blockDim.x) s_seg[i] = seg[i];
     if (blockIdx.x == 0)
         for (uint32_t i = threadIdx.x; i <= (B >> 4); i += blockDim.x) gsum[i] = 0;
     __syncthreads();
+    if (c_on_device) {  // c = the filter's counter ctl[0]; above the room c the filter dropped some:
+        const int64_t cd = ctl[0];  // nothing is merged (the host reruns the chunk with room)
+        if (cd > c) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) ctl[1] = 1;
+            return;
+        }
+        c = cd;
+    }
     const WSegMap map{s_seg, s_seg + kWSegMax + 1, s_seg + 2 * kWSegMax + 2, s_seg + 3 * kWSegMax + 2, ns};
     const int64_t total = m + c, stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
@@ -1042,7 +1055,9 @@ struct WSeg {
 // *done = false when a bucket or a run of equal h overflowed (a degenerate hash): the sort-based
 // merge then runs instead (the counters are zero again, the set untouched).
 hipError_t merge_bucketed(WideDistinct* d, int64_t c, int64_t span_hi, bool arrivals,
-                          const std::vector<WSeg>* segs, hipStream_t st, bool* done) {
+                          const std::vector<WSeg>* segs, hipStream_t st, bool* done, bool c_on_device = false) {
+    // c_on_device: c is the candidates' room, the count itself is the filter's counter ctl[0] (no host
+    // read between the filter and the merge); the caller reads ctl[0] afterwards
     *done = false;
     const int64_t N = d->m + c;
     int64_t hi = span_hi;
@@ -1083,9 +1098,10 @@ hipError_t merge_bucketed(WideDistinct* d, int64_t c, int64_t span_hi, bool arri
     if ((e = ensure_buckets(d, (uint32_t)B, st))) return e;
     const WRows R{d->set_k, d->cand_k, d->m, d->words};
     if ((e = hipMemcpyAsync(d->wb_seg, d->hwb_seg, kWSegWords * 8, hipMemcpyHostToDevice, st))) return e;
-    if ((e = hipMemsetAsync(d->ctl, 0, 8 * 8, st))) return e;
+    // ctl[1..6]; ctl[0] is the filter's count when c_on_device, ctl[7] the publication ticket (always 0)
+    if ((e = hipMemsetAsync(d->ctl + 1, 0, 6 * 8, st))) return e;
     hipLaunchKernelGGL(wb_scatter, dim3(wgrid(N, 8192)), dim3(kWBlock), 0, st, d->set_h, d->m, d->cand_h, c, d->wb_seg,
-                       ns, (uint32_t)B, d->wb_h, d->wb_e, d->wb_cnt, d->wb_gsum, d->ctl);
+                       ns, (uint32_t)B, d->wb_h, d->wb_e, d->wb_cnt, d->wb_gsum, d->ctl, c_on_device);
     hipLaunchKernelGGL(wb_sort, dim3((unsigned)((B + kWBlock / 64 - 1) / (kWBlock / 64))), dim3(kWBlock), 0, st, d->m,
                        (uint32_t)B, d->wb_h, d->wb_e, arrivals ? d->wb_a : nullptr, d->wb_cnt, d->wb_dist, d->wb_gsum, R,
                        d->cand_i, d->ctl);
@@ -1122,13 +1138,13 @@ hipError_t merge_bucketed(WideDistinct* d, int64_t c, int64_t span_hi, bool arri
 // span_hi: no candidate's h exceeds it (the filter's bound); arrivals: keep each element's first
 // arrival for the scheduled pass's proof
 hipError_t merge_cands(WideDistinct* d, int64_t c, hipStream_t st, int64_t span_hi = INT64_MAX,
-                       bool arrivals = false, const std::vector<WSeg>* segs = nullptr) {
+                       bool arrivals = false, const std::vector<WSeg>* segs = nullptr, bool sort_only = false) {
     if (c <= 0) return hipSuccess;
     const int64_t N = d->m + c;
     hipError_t e;
     if ((e = ensure_set(d, std::min<int64_t>(N, d->k), st))) return e;
     d->last_bucketed = false;
-    if (d->bucketed_on && N < ((int64_t)1 << 30)) {
+    if (d->bucketed_on && !sort_only && N < ((int64_t)1 << 30)) {
         bool done = false;
         if ((e = merge_bucketed(d, c, span_hi, arrivals, segs, st, &done))) return e;
         if (done) return hipSuccess;
@@ -1374,6 +1390,37 @@ hipError_t sample_chunk(WideDistinct* d, const void* keys, const int64_t* hashes
         const unsigned g = (unsigned)std::min<int64_t>(
             std::max<int64_t>((L / (d->src == kWideSrcHashes ? 2 * kWideU : kWideU) + kWBlock - 1) / kWBlock, 1),
             kWideGrid);
+        if (!d->ordered && d->bucketed_on && R == 0 && d->m + d->cand_cap < ((int64_t)1 << 30)) {
+            // Set mode: filter, rows and the bucketed merge enqueued together -- the candidate count
+            // stays on the device (the kernels read the filter's counter), one host read at the end
+            for (;;) {
+                if ((e = hipMemsetAsync(d->ctl, 0, 8, st))) return e;
+                if (d->timer) d->timer->mark(st);
+                if (d->src == kWideSrcHashes)
+                    hipLaunchKernelGGL(wide_filter_hashes, dim3(g), dim3(kWBlock), 0, st, hv, L, d->r0, d->r1, bound,
+                                       d->cand_h, d->cand_i, (unsigned long long*)d->ctl, d->cand_cap, d->sched, 0);
+                else
+                    hipLaunchKernelGGL(wide_filter_uuid, dim3(g), dim3(kWBlock), 0, st, rows, L, d->r0, d->r1, bound,
+                                       d->cand_h, d->cand_i, (unsigned long long*)d->ctl, d->cand_cap, d->sched, 0);
+                if (d->timer) d->timer->mark(st);
+                hipLaunchKernelGGL(wide_gather_rows, dim3(wgrid(d->cand_cap * d->words, 8192)), dim3(kWBlock), 0, st,
+                                   rows, d->cand_i, d->cand_cap, d->words, d->cand_k, (const int64_t*)d->ctl);
+                if ((e = hipGetLastError())) return e;
+                if ((e = ensure_set(d, std::min<int64_t>(d->m + d->cand_cap, d->k), st))) return e;
+                d->last_bucketed = false;
+                bool done = false;
+                if ((e = merge_bucketed(d, d->cand_cap, bound, false, nullptr, st, &done, true))) return e;
+                c = d->hctl[0];
+                if (c > d->cand_cap) {  // more candidates than room (nothing merged): again, with room
+                    if ((e = ensure_cand(d, c, st))) return e;
+                    continue;
+                }
+                if (c_out) *c_out = c;
+                // a degenerate hash overflowed a bucket: the sort-based merge of the same candidates
+                if (!done && (e = merge_cands(d, c, st, bound, false, nullptr, true))) return e;
+                return hipSuccess;
+            }
+        }
         for (;;) {
             if ((e = hipMemsetAsync(d->ctl, 0, 8, st))) return e;
             if (d->timer) d->timer->mark(st);

@@ -467,13 +467,15 @@ class GpuSampler:
             return out
         if self._h is None or not self._L.rsv_is_open(self._h):
             raise IllegalStateException("use of sampler after calling `result()`")
-        if not self._reusable and self._width <= 8:
+        if not self._reusable:
             # the published keys handed over instead of copied (rsv_result_take); the array owns the
-            # pinned buffer and releases it when the last view of it goes
+            # pinned buffer and releases it when the last view of it goes (byte keys: (n, key_width)
+            # uint8 rows over it -- a 65536-key UUID set is 1 MB, two host copies saved)
             buf, n = C.c_void_p(), C.c_int64(0)
             st = self._L.rsv_result_take(self._h, C.byref(buf), C.byref(n))
             if st == N.OK:
-                return np.asarray(_HostBuffer(self._L, buf.value or 0, n.value * self._width)).view(self._dtype)
+                raw = np.asarray(_HostBuffer(self._L, buf.value or 0, n.value * self._width))
+                return raw.reshape(-1, self._width) if self._width > 8 else raw.view(self._dtype)
             if st != N.E_UNSUPPORTED:
                 N.check(st)
         out = np.empty(self._k, dtype=self._dtype)

@@ -349,3 +349,34 @@ def test_wide_rejections(cuda):
         Sampler.distinct(10, key_type="bytes24")()
     with pytest.raises(ReservoirError):
         Sampler.distinct(10, key_type="bytes16")(hash="identity")
+
+
+@pytest.mark.parametrize("k", [1, 100, 1000])
+@pytest.mark.parametrize("nvals", [1, 3, 50])
+def test_wide_set_mode_degenerate_hash(cuda, k, nvals):
+    """Set mode with a hash of very few values (round 6): the bucketed merge's buckets overflow and the
+    sort-based merge takes over.  Set mode keeps the bottom-k by (scrambled hash, key words as
+    unsigned 64-bit, word 0 first) -- computed here from the oracle's scramble."""
+    import torch
+
+    from oracle import oracle as O
+    from reservoir_amd import Sampler
+
+    n, width = 200_000, 16
+    ids = _stream(n, 31 * k + nvals)
+    rows = _rows(ids, width)
+    hs = (np.asarray(ids, dtype=np.int64) % nvals) * 1000003 - 7
+    ref = O.Distinct(k, 21, O.HASH_IDENTITY)
+    r0, r1 = ref.r0, ref.r1
+    sh = {int(x): O.scramble(r0, r1, int(x)) for x in np.unique(hs).tolist()}
+    uniq = {}
+    for r, h in zip(rows, hs.tolist()):
+        b = bytes(r)
+        uniq[b] = sh[h]
+    words = lambda b: tuple(int.from_bytes(b[8 * w: 8 * w + 8], "little") for w in range(width // 8))
+    want = sorted(sorted(uniq.items(), key=lambda kv: (kv[1], words(kv[0])))[:k], key=lambda kv: kv[0])
+    d = Sampler.distinct(k, key_type=f"bytes{width}", seed=21, order="set")(hash=lambda b: 0)
+    rd, hd = torch.from_numpy(rows).to(cuda), torch.from_numpy(hs).to(cuda)
+    d.sample_all(rd[: n // 4], hashes=hd[: n // 4])
+    d.sample_all(rd[n // 4:], hashes=hd[n // 4:])
+    assert _sorted_rows(d.result()) == [kv[0] for kv in want]
