@@ -315,22 +315,31 @@ struct HostValuesWide {
         hs[(size_t)m] = s;
     }
     int32_t pq_dequeue() {  // dequeue + fixDown: larger child (left on ties), stop when parent >= child
-        const int32_t res = hs[1];
-        const int64_t h = hh[(size_t)n];
-        const int32_t e = hs[(size_t)n];
+        // (HostValues::pq_dequeue's form: the sinking hash in the slack slot past the end makes the
+        // child choice one branch-free compare; the grandchildren's lines are prefetched)
+        int64_t* H = hh.data();
+        int32_t* S = hs.data();
+        const int32_t res = S[1];
+        const int64_t h = H[n];
+        const int32_t e = S[n];
         const int64_t nn = --n;
         if (nn == 0) return res;
+        H[nn + 1] = h;
+        const int64_t last = (int64_t)hh.size() - 1;
         int64_t kk = 1;
         while (nn >= 2 * kk) {
             int64_t j = 2 * kk;
-            if (j < nn && hh[(size_t)j] < hh[(size_t)j + 1]) ++j;
-            if (h >= hh[(size_t)j]) break;
-            hh[(size_t)kk] = hh[(size_t)j];
-            hs[(size_t)kk] = hs[(size_t)j];
+            __builtin_prefetch(H + std::min(4 * j, last));
+            __builtin_prefetch(H + std::min(8 * j, last));
+            __builtin_prefetch(H + std::min(8 * j + 8, last));
+            j += H[j] < H[j + 1];
+            if (h >= H[j]) break;
+            H[kk] = H[j];
+            S[kk] = S[j];
             kk = j;
         }
-        hh[(size_t)kk] = h;
-        hs[(size_t)kk] = e;
+        H[kk] = h;
+        S[kk] = e;
         return res;
     }
     void insert(int64_t h, const uint64_t* r) {
@@ -366,6 +375,27 @@ struct HostValuesWide {
             free_slots.push_back(pq_dequeue());
             pq_add(alloc(h, r), h);
             max_hash = hh[1];
+        }
+    }
+    // sample_first for log entry `pos` of a run whose rows stay in place until adopt(): the heap holds
+    // -1 - pos instead of a pool slot, so a replacement moves no row and touches no slot pool (the
+    // UUID twin replay: the row copy into a recycled slot was a cache miss per replacement)
+    void sample_first_at(int64_t h, int64_t pos) {
+        if (n < k) {
+            pq_add((int32_t)(-1 - pos), h);
+            if (h > max_hash) max_hash = h;
+        } else if (h < max_hash) {
+            const int32_t old = pq_dequeue();
+            if (old >= 0) free_slots.push_back(old);
+            pq_add((int32_t)(-1 - pos), h);
+            max_hash = hh[1];
+        }
+    }
+    // the members still naming log entries take pool slots with their rows (run rows: log_rows)
+    void adopt(const uint64_t* log_rows) {
+        for (int64_t i = 1; i <= n; ++i) {
+            const int32_t s = hs[(size_t)i];
+            if (s < 0) hs[(size_t)i] = alloc(hh[(size_t)i], log_rows + (size_t)(-1 - (int64_t)s) * words);
         }
     }
     void table_rebuild() {

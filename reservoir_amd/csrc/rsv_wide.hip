@@ -1308,8 +1308,10 @@ hipError_t replay_log(WideDistinct* d, hipStream_t st) {
         std::vector<uint32_t> fl;
         if ((e = first_flags(d, fl, st))) return e;
         t2 = std::chrono::steady_clock::now();
+        // members name log entries during the run (no row moves per replacement), then take slots
         for (size_t t = 0; t < oh.size(); ++t)
-            if (fl[t]) d->rep.sample_first(oh[t], ok.data() + t * d->words);
+            if (fl[t]) d->rep.sample_first_at(oh[t], (int64_t)t);
+        d->rep.adopt(ok.data());
         d->rep.table_rebuild();
     } else {
         for (size_t t = 0; t < oh.size(); ++t) d->rep.sample(oh[t], ok.data() + t * d->words);
