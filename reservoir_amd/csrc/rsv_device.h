@@ -131,6 +131,54 @@ __device__ __forceinline__ void philox4x32_10_uniform_hi_x2(uint32_t c0, uint32_
     b = {b0, b1, b2, b3};
 }
 
+// M0^-1 mod 2^32: K1's queue entries carry lo(M0 c0) (the round-0 product a pair already holds)
+// instead of the counter word c0 itself, recovered as lo * M0^-1
+constexpr uint32_t kPhiloxM0Inv = 0x991A7CDBu;
+static_assert((uint32_t)(kPhiloxM0 * kPhiloxM0Inv) == 1u, "M0 inverse");
+
+// philox4x32_10_uniform_hi_x2 at counters c0 = gl + d and gl + d + 64 (d wave-uniform, no 2^32 wrap),
+// given m0v = M0 in a VGPR: each round-0 product is then one v_mad_u64_u32 m0v * gl + M0 (d [+ 64])
+// with the wave-uniform addend in SGPRs (a VOP3 reads one scalar operand), so the pair's counter word
+// needs no v_add.  lo_a = lo(M0 (gl + d)), the entry word K1 queues.
+__device__ __forceinline__ void philox4x32_10_uniform_hi_x2_at(uint32_t gl, uint32_t m0v, uint64_t offa,
+                                                               uint32_t c1, uint32_t c2, uint32_t c3,
+                                                               uint32_t k0, uint32_t k1, u32x4& a, u32x4& b,
+                                                               uint32_t& lo_a) {
+    const uint64_t p1u = (uint64_t)kPhiloxM1 * c2;
+    const uint32_t n0u = (uint32_t)(p1u >> 32) ^ c1 ^ k0;
+    const uint64_t pa = (uint64_t)m0v * gl + offa;
+    const uint64_t pb = (uint64_t)m0v * gl + (offa + (uint64_t)kPhiloxM0 * 64u);
+    lo_a = (uint32_t)pa;
+    const uint32_t da2 = xor3_key((uint32_t)(pa >> 32), c3, k1), db2 = xor3_key((uint32_t)(pb >> 32), c3, k1);
+    const uint32_t d1u = (uint32_t)p1u;
+    const uint32_t da3 = (uint32_t)pa, db3 = (uint32_t)pb;
+    const uint64_t q0u = (uint64_t)kPhiloxM0 * n0u;
+    const uint64_t qa = (uint64_t)kPhiloxM1 * da2, qb = (uint64_t)kPhiloxM1 * db2;
+    uint32_t a0 = (uint32_t)(qa >> 32) ^ (d1u ^ (k0 + kPhiloxW0)), b0 = (uint32_t)(qb >> 32) ^ (d1u ^ (k0 + kPhiloxW0));
+    uint32_t a2 = da3 ^ ((uint32_t)(q0u >> 32) ^ (k1 + kPhiloxW1)), b2 = db3 ^ ((uint32_t)(q0u >> 32) ^ (k1 + kPhiloxW1));
+    uint32_t a1 = (uint32_t)qa, b1 = (uint32_t)qb;
+    uint32_t a3 = (uint32_t)q0u, b3 = (uint32_t)q0u;
+#pragma unroll
+    for (int r = 2; r < 10; ++r) {
+        const uint64_t pa0 = (uint64_t)kPhiloxM0 * a0, pb0 = (uint64_t)kPhiloxM0 * b0;
+        const uint64_t pa1 = (uint64_t)kPhiloxM1 * a2, pb1 = (uint64_t)kPhiloxM1 * b2;
+        const uint32_t na0 = xor3_key((uint32_t)(pa1 >> 32), a1, k0 + (uint32_t)r * kPhiloxW0);
+        const uint32_t nb0 = xor3_key((uint32_t)(pb1 >> 32), b1, k0 + (uint32_t)r * kPhiloxW0);
+        const uint32_t na2 = xor3_key((uint32_t)(pa0 >> 32), a3, k1 + (uint32_t)r * kPhiloxW1);
+        const uint32_t nb2 = xor3_key((uint32_t)(pb0 >> 32), b3, k1 + (uint32_t)r * kPhiloxW1);
+        a0 = na0;
+        b0 = nb0;
+        a1 = (uint32_t)pa1;
+        b1 = (uint32_t)pb1;
+        a2 = na2;
+        b2 = nb2;
+        a3 = (uint32_t)pa0;
+        b3 = (uint32_t)pb0;
+    }
+    a = {a0, a1, a2, a3};
+    b = {b0, b1, b2, b3};
+}
+
 struct DrawKey {
     uint32_t k0, k1;  // Philox key = seed
     uint32_t s0, s1;  // Philox stream words (counter words 2, 3)

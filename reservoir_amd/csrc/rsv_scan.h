@@ -162,6 +162,8 @@ __device__ __forceinline__ uint32_t fold_pair(const u32x4& a, const u32x4& b) {
 // inside one asm block), so the unrolled window stays one basic block for the scheduler.
 template <int W>
 constexpr uint32_t k1q_cap() { return 64u * (1u + W / 2); }
+// waves per K1 workgroup (256 threads): the pooled tail's per-wave queue count
+constexpr uint32_t kQueueWaves = 4;
 
 // FAST (launch-uniform, the kernel picks): the level-1 counter's high word is uniform over the
 // launch and every index is below 2^40 -- the resolve then forms the counter's low word with
@@ -179,7 +181,8 @@ constexpr uint32_t k1q_cap() { return 64u * (1u + W / 2); }
 template <int W = 12, bool FAST = false>
 __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
                                           uint64_t n_groups, unsigned long long* __restrict__ win, uint64_t* q,
-                                          uint64_t* cq, uint32_t W1 = 0, uint32_t A = 0, uint32_t B = 0) {
+                                          uint64_t* cq, uint32_t W1 = 0, uint32_t A = 0, uint32_t B = 0,
+                                          uint32_t* pool = nullptr) {
     static_assert(W % 2 == 0, "half windows");
     constexpr int U = 2;
     const uint32_t lane = threadIdx.x & 63;
@@ -204,9 +207,10 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
     const uint32_t ng_steady = __builtin_amdgcn_readfirstlane((int)(ng - ((hi & 15) ? 1u : 0u)));
 
     // one queue entry per lane (valid lanes): its pair's first zero byte by level 1; the pair's other
-    // zero bytes go back to the queue; a dense / clipped pair (a z half 0) recomputes both blocks
+    // zero bytes go back to the queue; a dense / clipped pair (a z half 0) recomputes both blocks.  An
+    // entry's low word is lo(M0 gt) (what the steady pair's round 0 already holds), so gt = lo M0^-1.
     auto resolve = [&](bool valid, uint64_t ent) {
-        const uint32_t gt = (uint32_t)ent, off = gt - g0, z = (uint32_t)(ent >> 32);
+        const uint32_t gt = (uint32_t)ent * kPhiloxM0Inv, off = gt - g0, z = (uint32_t)(ent >> 32);
         // the dense test only while a partial iteration's dense entries are pending (the steady
         // loop appends none: a steady pair with a zero fold half would need 16 zero bytes in a
         // block, and resolving it as sparse is exact there anyway)
@@ -288,10 +292,15 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
     // the wave's queue base as a scalar (LDS addresses are 32-bit), so an append's address is one
     // v_lshl_add of the lane's slot onto base + 8 qn
     const uint32_t q_s = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)q);
-    // one steady iteration: the pair at counter word gt, its fold and mark appended (see below)
-    auto steady = [&](uint32_t gt) {
+    // M0 in a VGPR, opaque to the compiler (philox4x32_10_uniform_hi_x2_at)
+    uint32_t m0v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(m0v) : "s"(kPhiloxM0));
+    // one steady iteration: the pair at counter word gl + d (d wave-uniform), its fold and mark
+    // appended (see below); the entry's low word is lo(M0 (gl + d))
+    auto steady = [&](uint32_t d) {
         u32x4 w0, w1;
-        philox4x32_10_uniform_hi_x2(gt, ghi, dk.s0, dk.s1, dk.k0, dk.k1, w0, w1);
+        uint32_t glo;
+        philox4x32_10_uniform_hi_x2_at(gl, m0v, (uint64_t)kPhiloxM0 * d, ghi, dk.s0, dk.s1, dk.k0, dk.k1, w0, w1, glo);
         // the pair fold (with the gfx950 SDWA wait states, fold_pair) and its mark as a
         // lane mask in one asm block
         const uint32_t xa = w0.x | w0.y | w0.z | w0.w, xb = w1.x | w1.y | w1.z | w1.w;
@@ -308,7 +317,7 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
         // the marked lanes store (exec = m inside the asm, restored before it ends; one
         // wave's LDS operations complete in order, so the rounds' reads see the entries)
         const uint32_t sb = q_s + 8u * qn;
-        const uint64_t ent = (uint64_t)gt | ((uint64_t)z << 32);
+        const uint64_t ent = (uint64_t)glo | ((uint64_t)z << 32);
         unsigned long long sv;
         uint32_t addr;
         asm volatile("v_lshl_add_u32 %1, %2, 3, %3\n\t"
@@ -351,7 +360,7 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
             has = hb[0] | hb[1];
         }
         dpend += (int32_t)__popcll(__builtin_amdgcn_ballot_w64(has && ((z & 0xFFFFu) == 0 || (z >> 16) == 0)));
-        append(has, gl, z);
+        append(has, gl * kPhiloxM0, z);
         __builtin_amdgcn_wave_barrier();
         rounds();
     };
@@ -369,7 +378,7 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
             gl = g0 + ub + lane;
             if (ub >= off_steady && ub + UB <= ng_steady) {
 #pragma unroll
-                for (int t = 0; t < W / 2; ++t) steady(gl + t * (U * 64));
+                for (int t = 0; t < W / 2; ++t) steady(t * (U * 64));
                 __builtin_amdgcn_wave_barrier();
                 rounds();
             } else {  // a unit holding dense / clipped blocks or the launch's end
@@ -383,7 +392,7 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
 #pragma unroll
-                for (int t = 0; t < W / 2; ++t) steady(gl + t * stride);
+                for (int t = 0; t < W / 2; ++t) steady(t * stride);
                 gl += (W / 2) * stride;
                 __builtin_amdgcn_wave_barrier();
                 rounds();
@@ -395,14 +404,56 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
             }
         }
     }
-    while (qn > 0) {  // the last partial rounds (appends shrink geometrically)
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t nv = std::min<uint32_t>(qn, 64u);
-        qn -= nv;
-        const bool valid = lane < nv;
-        const uint64_t ent = valid ? q[qn + lane] : 0ull;
-        __builtin_amdgcn_wave_barrier();
-        resolve(valid, ent);
+    if (pool) {
+        // The workgroup's leftovers pooled (every wave holds < 64, and a pooled round's rests <= 64):
+        // round w of the waves' queues taken end to end goes to wave w, so a workgroup runs
+        // ceil(sum / 64) tail rounds at once instead of one or two per wave (each a whole wave's
+        // level-1 Philox however few lanes it holds); the rests they append are pooled again.  `pool`
+        // (LDS, one word per wave): the wave's count, bit 31 = it has dense entries pending (an entry
+        // may move to a wave without any, which then runs the dense test -- exact either way).
+        // Needs every wave of the workgroup here (k1_body_q is called workgroup-wide).  Measured
+        // (tools/micro_k1o o, profiles/r06/micro_k1o_tail_ab.jsonl): fewer VALU but no faster -- 81.2-81.5
+        // vs 80.7-81.2 us per 1e9 draws (the barriers hold each workgroup to its slowest wave), so the
+        // product kernels pass no pool and keep the per-wave tail below.
+        constexpr uint32_t cap = k1q_cap<W>(), NW = kQueueWaves;
+        const uint32_t wv = threadIdx.x >> 6;
+        const uint64_t* q0 = q - (size_t)wv * cap;
+        for (;;) {
+            if (lane == 0) pool[wv] = qn | (dpend > 0 ? 0x80000000u : 0u);
+            __syncthreads();
+            uint32_t c[NW], T = 0, anyd = 0;
+#pragma unroll
+            for (uint32_t v = 0; v < NW; ++v) {
+                const uint32_t pv = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool[v]);
+                c[v] = pv & 0x7FFFFFFFu;
+                anyd |= pv >> 31;
+                T += c[v];
+            }
+            if (T == 0) break;  // workgroup-uniform
+            uint32_t o = 64u * wv + lane, src = 0;
+            const bool valid = o < T;
+#pragma unroll
+            for (uint32_t v = 0; v + 1 < NW; ++v)
+                if (src == v && o >= c[v]) {
+                    o -= c[v];
+                    src = v + 1;
+                }
+            const uint64_t ent = valid ? q0[(size_t)src * cap + o] : 0ull;
+            __syncthreads();  // every read done before a wave appends to its own queue again
+            qn = 0;
+            dpend = anyd ? (1 << 30) : 0;
+            if (64u * wv < T) resolve(valid, ent);  // wave-uniform
+        }
+    } else {
+        while (qn > 0) {  // the last partial rounds (appends shrink geometrically)
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t nv = std::min<uint32_t>(qn, 64u);
+            qn -= nv;
+            const bool valid = lane < nv;
+            const uint64_t ent = valid ? q[qn + lane] : 0ull;
+            __builtin_amdgcn_wave_barrier();
+            resolve(valid, ent);
+        }
     }
     __builtin_amdgcn_wave_barrier();
     drain_queue(dk, cq, cqn, lane, k, hit);

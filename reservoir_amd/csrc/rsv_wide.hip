@@ -565,14 +565,28 @@ struct WSegMap {
     }
 };
 
+// the segment table as a kernel argument (2.3 KB of kernarg: no copy of its own on the stream)
+struct WSegTable {
+    int64_t w[kWSegWords];
+};
+
+// the merge's control words ctl[1..6] zeroed, and (first use of a bucket area) its counters: one
+// dispatch in place of the small memsets (a misaligned hipMemsetAsync is up to three fill kernels)
+__global__ __launch_bounds__(kWBlock) void wb_prep(int64_t* __restrict__ ctl, uint32_t* __restrict__ cnt,
+                                                   uint32_t n_cnt) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < 6) ctl[1 + t] = 0;
+    for (uint32_t i = t; i < n_cnt; i += gridDim.x * blockDim.x) cnt[i] = 0;
+}
+
 __global__ __launch_bounds__(kWBlock) void wb_scatter(const int64_t* __restrict__ set_h, int64_t m,
                                                       const int64_t* __restrict__ cand_h, int64_t c,
-                                                      const int64_t* __restrict__ seg, int32_t ns, uint32_t B,
+                                                      const WSegTable seg, int32_t ns, uint32_t B,
                                                       int64_t* __restrict__ bh, uint32_t* __restrict__ be,
                                                       uint32_t* __restrict__ cnt, uint32_t* __restrict__ gsum,
                                                       int64_t* __restrict__ ctl, bool c_on_device) {
     __shared__ int64_t s_seg[kWSegWords];
-    for (int i = threadIdx.x; i < kWSegWords; i += blockDim.x) s_seg[i] = seg[i];
+    for (int i = threadIdx.x; i < kWSegWords; i += blockDim.x) s_seg[i] = seg.w[i];
     if (blockIdx.x == 0)
         for (uint32_t i = threadIdx.x; i <= (B >> 4); i += blockDim.x) gsum[i] = 0;
     __syncthreads();
@@ -914,11 +928,11 @@ struct WideDistinct {
     uint32_t* wb_dist = nullptr;
     uint32_t* wb_gsum = nullptr;
     uint32_t wb_cap = 0;
+    bool wb_cnt_dirty = false;    // a new bucket area: its counters are zeroed by the next wb_prep
     bool bucketed_on = true;      // RSV_WIDE_BUCKETED=0: the sort-based merge only (A/B, tests)
     bool last_bucketed = false;   // the last merge's sorted entries are in the bucket area (wb_verify)
     uint32_t last_B = 0;
-    int64_t* wb_seg = nullptr;    // the bucket map's segment table (device) and its pinned staging
-    int64_t* hwb_seg = nullptr;
+    WSegTable hwb_seg;            // the bucket map's segment table (passed by value to wb_scatter)
     int64_t merges = 0;           // merges applied (a set swap each)
     // speculative publication (set mode's one-pass batches, wide_spec_target): armed around the pass,
     // enqueued behind its merge; valid when the pass proved its bound and no other merge followed
@@ -1038,7 +1052,7 @@ hipError_t ensure_buckets(WideDistinct* d, uint32_t B, hipStream_t st) {
     if ((e = wgrow((void**)&d->wb_dist, 0, c * 4, false, st))) return e;
     if ((e = wgrow((void**)&d->wb_gsum, 0, (c / 16 + 1) * 4, false, st))) return e;
     if ((e = wgrow((void**)&d->wb_cnt, 0, c * kWStride * 4, false, st))) return e;
-    if ((e = hipMemsetAsync(d->wb_cnt, 0, c * kWStride * 4, st))) return e;
+    d->wb_cnt_dirty = true;
     d->wb_cap = (uint32_t)c;
     return hipSuccess;
 }
@@ -1066,15 +1080,11 @@ hipError_t merge_bucketed(WideDistinct* d, int64_t c, int64_t span_hi, bool arri
     const std::vector<WSeg>& sg = segs && !segs->empty() && (int)segs->size() <= kWSegMax ? *segs : one;
     const int32_t ns = (int32_t)sg.size();
     hipError_t e;
-    if (!d->wb_seg) {
-        if ((e = walloc((void**)&d->wb_seg, kWSegWords * 8))) return e;
-        if ((e = pool_host_alloc((void**)&d->hwb_seg, kWSegWords * 8, hipHostMallocDefault))) return e;
-    }
     // buckets: ~64 entries each overall, shared out in proportion to each segment's expected entries
     const int64_t Bt = std::min<int64_t>(std::max<int64_t>((N + (1 << kWAvgLog) - 1) >> kWAvgLog, 1), 1 << 24);
     double tot = 0;
     for (const WSeg& x : sg) tot += std::max(x.expect, 0.0);
-    int64_t* lo = d->hwb_seg;
+    int64_t* lo = d->hwb_seg.w;
     int64_t* b0 = lo + kWSegMax + 1;
     int64_t* mult = lo + 2 * kWSegMax + 2;
     int64_t* nb = lo + 3 * kWSegMax + 2;
@@ -1097,10 +1107,12 @@ hipError_t merge_bucketed(WideDistinct* d, int64_t c, int64_t span_hi, bool arri
     b0[ns] = B;
     if ((e = ensure_buckets(d, (uint32_t)B, st))) return e;
     const WRows R{d->set_k, d->cand_k, d->m, d->words};
-    if ((e = hipMemcpyAsync(d->wb_seg, d->hwb_seg, kWSegWords * 8, hipMemcpyHostToDevice, st))) return e;
     // ctl[1..6]; ctl[0] is the filter's count when c_on_device, ctl[7] the publication ticket (always 0)
-    if ((e = hipMemsetAsync(d->ctl + 1, 0, 6 * 8, st))) return e;
-    hipLaunchKernelGGL(wb_scatter, dim3(wgrid(N, 8192)), dim3(kWBlock), 0, st, d->set_h, d->m, d->cand_h, c, d->wb_seg,
+    const uint32_t n_cnt = d->wb_cnt_dirty ? d->wb_cap * kWStride : 0u;
+    hipLaunchKernelGGL(wb_prep, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_cnt + 4 * kWBlock - 1) / (4 * kWBlock), 256))),
+                       dim3(kWBlock), 0, st, d->ctl, d->wb_cnt, n_cnt);
+    d->wb_cnt_dirty = false;
+    hipLaunchKernelGGL(wb_scatter, dim3(wgrid(N, 8192)), dim3(kWBlock), 0, st, d->set_h, d->m, d->cand_h, c, d->hwb_seg,
                        ns, (uint32_t)B, d->wb_h, d->wb_e, d->wb_cnt, d->wb_gsum, d->ctl, c_on_device);
     hipLaunchKernelGGL(wb_sort, dim3((unsigned)((B + kWBlock / 64 - 1) / (kWBlock / 64))), dim3(kWBlock), 0, st, d->m,
                        (uint32_t)B, d->wb_h, d->wb_e, arrivals ? d->wb_a : nullptr, d->wb_cnt, d->wb_dist, d->wb_gsum, R,
@@ -1117,7 +1129,7 @@ hipError_t merge_bucketed(WideDistinct* d, int64_t c, int64_t span_hi, bool arri
         d->spec_gen = gen;
         d->spec_merges = d->merges + 1;
     }
-    if ((e = read_ctl(d, st))) return e;  // (the pinned segment table is free again after this wait)
+    if ((e = read_ctl(d, st))) return e;
     if (d->hctl[1]) {
         d->spec_merges = -1;  // what was published is not a merge result
         return hipSuccess;
@@ -1675,9 +1687,8 @@ void wide_destroy(WideDistinct* d) {
                   d->ev0, d->ev1, d->flags, d->pos, d->temp, d->ctl, d->log_h, d->log_g, d->log_k};
     for (void* p : ps) pool_device_free(p);  // the owner's stream is idle (rsv_destroy)
     pool_device_free(d->sched);
-    void* wb[] = {d->wb_h, d->wb_e, d->wb_a, d->wb_cnt, d->wb_dist, d->wb_gsum, d->wb_seg};
+    void* wb[] = {d->wb_h, d->wb_e, d->wb_a, d->wb_cnt, d->wb_dist, d->wb_gsum};
     for (void* p : wb) pool_device_free(p);
-    pool_host_free(d->hwb_seg);
     pool_host_free(d->hsched);
     pool_host_free(d->hctl);
     delete d;

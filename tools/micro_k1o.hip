@@ -70,6 +70,7 @@ template <int W>
 struct K1QLds {
     uint64_t q[4][k1q_cap<W>()];
     uint64_t cq[4][kQueue];
+    uint32_t pool[4];
 };
 template <int W, bool FAST = false>
 __global__ __launch_bounds__(256) void k1_q(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
@@ -108,6 +109,16 @@ __global__ __launch_bounds__(256) void k1_qp(DrawKey dk, uint32_t k, uint64_t lo
     const int w = threadIdx.x >> 6;
     (void)TRIM;
     k1_body_q<W, FAST>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], W1, A, B);
+}
+
+// the product body with the workgroup-pooled tail (round 6; k1_qp keeps the per-wave tail)
+template <int W, bool FAST>
+__global__ __launch_bounds__(256) void k1_qpp(DrawKey dk, uint32_t k, uint64_t lo, uint64_t hi, uint64_t g_begin,
+                                              uint64_t n_groups, unsigned long long* __restrict__ win, uint32_t W1,
+                                              uint32_t A, uint32_t B) {
+    __shared__ K1QLds<W> L;
+    const int w = threadIdx.x >> 6;
+    k1_body_q<W, FAST>(dk, k, lo, hi, g_begin, n_groups, win, L.q[w], L.cq[w], W1, A, B, L.pool);
 }
 
 // the product body over its plan with each wave's shader clock stamped at entry and exit (a separate
@@ -315,6 +326,52 @@ int main(int argc, char** argv) {
                    "\"clock_GHz_p10\": %.3f, \"clock_GHz_p90\": %.3f}\n", ms / reps * 1e3, clk.size(),
                    clk[clk.size() / 2], clk[clk.size() / 10], clk[clk.size() * 9 / 10]);
         }
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'o') {  // round 6: per-wave vs workgroup-pooled tail; argv[2..] "W1:A:B" plans
+        // (the r05 schedule body k1_body_q_sched -- round-5 steady and tail -- beside them at 6144:10:2)
+        const uint32_t units = (uint32_t)((n_groups + 767) / 768);
+        for (int rep = 0; rep < 3000; ++rep)
+            hipLaunchKernelGGL((k1_qpp<12, true>), dim3(4024), dim3(256), 0, 0, dk, k, lo, n, 0ull, n_groups, win, 6144u,
+                               10u, 2u);
+        CK(hipDeviceSynchronize());
+        for (int p = 0; p < 3; ++p)
+            for (int a = 2; a < argc; ++a) {
+                unsigned W1, A, B;
+                if (sscanf(argv[a], "%u:%u:%u", &W1, &A, &B) != 3) return 2;
+                const uint64_t rest = (uint64_t)units > (uint64_t)W1 * A ? units - (uint64_t)W1 * A : 0;
+                const uint64_t waves = std::min<uint64_t>(W1, (units + A - 1) / A) + (rest + B - 1) / B;
+                const int grid = (int)((waves + 3) / 4);
+                for (int v = 0; v < 3; ++v) {
+                    if (v == 2 && !(W1 == 6144 && A == 10 && B == 2)) continue;
+                    auto launch = [&]() {
+                        if (v == 0)
+                            hipLaunchKernelGGL((k1_qp<12, true, false>), dim3(grid), dim3(256), 0, 0, dk, k, lo, n, 0ull,
+                                               n_groups, win, W1, A, B);
+                        else if (v == 1)
+                            hipLaunchKernelGGL((k1_qpp<12, true>), dim3(grid), dim3(256), 0, 0, dk, k, lo, n, 0ull, n_groups,
+                                               win, W1, A, B);
+                        else
+                            hipLaunchKernelGGL((k1_qs<12, true>), dim3(grid), dim3(256), 0, 0, dk, k, lo, n, 0ull, n_groups,
+                                               win, W1, A, B);
+                    };
+                    for (int rep = 0; rep < 3; ++rep) launch();
+                    const int reps = 20;
+                    CK(hipEventRecord(e0));
+                    for (int rep = 0; rep < reps; ++rep) launch();
+                    CK(hipEventRecord(e1));
+                    CK(hipEventSynchronize(e1));
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    CK(hipMemset(win, 0, k * 8));
+                    launch();
+                    CK(hipMemcpy(got.data(), win, k * 8, hipMemcpyDeviceToHost));
+                    printf("{\"mode\": \"tail\", \"body\": \"%s\", \"W1\": %u, \"A\": %u, \"B\": %u, \"grid\": %d, "
+                           "\"us\": %.2f, \"winners_match\": %s}\n",
+                           v == 0 ? "per_wave_tail" : v == 1 ? "pooled_tail" : "r05_sched_body", W1, A, B, grid,
+                           ms / reps * 1e3, got == ref ? "true" : "false");
+                }
+            }
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'w') {  // window length under the two-group plan: W = 8 / 12 / 16
