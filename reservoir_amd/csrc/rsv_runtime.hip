@@ -473,7 +473,9 @@ rsv_status process_device_batch(rsv_sampler* s, const void* keys, const int64_t*
         // Fused (one dispatch, the last workgroup resolves) for batches up to 2^27 draws, where the
         // saved dispatch is a visible share of the step; above that the two-dispatch form is faster
         // (C2: 112.5 vs 114.0 us per step, r02aa: the fused tail runs on one workgroup of the
-        // otherwise idle chip, while resolve_publish_kernel's dispatch overlaps K1's drain).
+        // otherwise idle chip, while resolve_publish_kernel's dispatch overlaps K1's drain; round 6,
+        // the two-group K1: 96.7 vs 83.0-83.7 us per launch, 97.2 vs 88.6-89.5 us per step --
+        // every workgroup's ticket wait holds its slot, profiles/r06/bench_k1_fuse_ab.jsonl).
         // RSV_K1_FUSE=0 / =1 forces either form (A/B measurements).
         static const int fuse_mode = [] {
             const char* e = std::getenv("RSV_K1_FUSE");
