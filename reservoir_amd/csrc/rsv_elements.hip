@@ -202,6 +202,53 @@ __global__ __launch_bounds__(1024) void resolve_publish_kernel(const KeyT* __res
     publish_flag(flag, gen);
 }
 
+// resolve_publish_kernel for one 256-thread workgroup with R slots per lane, all R winner loads
+// issued before any key gather (k <= 256 R).  For a resolve forked onto a second stream beside the
+// next batch's K1 (rsv_set_resolve_stream): 4 waves fit beside K1's six workgroups on a CU, where
+// the 1024-thread form's 16 waves displace one of them (K1's first-generation schedule then ends late).
+template <typename KeyT, int R>
+__global__ __launch_bounds__(kBlock) void resolve_publish_small_kernel(const KeyT* __restrict__ keys, int64_t base,
+                                                                       int64_t n, uint32_t k,
+                                                                       unsigned long long* __restrict__ win,
+                                                                       KeyT* __restrict__ slot_key,
+                                                                       int64_t* __restrict__ slot_idx, int fresh,
+                                                                       int64_t m, KeyT* dst, uint32_t* flag, uint32_t gen) {
+    unsigned long long wi[R];
+    KeyT v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t j = threadIdx.x + r * kBlock;
+        wi[r] = j < k ? win[j] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t j = threadIdx.x + r * kBlock;
+        if (j >= k) continue;
+        if (wi[r]) v[r] = keys[(int64_t)wi[r] - base];
+        else if (j >= base && j < base + n) v[r] = keys[j - base];
+        else if (fresh) v[r] = 0;
+        else v[r] = slot_key[j];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t j = threadIdx.x + r * kBlock;
+        if (j >= k) continue;
+        if (wi[r]) {
+            slot_key[j] = v[r];
+            slot_idx[j] = (int64_t)wi[r];
+            win[j] = 0;
+        } else if (j >= base && j < base + n) {
+            slot_key[j] = v[r];
+            slot_idx[j] = j;
+        } else if (fresh) {
+            slot_key[j] = 0;
+            slot_idx[j] = -1;
+        }
+        if (j < m) dst[j] = v[r];
+    }
+    publish_flag(flag, gen);
+}
+
 __global__ __launch_bounds__(kBlock) void replay_kernel(const int64_t* __restrict__ ev_pos,
                                                         const int32_t* __restrict__ ev_slot,
                                                         int64_t n_events, uint32_t k,
@@ -587,7 +634,24 @@ hipError_t launch_publish(const void* src, int64_t bytes, void* dst_host_dev, ui
 
 hipError_t launch_resolve_publish(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,
                                   unsigned long long* batch_win, void* slot_key, int64_t* slot_idx, bool fresh,
-                                  int64_t m, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st) {
+                                  int64_t m, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st,
+                                  bool small) {
+    if (small && k <= 8 * kBlock && (key_width == 8 || key_width == 4)) {
+#define RSV_SMALL(T, R)                                                                                              \
+    hipLaunchKernelGGL((resolve_publish_small_kernel<T, R>), dim3(1), dim3(kBlock), 0, st, (const T*)keys, base, n, \
+                       k, batch_win, (T*)slot_key, slot_idx, (int)fresh, m, (T*)dst_host_dev, flag_dev, gen)
+        if (key_width == 8) {
+            if (k <= 2 * kBlock) RSV_SMALL(int64_t, 2);
+            else if (k <= 4 * kBlock) RSV_SMALL(int64_t, 4);
+            else RSV_SMALL(int64_t, 8);
+        } else {
+            if (k <= 2 * kBlock) RSV_SMALL(int32_t, 2);
+            else if (k <= 4 * kBlock) RSV_SMALL(int32_t, 4);
+            else RSV_SMALL(int32_t, 8);
+        }
+#undef RSV_SMALL
+        return hipGetLastError();
+    }
     const unsigned threads = std::min<unsigned>(1024, std::max<unsigned>(64, (k + 63) / 64 * 64));
     if (key_width > 8) {
         hipLaunchKernelGGL(resolve_wide_kernel, dim3(1), dim3(threads), 0, st, (const uint32_t*)keys, base, n, k,

@@ -105,10 +105,12 @@ hipError_t launch_resolve(const void* keys, int key_width, int64_t base, int64_t
                           unsigned long long* batch_win, void* slot_key, int64_t* slot_idx, bool fresh,
                           hipStream_t st);
 // resolve + publish of the first m slot keys into coherent host memory + flag = gen (k <= 8192;
-// slot_idx must be non-null)
+// slot_idx must be non-null); small: one 256-thread workgroup where k <= 2048 (a resolve running
+// beside K1 on a second stream)
 hipError_t launch_resolve_publish(const void* keys, int key_width, int64_t base, int64_t n, uint32_t k,
                                   unsigned long long* batch_win, void* slot_key, int64_t* slot_idx, bool fresh,
-                                  int64_t m, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st);
+                                  int64_t m, void* dst_host_dev, uint32_t* flag_dev, uint32_t gen, hipStream_t st,
+                                  bool small = false);
 // index-only batches: resolve into slot_idx with offs[k] = the batch offset of each changed slot
 // (-1: unchanged); then the caller's keys into the changed slots
 hipError_t launch_resolve_indices(int64_t base, int64_t n, uint32_t k, unsigned long long* batch_win, int64_t* slot_idx,

@@ -373,6 +373,16 @@ rsv_status ensure_result_buffer(rsv_sampler* s) {
 
 constexpr uint32_t kFusedPublishMaxK = 8192;  // resolve_publish: one workgroup, <= 8 slots per lane
 
+// a resolve forked onto the resolve stream runs as ONE 256-thread workgroup (beside the next K1;
+// RSV_RESOLVE_SMALL=0: the 1024-thread form, for A/B)
+bool resolve_small() {
+    static const bool v = [] {
+        const char* e = std::getenv("RSV_RESOLVE_SMALL");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // The batch's resolve: fill phase + winners into the slots; for reservoirs of <= 8192 keys it
 // also writes the first min(count, k) keys into the coherent result buffer and publishes
 // generation ++result_gen there (one dispatch instead of resolve now + publish at result()).
@@ -385,7 +395,8 @@ rsv_status resolve_batch(rsv_sampler* s, const void* keys, int64_t base, int64_t
             const uint32_t gen = ++s->result_gen;
             const int64_t m = std::min<int64_t>(base + n, (int64_t)s->k);
             RSV_HIP_TRY(launch_resolve_publish(keys, s->kw, base, n, s->k, s->batch_win, s->slot_key, s->slot_idx,
-                                               fresh, m, s->result_dev, s->result_flag_dev, gen, rst));
+                                               fresh, m, s->result_dev, s->result_flag_dev, gen, rst,
+                                               rst != s->stream && resolve_small()));
             s->pub_ops = s->ops;  // the last work of this group
             s->pub_gen = gen;
             s->pub_valid = true;

@@ -4,7 +4,8 @@
 
 Copies the rocprofv3 kernel-stats CSVs and writes, per profiled kernel, the per-launch PMC figures:
   SQ_INSTS_VALU          wave-instructions (all XCDs)
-  GRBM_GUI_ACTIVE / 8    GPU cycles (the counter sums the 8 XCDs, MI355X_MICROARCH.md)
+  duration x 2.4 GHz     GPU cycles at the peak clock (GRBM_GUI_ACTIVE / 8 reads high on < 0.3 ms
+                         dispatches, MI355X_MICROARCH.md: kept as a diagnostic only)
   FETCH_SIZE, WRITE_SIZE KiB; on gfx950 FETCH_SIZE reads half the bytes of a coalesced read and
                          WRITE_SIZE reads them exactly (MI355X_MICROARCH.md HBM section)
                          -> hbm_bytes_per_launch = FETCH_SIZE x 2 KiB + WRITE_SIZE KiB (other access
@@ -54,6 +55,18 @@ def pmc(dirpath: str, kernel: str) -> dict:
     return out
 
 
+def in_kernel_clock(*dirs: str):
+    """The median in-kernel clock over the K1 launches of a k1_in_kernel_clock.jsonl, or None."""
+    for d in dirs:
+        p = os.path.join(d, "k1_in_kernel_clock.jsonl")
+        if not os.path.exists(p):
+            continue
+        rows = [json.loads(line) for line in open(p) if '"k1_in_kernel_clock"' in line]
+        if rows:
+            return {"clock_GHz_median": round(statistics.median(r["clock_GHz_median"] for r in rows), 3), "file": p}
+    return None
+
+
 def main(src: str, dst: str) -> None:
     os.makedirs(dst, exist_ok=True)
     # merged into an existing summary (other runs' kernels, e.g. the C3 line-request pass, stay)
@@ -71,17 +84,25 @@ def main(src: str, dst: str) -> None:
             continue
         d = {"kernel": kern, "sq_pass": sq, "fetch_pass": fe, "write_pass": wr,
              "pmc_source_run": summary["source_run"]}
-        if "SQ_INSTS_VALU" in sq and "GRBM_GUI_ACTIVE" in sq:
-            cyc = sq["GRBM_GUI_ACTIVE"] / 8
+        if "SQ_INSTS_VALU" in sq and "dur_us_median" in sq:
+            # GPU cycles per launch = the launch's duration x 2.4 GHz, the peak shader clock (so an
+            # upper bound on the cycles the launch had: no clock above the peak is implied).
+            # GRBM_GUI_ACTIVE / 8 / duration is kept only as a diagnostic: MI355X_MICROARCH.md ("DVFS
+            # give-back") notes that quotient reads high on dispatches shorter than ~0.3 ms (K1's 84 us
+            # launch read 2.53 GHz).  The in-kernel clock (s_memtime / s_memrealtime, tools/micro_k1o
+            # c) is reported beside it when a run of it is at hand.
+            cyc = sq["dur_us_median"] * 1e-6 * 2.4e9
             d["valu_instrs_per_launch"] = sq["SQ_INSTS_VALU"]
-            d["gpu_cycles_per_launch"] = cyc
+            d["gpu_cycles_per_launch"] = round(cyc, 1)
+            d["clock_GHz"] = 2.4
+            d["clock_source"] = "peak shader clock x launch duration (upper bound on cycles)"
             d["cycles_per_valu_instr_per_simd"] = round(cyc * 1024 / sq["SQ_INSTS_VALU"], 3)
-            if "dur_us_median" in sq:
-                d["clock_GHz"] = round(cyc / (sq["dur_us_median"] * 1e-6) / 1e9, 3)
-                # the same normalised by the launch's duration at the 2.4 GHz peak shader clock (the
-                # VALU model's clock): cycles per wave-instruction per SIMD if the clock ran at peak
-                d["cycles_per_valu_instr_per_simd_at_2.4GHz"] = round(
-                    sq["dur_us_median"] * 1e-6 * 2.4e9 * 1024 / sq["SQ_INSTS_VALU"], 3)
+            clk = in_kernel_clock(src, dst)
+            if clk:
+                d["in_kernel_clock_GHz_median"] = clk["clock_GHz_median"]
+                d["in_kernel_clock_file"] = clk["file"]
+            if "GRBM_GUI_ACTIVE" in sq:
+                d["grbm_quotient_GHz_diagnostic"] = round(sq["GRBM_GUI_ACTIVE"] / 8 / (sq["dur_us_median"] * 1e-6) / 1e9, 3)
         if "FETCH_SIZE" in fe and "WRITE_SIZE" in wr:
             d["hbm_bytes_per_launch"] = int((2 * fe["FETCH_SIZE"] + wr["WRITE_SIZE"]) * 1024)
             d["hbm_bytes_rule"] = "(2 x FETCH_SIZE + WRITE_SIZE) KiB (gfx950 FETCH_SIZE correction)"
