@@ -57,8 +57,7 @@ def pmc(dirpath: str, kernel: str) -> dict:
 
 def in_kernel_clock(*dirs: str):
     """The median in-kernel clock over the K1 launches of a k1_in_kernel_clock.jsonl, or None."""
-    for d in dirs:
-        p = os.path.join(d, "k1_in_kernel_clock.jsonl")
+    for p in (os.path.join(d, f) for d in dirs for f in ("k1_clock.log", "k1_in_kernel_clock.jsonl")):
         if not os.path.exists(p):
             continue
         rows = [json.loads(line) for line in open(p) if '"k1_in_kernel_clock"' in line]
