@@ -67,7 +67,8 @@ __device__ __forceinline__ u32x4 philox4x32_10_uniform_hi(uint32_t c0, uint32_t 
     const uint64_t p1u = (uint64_t)kPhiloxM1 * c2;                  // scalar
     const uint32_t n0u = (uint32_t)(p1u >> 32) ^ c1 ^ k0;           // scalar
     const uint64_t p0 = (uint64_t)kPhiloxM0 * c0 + add0;            // vector: M0 (c0 + d) mod 2^64
-    uint32_t d2 = xor3_key((uint32_t)(p0 >> 32), c3, k1);           // vector (c3 ^ k1 is scalar)
+    // c3 ^ k1 on the scalar unit: a v_bitop3 with two scalar operands costs a v_mov first
+    uint32_t d2 = (uint32_t)(p0 >> 32) ^ (c3 ^ k1);
     const uint32_t d1u = (uint32_t)p1u;                             // scalar
     uint32_t d3 = (uint32_t)p0;                                     // vector
     // round 1
@@ -77,8 +78,18 @@ __device__ __forceinline__ u32x4 philox4x32_10_uniform_hi(uint32_t c0, uint32_t 
     uint32_t c2v = d3 ^ ((uint32_t)(q0u >> 32) ^ (k1 + kPhiloxW1));  // one scalar operand
     uint32_t c1v = (uint32_t)q1;
     uint32_t c3v = (uint32_t)q0u;  // scalar until round 2 (its product's operand is c2v)
+    {  // round 2: c3v and the key are both scalar (one v_xor, no v_mov)
+        const uint64_t p0r = (uint64_t)kPhiloxM0 * c0v;
+        const uint64_t p1r = (uint64_t)kPhiloxM1 * c2v;
+        const uint32_t n0 = xor3_key((uint32_t)(p1r >> 32), c1v, k0 + 2u * kPhiloxW0);
+        const uint32_t n2 = (uint32_t)(p0r >> 32) ^ (c3v ^ (k1 + 2u * kPhiloxW1));
+        c0v = n0;
+        c1v = (uint32_t)p1r;
+        c2v = n2;
+        c3v = (uint32_t)p0r;
+    }
 #pragma unroll
-    for (int r = 2; r < 10; ++r) {
+    for (int r = 3; r < 10; ++r) {
         const uint64_t p0r = (uint64_t)kPhiloxM0 * c0v;
         const uint64_t p1r = (uint64_t)kPhiloxM1 * c2v;
         const uint32_t n0 = xor3_key((uint32_t)(p1r >> 32), c1v, k0 + (uint32_t)r * kPhiloxW0);
@@ -149,7 +160,8 @@ __device__ __forceinline__ void philox4x32_10_uniform_hi_x2_at(uint32_t gl, uint
     const uint64_t pa = (uint64_t)m0v * gl + offa;
     const uint64_t pb = (uint64_t)m0v * gl + (offa + (uint64_t)kPhiloxM0 * 64u);
     lo_a = (uint32_t)pa;
-    const uint32_t da2 = xor3_key((uint32_t)(pa >> 32), c3, k1), db2 = xor3_key((uint32_t)(pb >> 32), c3, k1);
+    const uint32_t c3k = c3 ^ k1;  // scalar (see philox4x32_10_uniform_hi)
+    const uint32_t da2 = (uint32_t)(pa >> 32) ^ c3k, db2 = (uint32_t)(pb >> 32) ^ c3k;
     const uint32_t d1u = (uint32_t)p1u;
     const uint32_t da3 = (uint32_t)pa, db3 = (uint32_t)pb;
     const uint64_t q0u = (uint64_t)kPhiloxM0 * n0u;
@@ -158,8 +170,24 @@ __device__ __forceinline__ void philox4x32_10_uniform_hi_x2_at(uint32_t gl, uint
     uint32_t a2 = da3 ^ ((uint32_t)(q0u >> 32) ^ (k1 + kPhiloxW1)), b2 = db3 ^ ((uint32_t)(q0u >> 32) ^ (k1 + kPhiloxW1));
     uint32_t a1 = (uint32_t)qa, b1 = (uint32_t)qb;
     uint32_t a3 = (uint32_t)q0u, b3 = (uint32_t)q0u;
+    {  // round 2: a3 = b3 and the key are scalar
+        const uint64_t pa0 = (uint64_t)kPhiloxM0 * a0, pb0 = (uint64_t)kPhiloxM0 * b0;
+        const uint64_t pa1 = (uint64_t)kPhiloxM1 * a2, pb1 = (uint64_t)kPhiloxM1 * b2;
+        const uint32_t na0 = xor3_key((uint32_t)(pa1 >> 32), a1, k0 + 2u * kPhiloxW0);
+        const uint32_t nb0 = xor3_key((uint32_t)(pb1 >> 32), b1, k0 + 2u * kPhiloxW0);
+        const uint32_t s3 = (uint32_t)q0u ^ (k1 + 2u * kPhiloxW1);
+        const uint32_t na2 = (uint32_t)(pa0 >> 32) ^ s3, nb2 = (uint32_t)(pb0 >> 32) ^ s3;
+        a0 = na0;
+        b0 = nb0;
+        a1 = (uint32_t)pa1;
+        b1 = (uint32_t)pb1;
+        a2 = na2;
+        b2 = nb2;
+        a3 = (uint32_t)pa0;
+        b3 = (uint32_t)pb0;
+    }
 #pragma unroll
-    for (int r = 2; r < 10; ++r) {
+    for (int r = 3; r < 10; ++r) {
         const uint64_t pa0 = (uint64_t)kPhiloxM0 * a0, pb0 = (uint64_t)kPhiloxM0 * b0;
         const uint64_t pa1 = (uint64_t)kPhiloxM1 * a2, pb1 = (uint64_t)kPhiloxM1 * b2;
         const uint32_t na0 = xor3_key((uint32_t)(pa1 >> 32), a1, k0 + (uint32_t)r * kPhiloxW0);

@@ -211,6 +211,9 @@ __device__ __forceinline__ void k1_body_q(const DrawKey& dk, uint32_t k, uint64_
     // entry's low word is lo(M0 gt) (what the steady pair's round 0 already holds), so gt = lo M0^-1.
     auto resolve = [&](bool valid, uint64_t ent) {
         const uint32_t gt = (uint32_t)ent * kPhiloxM0Inv, off = gt - g0, z = (uint32_t)(ent >> 32);
+        // every queued entry holds a zero byte or a dense half (its fold is never all ones): a full
+        // round (valid) needs no zm != 0 test
+        __builtin_assume(!valid || z != 0xFFFFFFFFu);
         // the dense test only while a partial iteration's dense entries are pending (the steady
         // loop appends none: a steady pair with a zero fold half would need 16 zero bytes in a
         // block, and resolving it as sparse is exact there anyway)
