@@ -225,11 +225,22 @@ __device__ __forceinline__ int64_t k2_stream(const Wave& W, const KeyT* __restri
         const uint32_t tag = (ring << 10) | (lane << 4);  // = (g mod 256) << 4
         if (tail - head + tot <= W.fifo_cap) {  // uniform: the whole iteration fits
             uint32_t pos = tail + incl - cnt;
-            while (mask) {
-                const uint32_t e = __builtin_ctz(mask);
-                mask &= mask - 1;
-                W.q[pos & (QC - 1)] = (uint16_t)(tag | e);
-                ++pos;
+            if ((tail & (QC - 1)) + tot <= QC) {  // uniform: no ring wrap inside the iteration's span
+                // the lane's run is contiguous: one address increment per entry (round 6: no
+                // ring mask and address rebuild per entry, ~2 VALU per append-loop trip)
+                uint16_t* qp = W.q + (pos & (QC - 1));
+                while (mask) {
+                    const uint32_t e = __builtin_ctz(mask);
+                    mask &= mask - 1;
+                    *qp++ = (uint16_t)(tag | e);
+                }
+            } else {
+                while (mask) {
+                    const uint32_t e = __builtin_ctz(mask);
+                    mask &= mask - 1;
+                    W.q[pos & (QC - 1)] = (uint16_t)(tag | e);
+                    ++pos;
+                }
             }
             tail += tot;
         } else {  // an iteration denser than the FIFO (never at random draws beyond the dense
