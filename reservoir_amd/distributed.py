@@ -73,7 +73,10 @@ def combine(sampler, group=None, device=None, total_count: int | None = None, ma
     sequential set (every rank needs ``retain_log``; ``sample_shard`` sets it).  When the replay is
     needed and a rank did not retain its log, ``strict`` (default) raises IllegalStateException --
     the reference's set cannot be formed -- and ``strict=False`` warns and keeps the (hash, key)
-    bottom-k instead.  Returns whether the replay ran.
+    bottom-k instead.  The tie is only known once the device merge has run, so when it raises,
+    ``sampler`` already holds that merged (hash, key) bottom-k (as with ``strict=False``); callers
+    that want the old warn-and-continue behaviour (before round 6 the default) pass
+    ``strict=False``.  Returns whether the replay ran.
     ``marks`` (a list): CUDA events are appended after the export, the all-gather and the merge.
     """
     world = dist.get_world_size(group)
