@@ -31,6 +31,27 @@ def test_ragged_parity(cuda, oracle, k):
     assert np.array_equal(out.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("k", [1, 2, 3, 17, 63, 64])
+def test_two_deep_gather_stream_counts(cuda, oracle, k):
+    """k <= 64 gathers each stream's winners two streams later (rsv_k2.h, slot u waited on with an
+    explicit vmcnt(2)): odd and even numbers of streams per wave, and the launch's last streams
+    (a wave's final one or two slots drained after its loop), vs the oracle."""
+    import torch
+
+    from reservoir_amd import batch
+
+    for S in (1, 2, 3, 5, 4096 * 4 + 1, 4096 * 4 * 3 + 7, 100_003):
+        rng = np.random.default_rng(S * 131 + k)
+        lens = rng.integers(0, 300, size=S)
+        offs = np.r_[0, np.cumsum(lens)].astype(np.int64)
+        keys = oracle.splitmix_keys(S + k, int(offs[-1]))
+        want, wcnt = oracle.algo_r_segmented(5, 3, k, keys, offs)
+        out, cnt = batch.sample_segmented(torch.from_numpy(keys).to(cuda), torch.from_numpy(offs).to(cuda), k,
+                                          seed=5, stream_base=3)
+        assert np.array_equal(cnt.cpu().numpy(), wcnt), S
+        assert np.array_equal(out.cpu().numpy(), want), S
+
+
 _FIFO_CASE = """
 import sys
 import numpy as np
