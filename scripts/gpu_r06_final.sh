@@ -8,6 +8,7 @@ SQ="GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYC
 B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary"
 D=gpurun_out/$OUT
 exec scripts/gpu_run.sh $OUT \
+  suite 700 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread :: \
   smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" :: \
   bench20 300 python3 bench.py --steps 20 --warmup 5 :: \
   bench 600 python3 bench.py :: \
