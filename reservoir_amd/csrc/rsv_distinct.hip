@@ -1906,6 +1906,12 @@ struct DistinctState {
     int64_t fcap = 0;               // capacity (entries) of fk_in / fk_out / fv; fflag / pflag hold ord_cap
     int64_t pmem_cap = 0;
     int64_t first_min = 4096;       // segments at least this long replay through the flags (no host set)
+    // the next segment staged while the host runs this one (replay_log): its pinned copies
+    int64_t* ph2 = nullptr;
+    void* pk2 = nullptr;
+    uint8_t* pflag2 = nullptr;
+    int64_t ord2_cap = 0;
+    bool overlap = true;            // RSV_REPLAY_OVERLAP=0 (test hook): stage no segment ahead
     // Exact multi-rank merge of ordered samplers (rsv_export_log / rsv_merge_log): the candidates
     // the replica consumed (arrival order, host) + the segments still in the log, and the segments
     // logged before the last merge -- together every candidate logged since creation (`arch_ok`).
@@ -2059,6 +2065,7 @@ DistinctState* distinct_create(int32_t k, int key_width, int hash_kind, int64_t 
     if (const char* v = std::getenv("RSV_SCHED_BETA")) d->sched_beta = std::atof(v);
     if (const char* v = std::getenv("RSV_FIRST_MIN"))  // test hook: which replay form serves small segments
         d->first_min = std::max<int64_t>(1, std::atoll(v));
+    if (const char* v = std::getenv("RSV_REPLAY_OVERLAP")) d->overlap = v[0] != '0';  // test hook
     if (const char* v = std::getenv("RSV_SPEC_MIN_BATCH"))  // test hook: speculative publication
         d->spec_min = std::max<int64_t>(1, std::atoll(v));
     hipError_t e = hipSuccess;
@@ -2126,6 +2133,9 @@ void distinct_destroy(DistinctState* d) {
     pool_host_free(d->ph);
     pool_host_free(d->pk);
     pool_host_free(d->pflag);
+    pool_host_free(d->ph2);
+    pool_host_free(d->pk2);
+    pool_host_free(d->pflag2);
     pool_host_free(d->pmem);
     pool_host_free(d->shc);
     delete d;
@@ -2699,24 +2709,135 @@ static hipError_t rebuild_replica(DistinctState* d, hipStream_t st) {
     return hipSuccess;
 }
 
+// The next segment's host copies staged while the host replays this one (replay_log): segment gn in
+// arrival order into the pinned buffers the current run does not read, with first-occurrence flags
+// taken against the members at the START of the current segment gs plus all of gs's keys -- the
+// replica's members at gn's start are a subset of those, and a key of gs that is no member there
+// cannot be admitted at gn either (rejected at its first arrival, or evicted as the heap's maximum:
+// maxHash has not risen since, Sampler.scala:403), so the flags are exactly as exact as gn's own
+// would be.  gs's keys are still in ord_k (put there in arrival order for gs's own copies).  Enqueued
+// only: the caller synchronizes the stream before it reads the copies.
+template <typename KeyT>
+static hipError_t segment_stage_next(DistinctState* d, const DistinctState::Seg& gs, const DistinctState::Seg& gn,
+                                     int64_t* dph, void* dpk, uint8_t* dpflag, hipStream_t st) {
+    hipError_t e;
+    const int64_t nm = d->rep.size();  // the members at gs's start (gs has not been replayed yet)
+    const int64_t total = nm + gs.c + gn.c;
+    KeyT* pm = (KeyT*)d->pmem;  // free: the stream was synchronized since its last upload
+    for (int64_t i = 0; i < nm; ++i) pm[i] = (KeyT)d->rep.he[(size_t)i + 1];
+    if (nm && (e = hipMemcpyAsync(d->fk_in, pm, (size_t)nm * sizeof(KeyT), hipMemcpyHostToDevice, st))) return e;
+    if ((e = hipMemcpyAsync((KeyT*)d->fk_in + nm, d->ord_k, (size_t)gs.c * sizeof(KeyT), hipMemcpyDeviceToDevice, st)))
+        return e;
+    unsigned bits = 1;
+    while (bits < 32 && ((uint64_t)1 << bits) < (uint64_t)gn.m) ++bits;
+    size_t tb = d->temp_bytes;
+    if ((e = rocprim::radix_sort_pairs(d->temp, tb, d->log_i + gn.off, d->sorted_i,
+                                       rocprim::counting_iterator<uint32_t>(0), d->perm, (size_t)gn.c, 0, bits, st)))
+        return e;
+    hipLaunchKernelGGL(permute_log<KeyT>, dim3((unsigned)std::min<int64_t>((gn.c + kBlock - 1) / kBlock, 8192)),
+                       dim3(kBlock), 0, st, d->perm, d->log_h + gn.off, (const KeyT*)d->log_k + gn.off, gn.c, d->ord_h,
+                       (KeyT*)d->ord_k);
+    if ((e = hipGetLastError())) return e;
+    if ((e = hipMemcpyAsync((KeyT*)d->fk_in + nm + gs.c, d->ord_k, (size_t)gn.c * sizeof(KeyT), hipMemcpyDeviceToDevice,
+                            st)))
+        return e;
+    size_t fb = d->temp_bytes;
+    if ((e = rocprim::radix_sort_pairs(d->temp, fb, (KeyT*)d->fk_in, (KeyT*)d->fk_out,
+                                       rocprim::counting_iterator<uint32_t>(0), d->fv, (size_t)total, 0,
+                                       8 * (unsigned)sizeof(KeyT), st)))
+        return e;
+    hipLaunchKernelGGL(mark_first<KeyT>, dim3((unsigned)std::min<int64_t>((total + kBlock - 1) / kBlock, 8192)),
+                       dim3(kBlock), 0, st, (const KeyT*)d->fk_out, (const uint32_t*)d->fv, total,
+                       (uint32_t)(nm + gs.c), d->fflag);
+    if ((e = hipGetLastError())) return e;
+    if ((e = hipMemcpyAsync(dpflag, d->fflag, (size_t)gn.c, hipMemcpyDeviceToHost, st))) return e;
+    if ((e = hipMemcpyAsync(dph, d->ord_h, (size_t)gn.c * 8, hipMemcpyDeviceToHost, st))) return e;
+    return hipMemcpyAsync(dpk, d->ord_k, (size_t)gn.c * sizeof(KeyT), hipMemcpyDeviceToHost, st);
+}
+
+// the alternate pinned copies for segments of up to `cap` candidates
+static hipError_t ensure_ordered2(DistinctState* d, int64_t cap) {
+    if (cap <= d->ord2_cap) return hipSuccess;
+    hipError_t e;
+    pool_host_free(d->ph2);
+    pool_host_free(d->pk2);
+    pool_host_free(d->pflag2);
+    d->ph2 = nullptr;
+    d->pk2 = nullptr;
+    d->pflag2 = nullptr;
+    d->ord2_cap = 0;
+    if ((e = pool_host_alloc((void**)&d->ph2, (size_t)cap * 8, hipHostMallocDefault))) return e;
+    if ((e = pool_host_alloc(&d->pk2, (size_t)cap * d->kw, hipHostMallocDefault))) return e;
+    if ((e = pool_host_alloc((void**)&d->pflag2, (size_t)cap, hipHostMallocDefault))) return e;
+    d->ord2_cap = cap;
+    return hipSuccess;
+}
+
 // Every logged segment, in order, through the host replica (RandomValues.sample on each candidate,
 // Sampler.scala:394-409); the consumed candidates are kept in the host archive for rsv_export_log
-// when the sampler retains its log (rsv_retain_log).
+// when the sampler retains its log (rsv_retain_log).  When two consecutive segments both replay
+// through the first-occurrence flags, the next one's sort, flags and copies run on the device while
+// the host replays the current one (segment_stage_next; C4's hash-twin share: the second segment's
+// 0.76 ms to the host hidden under the first one's 2.4 ms heap run).
 template <typename KeyT>
 static hipError_t replay_log(DistinctState* d, hipStream_t st) {
     hipError_t e;
     if (d->rep_stale && (e = rebuild_replica<KeyT>(d, st))) return e;
-    for (const DistinctState::Seg& g : d->segs) {
-        if (g.c == 0) continue;
-        // (the flags' sort holds the members too: ~20 B per entry on the device, so a huge replica
-        // keeps the set-based form)
-        const bool first = g.c >= d->first_min && d->rep.size() + g.c <= ((int64_t)1 << 28);
+    // (the flags' sort holds the members too: ~20 B per entry on the device, so a huge replica
+    // keeps the set-based form)
+    auto first_ok = [&](int64_t c, int64_t extra) {
+        return c >= d->first_min && d->rep.size() + extra + c <= ((int64_t)1 << 28);
+    };
+    const size_t ns = d->segs.size();
+    if (d->overlap && ns >= 2) {  // every buffer at its final size first: a growth would drop ord_k
+        int64_t cmax = 0, pair = 0;
+        for (size_t s = 0; s < ns; ++s) {
+            cmax = std::max(cmax, d->segs[s].c);
+            if (s + 1 < ns) pair = std::max(pair, d->segs[s].c + d->segs[s + 1].c);
+        }
+        if ((e = ensure_ordered(d, cmax, st))) return e;
+        if ((e = ensure_first<KeyT>(d, d->k, d->k + pair, st))) return e;
+        if ((e = ensure_ordered2(d, cmax))) return e;
+    }
+    // the pinned copies of a segment: set 0 (ph / pk / pflag, segment_to_host's, which may grow them)
+    // or set 1 (ph2 / pk2 / pflag2)
+    auto set_h = [&](int c) { return c ? d->ph2 : d->ph; };
+    auto set_k = [&](int c) { return c ? d->pk2 : d->pk; };
+    auto set_f = [&](int c) { return c ? d->pflag2 : d->pflag; };
+    bool staged = false;  // segment s's copies (and flags) were staged behind the previous run
+    int cur = 0;          // the set segment s's copies are in
+    for (size_t s = 0; s < ns; ++s) {
+        const DistinctState::Seg& g = d->segs[s];
+        if (g.c == 0) {
+            staged = false;
+            continue;
+        }
         static const bool debug = std::getenv("RSV_REPLAY_DEBUG") != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
-        if ((e = segment_to_host<KeyT>(d, g, st, first))) return e;
+        bool first;
+        if (staged) {  // staged behind the previous segment's run: wait for its copies
+            if ((e = hipStreamSynchronize(st))) return e;
+            cur ^= 1;
+            first = true;
+        } else {
+            first = first_ok(g.c, 0);
+            if ((e = segment_to_host<KeyT>(d, g, st, first))) return e;
+            cur = 0;
+        }
+        staged = false;
+        if (d->overlap && first && s + 1 < ns && d->ph2) {
+            const DistinctState::Seg& gn = d->segs[s + 1];
+            const int64_t nm = d->rep.size();
+            if (gn.c > 0 && first_ok(gn.c, g.c) && nm + g.c + gn.c <= d->fcap && gn.c <= d->ord2_cap &&
+                gn.c <= d->ord_cap && d->pmem_cap >= nm) {
+                if ((e = segment_stage_next<KeyT>(d, g, gn, set_h(cur ^ 1), set_k(cur ^ 1), set_f(cur ^ 1), st))) return e;
+                staged = true;
+            }
+        }
         const auto t1 = std::chrono::steady_clock::now();
-        const KeyT* pk = (const KeyT*)d->pk;
-        const int64_t* ph = d->ph;
+        const KeyT* pk = (const KeyT*)set_k(cur);
+        const int64_t* ph = set_h(cur);
+        const uint8_t* pflag = set_f(cur);
         if (d->retain && d->arch_ok) {
             if ((int64_t)d->arch_h.size() + g.c > kArchMax) {
                 archive_drop(d);
@@ -2727,7 +2848,7 @@ static hipError_t replay_log(DistinctState* d, hipStream_t st) {
             }
         }
         if (first)
-            d->rep.sample_run_unique(g.c, d->pflag, [&](int64_t t) { return (int64_t)pk[t]; },
+            d->rep.sample_run_unique(g.c, pflag, [&](int64_t t) { return (int64_t)pk[t]; },
                                      [&](int64_t t) { return ph[t]; });
         else
             d->rep.sample_run(g.c, [&](int64_t t) { return (int64_t)pk[t]; }, [&](int64_t t) { return ph[t]; });
@@ -2735,13 +2856,14 @@ static hipError_t replay_log(DistinctState* d, hipStream_t st) {
             const auto t2 = std::chrono::steady_clock::now();
             int64_t kept = 0;
             if (first)
-                for (int64_t t = 0; t < g.c; ++t) kept += d->pflag[t];
-            std::fprintf(stderr, "[rsv replay] candidates=%lld first=%d kept=%lld to_host_us=%.1f run_us=%.1f\n",
-                         (long long)g.c, (int)first, (long long)kept,
+                for (int64_t t = 0; t < g.c; ++t) kept += pflag[t];
+            std::fprintf(stderr, "[rsv replay] candidates=%lld first=%d kept=%lld staged_next=%d to_host_us=%.1f run_us=%.1f\n",
+                         (long long)g.c, (int)first, (long long)kept, (int)staged,
                          std::chrono::duration<double, std::micro>(t1 - t0).count(),
                          std::chrono::duration<double, std::micro>(t2 - t1).count());
         }
     }
+    if (staged && (e = hipStreamSynchronize(st))) return e;  // (never: the last segment stages nothing)
     d->segs.clear();
     if (d->pre_segs.empty()) d->log_n = 0;  // else the log still holds the pre-merge segments
     return hipSuccess;

@@ -255,18 +255,22 @@ def test_ordered_eager_log_replay(cuda, oracle, monkeypatch):
         assert d.result().tolist() == want
 
 
-@pytest.mark.parametrize("first_min", ["1", "1000000000"])
-def test_ordered_first_occurrence_replay(cuda, oracle, monkeypatch, first_min):
+@pytest.mark.parametrize("first_min,overlap", [("1", "1"), ("1", "0"), ("1000000000", "1")])
+def test_ordered_first_occurrence_replay(cuda, oracle, monkeypatch, first_min, overlap):
     """The host replay of a logged segment either probes the member set per candidate or runs the
     heap alone over the device's first-occurrence flags (a key that repeats an earlier candidate of
     the segment or a member at its start can never be admitted).  RSV_FIRST_MIN (test hook, read at
     creation) picks the form for every segment; eager replays (RSV_ORDERED_LOG_LIMIT) and a reusable
-    sampler give many segments whose candidates repeat members and each other: the same set."""
+    sampler give many segments whose candidates repeat members and each other: the same set.
+    RSV_REPLAY_OVERLAP (test hook, read at creation): each next segment's flags and copies staged on
+    the device while the host replays the current one (flags against the members at the current
+    segment's start plus its keys) or not."""
     import torch
 
     from reservoir_amd import Sampler
 
     monkeypatch.setenv("RSV_FIRST_MIN", first_min)
+    monkeypatch.setenv("RSV_REPLAY_OVERLAP", overlap)
     rng = np.random.default_rng(21)
     base = _colliding(rng, 300_000, 2000)
     vals = np.concatenate([base, base[rng.integers(0, base.size, size=200_000)]])
