@@ -945,6 +945,13 @@ struct WideDistinct {
     double sched_beta = 1.6;      // bound margin over the predicted k-th smallest hash
     int64_t first_min = 4096;     // logs at least this long replay through first-occurrence flags
     bool sched_on = true;
+    // pinned host copies of the log for the replay (hashes, rows, first-occurrence flags), kept
+    // between replays: a fresh pageable vector per replay paid its page faults and zero fill, and
+    // pageable copies run at about half the DMA rate
+    int64_t* p_oh = nullptr;
+    uint64_t* p_ok = nullptr;
+    uint32_t* p_fl = nullptr;
+    int64_t p_cap = 0;
 };
 
 namespace {
@@ -1240,10 +1247,9 @@ hipError_t rebuild_replica(WideDistinct* d, hipStream_t st) {
 }
 
 // the log in arrival order on the host: sort by global index on the device, permute, copy back
-hipError_t log_to_host(WideDistinct* d, std::vector<int64_t>& oh, std::vector<uint64_t>& ok, hipStream_t st) {
+// into oh[n] / ok[n x words] (synchronized when `sync`)
+hipError_t log_to_host(WideDistinct* d, int64_t* oh, uint64_t* ok, hipStream_t st, bool sync = true) {
     const int64_t n = d->log_n;
-    oh.resize((size_t)n);
-    ok.resize((size_t)(n * d->words));
     if (!n) return hipSuccess;
     hipError_t e;
     if ((e = ensure_merge(d, n, st))) return e;
@@ -1256,15 +1262,40 @@ hipError_t log_to_host(WideDistinct* d, std::vector<int64_t>& oh, std::vector<ui
     hipLaunchKernelGGL(wide_log_permute, dim3(g), dim3(kWBlock), 0, st, d->ev1, d->log_h, d->log_k, n, d->words,
                        d->cand_h, d->cand_k);
     if ((e = hipGetLastError())) return e;
-    if ((e = hipMemcpyAsync(oh.data(), d->cand_h, (size_t)n * 8, hipMemcpyDeviceToHost, st))) return e;
-    if ((e = hipMemcpyAsync(ok.data(), d->cand_k, (size_t)n * d->words * 8, hipMemcpyDeviceToHost, st))) return e;
-    return hipStreamSynchronize(st);
+    if ((e = hipMemcpyAsync(oh, d->cand_h, (size_t)n * 8, hipMemcpyDeviceToHost, st))) return e;
+    if ((e = hipMemcpyAsync(ok, d->cand_k, (size_t)n * d->words * 8, hipMemcpyDeviceToHost, st))) return e;
+    return sync ? hipStreamSynchronize(st) : hipSuccess;
+}
+
+hipError_t log_to_host(WideDistinct* d, std::vector<int64_t>& oh, std::vector<uint64_t>& ok, hipStream_t st) {
+    oh.resize((size_t)d->log_n);
+    ok.resize((size_t)(d->log_n * d->words));
+    return log_to_host(d, oh.data(), ok.data(), st);
+}
+
+// the replay's pinned copies for a log of n entries
+hipError_t ensure_pinned_log(WideDistinct* d, int64_t n) {
+    if (n <= d->p_cap) return hipSuccess;
+    const int64_t c = std::max<int64_t>(n, 2 * d->p_cap);
+    pool_host_free(d->p_oh);
+    pool_host_free(d->p_ok);
+    pool_host_free(d->p_fl);
+    d->p_oh = nullptr;
+    d->p_ok = nullptr;
+    d->p_fl = nullptr;
+    d->p_cap = 0;
+    hipError_t e;
+    if ((e = pool_host_alloc((void**)&d->p_oh, (size_t)c * 8, hipHostMallocDefault))) return e;
+    if ((e = pool_host_alloc((void**)&d->p_ok, (size_t)c * d->words * 8, hipHostMallocDefault))) return e;
+    if ((e = pool_host_alloc((void**)&d->p_fl, (size_t)c * 4, hipHostMallocDefault))) return e;
+    d->p_cap = c;
+    return hipSuccess;
 }
 
 // First-occurrence flags of the log (already in arrival order in cand_h / cand_k, log_to_host):
 // entries [the replica's members | the log] through the merge's sort (stable radix by h, runs of
 // equal h stably by the key words, or the comparison sort for runs > kRunMax), then wide_mark_first.
-hipError_t first_flags(WideDistinct* d, std::vector<uint32_t>& flags, hipStream_t st) {
+hipError_t first_flags(WideDistinct* d, uint32_t* flags, hipStream_t st) {
     const int64_t n = d->log_n;
     std::vector<int64_t> mh;
     std::vector<uint64_t> mk;
@@ -1297,8 +1328,7 @@ hipError_t first_flags(WideDistinct* d, std::vector<uint32_t>& flags, hipStream_
     }
     hipLaunchKernelGGL(wide_mark_first, dim3(g), dim3(kWBlock), 0, st, d->eh1, d->ev1, N, R, d->pos);
     if ((e = hipGetLastError())) return e;
-    flags.resize((size_t)n);
-    if ((e = hipMemcpyAsync(flags.data(), d->pos, (size_t)n * 4, hipMemcpyDeviceToHost, st))) return e;
+    if ((e = hipMemcpyAsync(flags, d->pos, (size_t)n * 4, hipMemcpyDeviceToHost, st))) return e;
     return hipStreamSynchronize(st);
 }
 
@@ -1308,35 +1338,37 @@ hipError_t first_flags(WideDistinct* d, std::vector<uint32_t>& flags, hipStream_
 hipError_t replay_log(WideDistinct* d, hipStream_t st) {
     hipError_t e;
     if (d->rep_stale && (e = rebuild_replica(d, st))) return e;
-    std::vector<int64_t> oh;
-    std::vector<uint64_t> ok;
     const bool first = d->log_n > 0 && d->log_n >= d->first_min;
     const int64_t n_log = d->log_n;
     const auto t0 = std::chrono::steady_clock::now();
-    if ((e = log_to_host(d, oh, ok, st))) return e;
+    if ((e = ensure_pinned_log(d, n_log))) return e;
+    const int64_t* oh = d->p_oh;
+    const uint64_t* ok = d->p_ok;
+    // the log's copies are enqueued before the flags' sort (one wait for both when first)
+    if ((e = log_to_host(d, d->p_oh, d->p_ok, st, !first))) return e;
     const auto t1 = std::chrono::steady_clock::now();
     auto t2 = t1;
     if (first) {
-        std::vector<uint32_t> fl;
-        if ((e = first_flags(d, fl, st))) return e;
+        const uint32_t* fl = d->p_fl;
+        if ((e = first_flags(d, d->p_fl, st))) return e;
         t2 = std::chrono::steady_clock::now();
         // members name log entries during the run (no row moves per replacement), then take slots
-        for (size_t t = 0; t < oh.size(); ++t)
-            if (fl[t]) d->rep.sample_first_at(oh[t], (int64_t)t);
-        d->rep.adopt(ok.data());
+        for (int64_t t = 0; t < n_log; ++t)
+            if (fl[t]) d->rep.sample_first_at(oh[t], t);
+        d->rep.adopt(ok);
         d->rep.table_rebuild();
     } else {
-        for (size_t t = 0; t < oh.size(); ++t) d->rep.sample(oh[t], ok.data() + t * d->words);
+        for (int64_t t = 0; t < n_log; ++t) d->rep.sample(oh[t], ok + t * d->words);
     }
     const auto t3 = std::chrono::steady_clock::now();
     if (d->retain && d->arch_ok) {
-        if ((int64_t)(d->arch_h.size() + oh.size()) > ((int64_t)1 << 27)) {
+        if ((int64_t)d->arch_h.size() + n_log > ((int64_t)1 << 27)) {
             d->arch_ok = false;
             d->arch_h.clear();
             d->arch_k.clear();
         } else {
-            d->arch_h.insert(d->arch_h.end(), oh.begin(), oh.end());
-            d->arch_k.insert(d->arch_k.end(), ok.begin(), ok.end());
+            d->arch_h.insert(d->arch_h.end(), oh, oh + n_log);
+            d->arch_k.insert(d->arch_k.end(), ok, ok + n_log * d->words);
         }
     }
     d->log_n = 0;
@@ -1691,6 +1723,9 @@ void wide_destroy(WideDistinct* d) {
     for (void* p : wb) pool_device_free(p);
     pool_host_free(d->hsched);
     pool_host_free(d->hctl);
+    pool_host_free(d->p_oh);
+    pool_host_free(d->p_ok);
+    pool_host_free(d->p_fl);
     delete d;
 }
 
