@@ -1912,6 +1912,7 @@ struct DistinctState {
     uint8_t* pflag2 = nullptr;
     int64_t ord2_cap = 0;
     bool overlap = true;            // RSV_REPLAY_OVERLAP=0 (test hook): stage no segment ahead
+    hipEvent_t seg_ev = nullptr;    // a segment's own copies done (the next one's staging may still run)
     // Exact multi-rank merge of ordered samplers (rsv_export_log / rsv_merge_log): the candidates
     // the replica consumed (arrival order, host) + the segments still in the log, and the segments
     // logged before the last merge -- together every candidate logged since creation (`arch_ok`).
@@ -2136,6 +2137,7 @@ void distinct_destroy(DistinctState* d) {
     pool_host_free(d->ph2);
     pool_host_free(d->pk2);
     pool_host_free(d->pflag2);
+    if (d->seg_ev) (void)hipEventDestroy(d->seg_ev);
     pool_host_free(d->pmem);
     pool_host_free(d->shc);
     delete d;
@@ -2646,7 +2648,8 @@ static hipError_t ensure_first(DistinctState* d, int64_t nm, int64_t total, hipS
 // the host reads the segment sequentially (two random reads per element from a ~20 MB log cost
 // more than the replica's heap).  With `first`, also its first-occurrence flags into d->pflag.
 template <typename KeyT>
-static hipError_t segment_to_host(DistinctState* d, const DistinctState::Seg& g, hipStream_t st, bool first) {
+static hipError_t segment_to_host(DistinctState* d, const DistinctState::Seg& g, hipStream_t st, bool first,
+                                  bool sync = true) {
     hipError_t e;
     if ((e = ensure_ordered(d, g.c, st))) return e;
     unsigned bits = 1;
@@ -2680,7 +2683,10 @@ static hipError_t segment_to_host(DistinctState* d, const DistinctState::Seg& g,
     }
     if ((e = hipMemcpyAsync(d->ph, d->ord_h, (size_t)g.c * 8, hipMemcpyDeviceToHost, st))) return e;
     if ((e = hipMemcpyAsync(d->pk, d->ord_k, (size_t)g.c * sizeof(KeyT), hipMemcpyDeviceToHost, st))) return e;
-    return hipStreamSynchronize(st);
+    if (sync) return hipStreamSynchronize(st);
+    // the caller enqueues more (the next segment's staging), then waits for this event only
+    if (!d->seg_ev && (e = hipEventCreateWithFlags(&d->seg_ev, hipEventDisableTiming))) return e;
+    return hipEventRecord(d->seg_ev, st);
 }
 
 static void archive_drop(DistinctState* d) {
@@ -2762,6 +2768,7 @@ static hipError_t ensure_ordered2(DistinctState* d, int64_t cap) {
     pool_host_free(d->ph2);
     pool_host_free(d->pk2);
     pool_host_free(d->pflag2);
+    if (d->seg_ev) (void)hipEventDestroy(d->seg_ev);
     d->ph2 = nullptr;
     d->pk2 = nullptr;
     d->pflag2 = nullptr;
@@ -2814,25 +2821,29 @@ static hipError_t replay_log(DistinctState* d, hipStream_t st) {
         }
         static const bool debug = std::getenv("RSV_REPLAY_DEBUG") != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
-        bool first;
+        bool first = true;
         if (staged) {  // staged behind the previous segment's run: wait for its copies
             if ((e = hipStreamSynchronize(st))) return e;
             cur ^= 1;
-            first = true;
-        } else {
+        }
+        // the next segment is staged behind this one when both replay through the flags
+        const DistinctState::Seg* gn = s + 1 < ns ? &d->segs[s + 1] : nullptr;
+        const int64_t nm = d->rep.size();
+        const bool stage_next = d->overlap && d->ph2 && gn && gn->c > 0 && first_ok(gn->c, g.c) &&
+                                nm + g.c + gn->c <= d->fcap && gn->c <= d->ord2_cap && gn->c <= d->ord_cap &&
+                                d->pmem_cap >= nm;
+        if (!staged) {
             first = first_ok(g.c, 0);
-            if ((e = segment_to_host<KeyT>(d, g, st, first))) return e;
+            // (when staging follows, wait only for this segment's own copies, after enqueueing it)
+            if ((e = segment_to_host<KeyT>(d, g, st, first, !(stage_next && first)))) return e;
             cur = 0;
         }
+        const bool was_staged = staged;
         staged = false;
-        if (d->overlap && first && s + 1 < ns && d->ph2) {
-            const DistinctState::Seg& gn = d->segs[s + 1];
-            const int64_t nm = d->rep.size();
-            if (gn.c > 0 && first_ok(gn.c, g.c) && nm + g.c + gn.c <= d->fcap && gn.c <= d->ord2_cap &&
-                gn.c <= d->ord_cap && d->pmem_cap >= nm) {
-                if ((e = segment_stage_next<KeyT>(d, g, gn, set_h(cur ^ 1), set_k(cur ^ 1), set_f(cur ^ 1), st))) return e;
-                staged = true;
-            }
+        if (stage_next && first) {
+            if ((e = segment_stage_next<KeyT>(d, g, *gn, set_h(cur ^ 1), set_k(cur ^ 1), set_f(cur ^ 1), st))) return e;
+            staged = true;
+            if (!was_staged && (e = hipEventSynchronize(d->seg_ev))) return e;
         }
         const auto t1 = std::chrono::steady_clock::now();
         const KeyT* pk = (const KeyT*)set_k(cur);
